@@ -1,0 +1,290 @@
+"""bench.py -- FastDFS upload-path CRC32 + dedup-signature throughput on MI355X.
+
+Default workload (BASELINE.json configs[1], "config 2"): per GPU, a batch of
+1,000,000 files of U[4 KiB, 64 KiB] bytes (~34.8 GB) resident in HBM.  One
+step = the whole upload-path signature work for the batch
+(fdfs_gpu_sig_batch, FDFS_SIG_HASH: CRC32 + INIT/CALC/FINISH_HASH_CODES4 +
+STORAGE_GEN_FILE_SIGNATURE for every file) followed by the bulk dedup of the
+step's signatures across all ranks (bucket -> RCCL all-to-all -> group ->
+all-to-all back).  Weak scaling: every rank owns its own batch.
+
+Other workloads: --config c3 (MD5 method, 1-4 MiB files), c4 (1 GiB files,
+CRC-only segmented path), c5 (dedup only, 100M signatures, strong scaling).
+
+Prints ONE JSON line on rank 0 (contract in the task statement), with a
+"roofline" object for the dominant kernel (its duration measured by HIP
+events recorded inside libfdfs_gpu on the launch stream) and a
+"cpu_baseline" object (the C oracle of the reference loops on host cores).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+import fastdfs_amd as F  # noqa: E402
+from fastdfs_amd import _lib, corpus as C  # noqa: E402
+from fastdfs_amd.dist import dedup_global  # noqa: E402
+
+HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+VALU_PEAK_TOPS = 78.6  # 256 CU x 4 SIMD x 32 lanes x 2.4 GHz int32 lane-ops/s (1 op/lane/clk)
+
+METRIC = "GB/s CRC32+signature per node; dedup files/sec at 1/2/4/8 MI355X"
+
+
+def parse():
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=10)
+    p.add_argument("--warmup", type=int, default=3)
+    p.add_argument("--config", default="c2", choices=["c2", "c3", "c4", "c5"])
+    p.add_argument("--files", type=int, default=0, help="override files per GPU")
+    p.add_argument("--cpu-seconds", type=float, default=10.0)
+    p.add_argument("--cpu-threads", type=int, default=16)
+    p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--unsigned-hash", action="store_true")
+    return p.parse_args()
+
+
+def setup_dist(args):
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    if world != args.gpus and rank == 0:
+        print(f"warning: --gpus {args.gpus} but WORLD_SIZE {world}", file=sys.stderr)
+    return world, rank, local
+
+
+def barrier(world):
+    if world > 1:
+        dist.barrier()
+
+
+def max_over_ranks(x: float, world: int) -> float:
+    if world == 1:
+        return x
+    t = torch.tensor([x], dtype=torch.float64, device="cuda")
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
+
+
+def sum_over_ranks(x: float, world: int) -> float:
+    if world == 1:
+        return x
+    t = torch.tensor([x], dtype=torch.float64, device="cuda")
+    dist.all_reduce(t, op=dist.ReduceOp.SUM)
+    return float(t.item())
+
+
+def timed(fn, steps, warmup, world):
+    for _ in range(warmup):
+        fn()
+    torch.cuda.synchronize()
+    barrier(world)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        fn()
+    torch.cuda.synchronize()
+    barrier(world)
+    torch.cuda.synchronize()
+    return max_over_ranks(time.perf_counter() - t0, world)
+
+
+def dedup_step(ctx, sig, gidx, world):
+    if world > 1:
+        return dedup_global(ctx, sig, gidx)
+    return ctx.dedup(sig, gidx)
+
+
+def cpu_baseline(data, offs_np, sizes_np, method, variant, seconds, threads):
+    """The C oracle (restated reference loops, 256 KiB chunks as dio_write_file
+    gets them) on a bounded prefix of the same batch, `threads` host threads."""
+    from oracle import oracle as O
+    O.lib()
+
+    def run(k):
+        end = int(offs_np[k - 1] + sizes_np[k - 1])
+        host = data[:end].cpu().numpy()
+        t0 = time.perf_counter()
+        O.dio_batch(host, offs_np[:k], sizes_np[:k], method, variant, 256 * 1024, threads)
+        return time.perf_counter() - t0, int(sizes_np[:k].sum())
+
+    n = len(sizes_np)
+    k = min(n, max(threads * 4, 64))
+    dt, nb = run(k)
+    while dt < 0.5 and k < n:  # probe until the timing is meaningful
+        k = min(n, k * 4)
+        dt, nb = run(k)
+    rate = nb / dt
+    # size the measured sample to ~`seconds` of CPU work
+    want = rate * seconds
+    cum = np.cumsum(sizes_np)
+    k2 = int(min(n, max(k, np.searchsorted(cum, want) + 1)))
+    if k2 > k:
+        dt, nb = run(k2)
+        k = k2
+    return {"value": round(nb / dt / 1e9, 4), "unit": "GB/s", "cores": threads, "kind": "port",
+            "sample": f"first {k} files of the rank-0 batch ({nb / 1e9:.2f} GB), "
+                      f"oracle/fdfs_oracle.c orc_dio_batch, 256 KiB chunks, {threads} threads, "
+                      f"{dt:.1f} s", "cpu_model": cpu_model()}
+
+
+def cpu_model() -> str:
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+def load_traffic(config: str, kernel: str):
+    """HBM bytes per launch from a committed rocprofv3 --pmc pass (see
+    profiles/README.md), or None."""
+    path = os.path.join(ROOT, "profiles", f"pmc_{config}.json")
+    try:
+        d = json.load(open(path))
+        if d.get("kernel") == kernel:
+            return d.get("hbm_bytes_per_launch"), os.path.relpath(path, ROOT)
+    except (OSError, ValueError):
+        pass
+    return None, None
+
+
+def main():
+    args = parse()
+    world, rank, local = setup_dist(args)
+    dev = torch.device("cuda", local)
+    ctx = F.Context(local, unsigned_hash=args.unsigned_hash)
+    variant = 1 if args.unsigned_hash else 0
+    res = {"metric": METRIC, "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+           "higher_is_better": True, "vs_baseline": None, "dtype": "u8",
+           "data": "synthetic (seeded sizes, random bytes generated in HBM)"}
+
+    if args.config in ("c2", "c3", "c4"):
+        if args.config == "c2":
+            n = args.files or 1_000_000
+            sizes = C.small_files_sizes(n, seed=1 + 1000 * rank)
+            method, kernel, kname = F.SIG_HASH, _lib.KERNEL_SIG_LANE, "sig_lane_kernel<SAR,1>"
+            workload = ("config 2: 1M files/GPU of U[4,64] KiB, CRC32 + HASH_CODES4 signature "
+                        "+ bulk dedup per step")
+        elif args.config == "c3":
+            n = args.files or 24_000
+            sizes = C.photo_sizes(n, seed=3 + 1000 * rank)
+            method, kernel, kname = F.SIG_MD5, _lib.KERNEL_SIG_LANE, "sig_lane_kernel<SAR,2>"
+            workload = f"config 3: {n} files/GPU of U[1,4] MiB, CRC32 + MD5 signature + dedup"
+        else:
+            n = args.files or 8
+            sizes = np.full(n, 1 << 30, dtype=np.int64)
+            method, kernel, kname = F.SIG_CRC_ONLY, _lib.KERNEL_CRC_SEG, "crc_seg_kernel<SAR>"
+            workload = f"config 4: {n} x 1 GiB files/GPU, segmented CRC32 (64 KiB) + GF(2) combine"
+        data, offs_t, sizes_t = C.device_batch(sizes, seed=2 + 1000 * rank, device=dev)
+        nbytes = int(sizes.sum())
+        gidx = (torch.arange(n, device=dev, dtype=torch.int64) + rank * n)
+        ctx.reserve(n, n)
+
+        def step():
+            crc, sig, _ = ctx.sig_batch(data, offs_t, sizes_t, method=method)
+            if sig is not None:
+                dedup_step(ctx, sig, gidx, world)
+
+        for _ in range(args.warmup):
+            step()
+        torch.cuda.synchronize()
+        ctx.set_timing(True)
+        ctx.read_timing(kernel)
+        dt = timed(step, args.steps, 0, world)
+        kms, launches = ctx.read_timing(kernel)
+        ctx.set_timing(False)
+        total_bytes = sum_over_ranks(float(nbytes), world) * args.steps
+        res.update({"value": round(total_bytes / dt / 1e9, 3), "unit": "GB/s",
+                    "ms_per_step": round(dt / args.steps * 1e3, 3), "scaling": "weak",
+                    "files_per_s": round(sum_over_ranks(float(n), world) * args.steps / dt, 1)})
+        avg_ms = kms / max(launches, 1)
+        per_launch = float(nbytes)  # each file byte read once; 28 B/file of outputs on top
+        achieved = per_launch / (avg_ms * 1e-3) / 1e9
+        traffic, tsrc = load_traffic(args.config, kname)
+        res["roofline"] = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
+                           "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
+                           "traffic": traffic, "kernel": kname,
+                           "kernel_ms_avg": round(avg_ms, 4), "launches": launches,
+                           "algorithmic_bytes_per_launch": nbytes}
+        if tsrc:
+            res["roofline"]["traffic_source"] = tsrc
+        if method != F.SIG_CRC_ONLY:
+            # dedup-only throughput of the same signatures (files/s, all ranks)
+            _, sig, _ = ctx.sig_batch(data, offs_t, sizes_t, method=method)
+            ddt = timed(lambda: dedup_step(ctx, sig, gidx, world), args.steps, 1, world)
+            res["dedup_files_per_s"] = round(sum_over_ranks(float(n), world) * args.steps / ddt, 1)
+        cfg = {"workload": workload, "files_per_gpu": n, "bytes_per_gpu": nbytes,
+               "method": {0: "crc_only", 1: "hash", 2: "md5"}[method],
+               "crc_variant": "unsigned" if variant else "signed", "align": 16,
+               "parallelism": f"dp{world} (files sharded, dedup all-to-all)"}
+        res["config"] = cfg
+        if rank == 0 and world == 1 and not args.no_cpu_baseline:
+            res["cpu_baseline"] = cpu_baseline(data, C.layout(sizes)[0], sizes, method, variant,
+                                               args.cpu_seconds, args.cpu_threads)
+        else:
+            res["cpu_baseline"] = None
+    else:  # c5: dedup only, strong scaling over a fixed 100M-signature set
+        total = args.files or 100_000_000
+        per = total // world
+        g = torch.Generator(device=dev)
+        g.manual_seed(5)
+        # every rank derives the same global set; takes its contiguous share
+        nu = total - total // 10
+        uniq_idx = torch.randint(0, nu, (total - nu,), generator=g, device=dev)
+        lo, hi = rank * per, (rank + 1) * per if rank < world - 1 else total
+        idx = torch.arange(lo, hi, device=dev, dtype=torch.int64)
+        src = torch.where(idx < nu, idx, uniq_idx[(idx - nu).clamp(min=0, max=max(total - nu - 1, 0))])
+        # signature bytes = fixed mix of the unique id (deterministic, 16 random-looking bytes)
+        sig = torch.zeros((hi - lo, 24), dtype=torch.uint8, device=dev)
+        x = (src * (0x9E3779B97F4A7C15 - (1 << 64))) ^ 0x5DEECE66D
+        for k in range(2):
+            x = x ^ (x >> 31)
+            x = x * 0x7FB5D329728EA185
+            sig[:, 8 + 8 * k: 16 + 8 * k] = x.contiguous().view(torch.uint8).view(-1, 8)
+        sig[:, 5:8] = (src % 251).to(torch.uint8).view(-1, 1)
+        gidx = idx
+        ctx.reserve(0, 2 * (hi - lo))
+        ctx.set_timing(True)
+        dt = timed(lambda: dedup_step(ctx, sig, gidx, world), args.steps, args.warmup, world)
+        kms, launches = ctx.read_timing(_lib.KERNEL_DEDUP)
+        ctx.set_timing(False)
+        res.update({"metric": METRIC, "value": round(total * args.steps / dt, 1),
+                    "unit": "files/s", "ms_per_step": round(dt / args.steps * 1e3, 3),
+                    "scaling": "strong",
+                    "config": {"workload": "config 5: 100M-file dedup, 10% duplicates, "
+                                           "bucket + RCCL all-to-all + hash grouping",
+                               "records_total": total, "parallelism": f"dp{world}"}})
+        avg_ms = kms / max(launches, 1)
+        nb = (hi - lo) * 32.0  # sig read + rep/ref write per record (algorithmic)
+        res["roofline"] = {"bound": "hbm", "achieved": round(nb / (avg_ms * 1e-3) / 1e9, 1),
+                           "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                           "frac": round(nb / (avg_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+                           "traffic": None, "kernel": "dedup insert+emit",
+                           "kernel_ms_avg": round(avg_ms, 4)}
+        res["cpu_baseline"] = None
+    if rank == 0:
+        print(json.dumps(res), flush=True)
+    ctx.close()
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

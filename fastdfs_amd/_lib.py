@@ -1,0 +1,88 @@
+"""ctypes binding of libfdfs_gpu (include/fdfs_gpu.h).
+
+There is no fallback: if the gfx950 library is missing this module raises,
+and every compute entry point goes through the HIP kernels.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "lib", "libfdfs_gpu.so")
+HEADER_PATH = os.path.join(os.path.dirname(_HERE), "include", "fdfs_gpu.h")
+
+SIG_CRC_ONLY = 0
+SIG_HASH = 1
+SIG_MD5 = 2
+FLAG_UNSIGNED_HASH = 0x1
+FILE_SIGNATURE_SIZE = 24
+
+# Every entry point declared in include/fdfs_gpu.h.
+EXPORTS = (
+    "fdfs_gpu_abi_version",
+    "fdfs_gpu_open",
+    "fdfs_gpu_close",
+    "fdfs_gpu_reserve",
+    "fdfs_gpu_sig_batch",
+    "fdfs_gpu_dedup",
+    "fdfs_gpu_dedup_bucket",
+    "fdfs_gpu_dedup_group",
+    "fdfs_gpu_set_timing",
+    "fdfs_gpu_read_timing",
+    "fdfs_gpu_last_error",
+)
+KERNEL_SIG_LANE = 0
+KERNEL_CRC_SEG = 1
+KERNEL_DEDUP = 2
+KERNEL_BUCKET = 3
+
+
+class FdfsGpuBatch(ctypes.Structure):
+    _fields_ = [
+        ("base", ctypes.c_void_p),
+        ("offset", ctypes.c_void_p),
+        ("size", ctypes.c_void_p),
+        ("n", ctypes.c_uint32),
+    ]
+
+
+_lib = None
+
+
+def load() -> ctypes.CDLL:
+    """Load libfdfs_gpu.so; raises if it has not been built."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise RuntimeError(
+            f"libfdfs_gpu.so not found at {LIB_PATH}: build it with "
+            "`python -c 'import __graft_entry__ as g; g.build()'` (no CPU fallback exists)")
+    L = ctypes.CDLL(LIB_PATH)
+    vp, u64, u32, i32 = ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint32, ctypes.c_int
+    L.fdfs_gpu_abi_version.restype = i32
+    L.fdfs_gpu_abi_version.argtypes = []
+    L.fdfs_gpu_open.restype = i32
+    L.fdfs_gpu_open.argtypes = [i32, ctypes.c_uint, ctypes.POINTER(vp)]
+    L.fdfs_gpu_close.restype = i32
+    L.fdfs_gpu_close.argtypes = [vp]
+    L.fdfs_gpu_reserve.restype = i32
+    L.fdfs_gpu_reserve.argtypes = [vp, u64, u64]
+    L.fdfs_gpu_sig_batch.restype = i32
+    L.fdfs_gpu_sig_batch.argtypes = [vp, ctypes.POINTER(FdfsGpuBatch), i32, vp, vp, vp, vp]
+    L.fdfs_gpu_dedup.restype = i32
+    L.fdfs_gpu_dedup.argtypes = [vp, vp, vp, u64, vp, vp, vp]
+    L.fdfs_gpu_dedup_bucket.restype = i32
+    L.fdfs_gpu_dedup_bucket.argtypes = [vp, vp, vp, u64, u32, vp, vp, vp, vp]
+    L.fdfs_gpu_dedup_group.restype = i32
+    L.fdfs_gpu_dedup_group.argtypes = [vp, vp, u64, vp, vp, vp]
+    L.fdfs_gpu_set_timing.restype = i32
+    L.fdfs_gpu_set_timing.argtypes = [vp, i32]
+    L.fdfs_gpu_read_timing.restype = i32
+    L.fdfs_gpu_read_timing.argtypes = [vp, i32, ctypes.POINTER(ctypes.c_double),
+                                       ctypes.POINTER(ctypes.c_uint64)]
+    L.fdfs_gpu_last_error.restype = ctypes.c_char_p
+    L.fdfs_gpu_last_error.argtypes = [vp]
+    _lib = L
+    return L

@@ -1,0 +1,166 @@
+"""Host-side API over libfdfs_gpu for torch-resident batches.
+
+Mirrors the reference's call shape: one context per storage process /
+device (storage_write_to_file initialises, dio_write_file computes,
+storage_service_upload_file_done consumes), with the per-chunk CPU loops of
+storage/storage_dio.c:465-515 replaced by one batched GPU call.
+"""
+from __future__ import annotations
+
+import ctypes
+import errno
+import os
+
+import torch
+
+from . import _lib
+from ._lib import SIG_CRC_ONLY, SIG_HASH, SIG_MD5, FLAG_UNSIGNED_HASH  # noqa: F401
+
+
+class FdfsGpuError(RuntimeError):
+    def __init__(self, rc: int, where: str, detail: str = ""):
+        self.errno = rc
+        msg = f"{where} failed: {errno.errorcode.get(rc, rc)} ({os.strerror(rc)})"
+        if detail:
+            msg += f": {detail}"
+        super().__init__(msg)
+
+
+def _ptr(t: torch.Tensor | None) -> int | None:
+    return None if t is None else t.data_ptr()
+
+
+def _stream_handle(stream) -> int | None:
+    if stream is None:
+        stream = torch.cuda.current_stream()
+    return stream.cuda_stream or None
+
+
+def _check_dev(t: torch.Tensor, name: str, dtype=None):
+    if not t.is_cuda:
+        raise ValueError(f"{name} must be a device tensor (got {t.device}); no CPU path exists")
+    if not t.is_contiguous():
+        raise ValueError(f"{name} must be contiguous")
+    if dtype is not None and t.dtype != dtype:
+        raise ValueError(f"{name} must be {dtype}, got {t.dtype}")
+
+
+class Context:
+    """A libfdfs_gpu context on one HIP device.
+
+    unsigned_hash=False (default) is the signed-int CRC32_ex / ELFHash_ex
+    state libfastcommon declares; True selects logical shifts (zlib CRC).
+    """
+
+    def __init__(self, device: int | None = None, unsigned_hash: bool = False):
+        self._L = _lib.load()
+        if device is None:
+            device = torch.cuda.current_device()
+        self.device = int(device)
+        self.unsigned_hash = bool(unsigned_hash)
+        h = ctypes.c_void_p()
+        rc = self._L.fdfs_gpu_open(self.device, _lib.FLAG_UNSIGNED_HASH if unsigned_hash else 0,
+                                   ctypes.byref(h))
+        if rc:
+            raise FdfsGpuError(rc, "fdfs_gpu_open")
+        self._h = h
+
+    def close(self):
+        if getattr(self, "_h", None):
+            self._L.fdfs_gpu_close(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def _rc(self, rc: int, where: str):
+        if rc:
+            raise FdfsGpuError(rc, where, (self._L.fdfs_gpu_last_error(self._h) or b"").decode())
+
+    def set_timing(self, enable: bool = True):
+        self._rc(self._L.fdfs_gpu_set_timing(self._h, 1 if enable else 0), "fdfs_gpu_set_timing")
+
+    def read_timing(self, kernel: int) -> tuple[float, int]:
+        """(summed ms, launches) of `kernel` (KERNEL_* in _lib) since the last read."""
+        ms = ctypes.c_double()
+        cnt = ctypes.c_uint64()
+        self._rc(self._L.fdfs_gpu_read_timing(self._h, kernel, ctypes.byref(ms), ctypes.byref(cnt)),
+                 "fdfs_gpu_read_timing")
+        return ms.value, cnt.value
+
+    def reserve(self, max_files: int, max_records: int = 0):
+        self._rc(self._L.fdfs_gpu_reserve(self._h, max_files, max_records), "fdfs_gpu_reserve")
+
+    # ------------------------------------------------------------- signature
+    def sig_batch(self, data: torch.Tensor, offsets: torch.Tensor, sizes: torch.Tensor,
+                  method: int = SIG_HASH, crc_out: torch.Tensor | None = None,
+                  sig_out: torch.Tensor | None = None, codes_out: torch.Tensor | None = None,
+                  want_sig: bool = True, want_codes: bool = False, stream=None):
+        """CRC32 (+ 24-byte signature for SIG_HASH / SIG_MD5) of every file.
+
+        data: uint8 device tensor; offsets/sizes: int64 device tensors [n].
+        Returns (crc int32[n] holding the uint32 bit pattern, sig uint8[n,24]
+        or None, codes int32[n,4] or None).
+        """
+        _check_dev(data, "data", torch.uint8)
+        _check_dev(offsets, "offsets", torch.int64)
+        _check_dev(sizes, "sizes", torch.int64)
+        n = offsets.numel()
+        if sizes.numel() != n:
+            raise ValueError("offsets and sizes differ in length")
+        dev = data.device
+        if crc_out is None:
+            crc_out = torch.empty(n, dtype=torch.int32, device=dev)
+        if method != SIG_CRC_ONLY:
+            if sig_out is None and want_sig:
+                sig_out = torch.empty((n, 24), dtype=torch.uint8, device=dev)
+            if codes_out is None and want_codes:
+                codes_out = torch.empty((n, 4), dtype=torch.int32, device=dev)
+        else:
+            sig_out = codes_out = None
+        b = _lib.FdfsGpuBatch(data.data_ptr(), offsets.data_ptr(), sizes.data_ptr(), n)
+        self._rc(self._L.fdfs_gpu_sig_batch(self._h, ctypes.byref(b), method, crc_out.data_ptr(),
+                                            _ptr(sig_out), _ptr(codes_out), _stream_handle(stream)),
+                 "fdfs_gpu_sig_batch")
+        return crc_out, sig_out, codes_out
+
+    # ----------------------------------------------------------------- dedup
+    def dedup(self, sig: torch.Tensor, gidx: torch.Tensor | None = None, stream=None):
+        """rep int64[n] (first ingest index of the class), ref int32[n] (class size)."""
+        _check_dev(sig, "sig", torch.uint8)
+        n = sig.numel() // 24
+        if gidx is not None:
+            _check_dev(gidx, "gidx", torch.int64)
+        rep = torch.empty(n, dtype=torch.int64, device=sig.device)
+        ref = torch.empty(n, dtype=torch.int32, device=sig.device)
+        self._rc(self._L.fdfs_gpu_dedup(self._h, sig.data_ptr(), _ptr(gidx), n, rep.data_ptr(),
+                                        ref.data_ptr(), _stream_handle(stream)), "fdfs_gpu_dedup")
+        return rep, ref
+
+    def dedup_bucket(self, sig: torch.Tensor, gidx: torch.Tensor | None, nranks: int, stream=None):
+        """Pack {sig, gidx} rows by owner rank: (rows uint8[n,32], counts int64[nranks], row_of int64[n])."""
+        _check_dev(sig, "sig", torch.uint8)
+        n = sig.numel() // 24
+        if gidx is not None:
+            _check_dev(gidx, "gidx", torch.int64)
+        rows = torch.empty((n, 32), dtype=torch.uint8, device=sig.device)
+        counts = torch.empty(nranks, dtype=torch.int64, device=sig.device)
+        row_of = torch.empty(n, dtype=torch.int64, device=sig.device)
+        self._rc(self._L.fdfs_gpu_dedup_bucket(self._h, sig.data_ptr(), _ptr(gidx), n, nranks,
+                                               rows.data_ptr(), counts.data_ptr(), row_of.data_ptr(),
+                                               _stream_handle(stream)), "fdfs_gpu_dedup_bucket")
+        return rows, counts, row_of
+
+    def dedup_group(self, rows: torch.Tensor, stream=None):
+        """Owner-side grouping of 32-byte rows: (rep int64[m], ref int32[m])."""
+        _check_dev(rows, "rows", torch.uint8)
+        m = rows.numel() // 32
+        rep = torch.empty(m, dtype=torch.int64, device=rows.device)
+        ref = torch.empty(m, dtype=torch.int32, device=rows.device)
+        self._rc(self._L.fdfs_gpu_dedup_group(self._h, rows.data_ptr(), m, rep.data_ptr(),
+                                              ref.data_ptr(), _stream_handle(stream)),
+                 "fdfs_gpu_dedup_group")
+        return rep, ref

@@ -1,0 +1,377 @@
+// C ABI of libfdfs_gpu (include/fdfs_gpu.h): context, workspace and argument
+// checking around the kernels.  No CPU compute path exists: every result
+// comes from a gfx950 kernel, and a missing/failed device is an error.
+#include <hip/hip_runtime.h>
+
+#include <cerrno>
+#include <cstdio>
+#include <cstring>
+#include <new>
+#include <vector>
+
+#include "../../include/fdfs_gpu.h"
+#include "fdfs_device.hpp"
+#include "fdfs_kernels.hpp"
+
+struct fdfs_gpu_ctx {
+    int device = 0;
+    unsigned flags = 0;
+    bool sar = true;
+    fdfs::DevTables *d_tabs = nullptr;
+    unsigned seg_grid = 0;
+    void *ws = nullptr;
+    size_t ws_bytes = 0;
+    char err[256] = {0};
+    // kernel timing (fdfs_gpu_set_timing)
+    bool timing = false;
+    struct Rec {
+        hipEvent_t a, b;
+        int kernel;
+    };
+    std::vector<Rec> recs;
+    std::vector<hipEvent_t> pool;
+    double acc_ms[4] = {0, 0, 0, 0};
+    uint64_t acc_n[4] = {0, 0, 0, 0};
+};
+
+namespace {
+
+struct DeviceGuard {
+    int prev = -1;
+    bool ok = false;
+    explicit DeviceGuard(int dev)
+    {
+        if (hipGetDevice(&prev) != hipSuccess)
+            prev = -1;
+        ok = (prev == dev) || (hipSetDevice(dev) == hipSuccess);
+    }
+    ~DeviceGuard()
+    {
+        if (prev >= 0)
+            (void)hipSetDevice(prev);
+    }
+};
+
+int fail(fdfs_gpu_ctx *ctx, hipError_t e, const char *where)
+{
+    if (ctx)
+        std::snprintf(ctx->err, sizeof(ctx->err), "%s: %s", where, hipGetErrorString(e));
+    return EIO;
+}
+
+constexpr size_t kAlign = 256;
+size_t align_up(size_t x) { return (x + kAlign - 1) & ~(kAlign - 1); }
+
+// Bump allocator over the context workspace.
+struct Carve {
+    char *base;
+    size_t off = 0;
+    template <typename T>
+    T *take(size_t count)
+    {
+        T *p = reinterpret_cast<T *>(base + off);
+        off += align_up(count * sizeof(T));
+        return p;
+    }
+};
+
+size_t sig_ws_bytes(uint64_t n)
+{
+    size_t lane = align_up(sizeof(uint32_t) * 2 * fdfs::kSizeBins) + align_up(sizeof(uint32_t) * n);
+    size_t seg = align_up(sizeof(uint64_t) * n) + align_up(sizeof(uint64_t) * (n + 1)) +
+                 align_up(sizeof(uint64_t) * fdfs::scan_workspace_elems(n));
+    return lane > seg ? lane : seg;
+}
+
+size_t dedup_ws_bytes(uint64_t n)
+{
+    const uint64_t c = fdfs::dedup_table_slots(n);
+    return align_up(4 * c) + align_up(8 * c) + align_up(4 * c) + align_up(4 * n) + align_up(8 * 64);
+}
+
+int ensure_ws(fdfs_gpu_ctx *ctx, size_t bytes, hipStream_t st)
+{
+    if (bytes <= ctx->ws_bytes)
+        return 0;
+    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+    if (hipStreamIsCapturing(st, &cs) == hipSuccess && cs != hipStreamCaptureStatusNone) {
+        std::snprintf(ctx->err, sizeof(ctx->err),
+                      "workspace growth needed during stream capture; call fdfs_gpu_reserve first");
+        return ENOMEM;
+    }
+    if (ctx->ws) {
+        hipError_t e = hipStreamSynchronize(st);
+        if (e != hipSuccess)
+            return fail(ctx, e, "hipStreamSynchronize");
+        (void)hipFree(ctx->ws);
+        ctx->ws = nullptr;
+        ctx->ws_bytes = 0;
+    }
+    size_t sz = bytes + bytes / 4;
+    hipError_t e = hipMalloc(&ctx->ws, sz);
+    if (e != hipSuccess) {
+        std::snprintf(ctx->err, sizeof(ctx->err), "hipMalloc(%zu): %s", sz, hipGetErrorString(e));
+        return ENOMEM;
+    }
+    ctx->ws_bytes = sz;
+    return 0;
+}
+
+// Event pair for one main-kernel launch when timing is on, else nulls.
+void timing_pair(fdfs_gpu_ctx *ctx, int kernel, hipEvent_t &a, hipEvent_t &b)
+{
+    a = b = nullptr;
+    if (!ctx->timing)
+        return;
+    hipEvent_t ev[2] = {nullptr, nullptr};
+    for (auto &e : ev) {
+        if (!ctx->pool.empty()) {
+            e = ctx->pool.back();
+            ctx->pool.pop_back();
+        } else if (hipEventCreate(&e) != hipSuccess) {
+            e = nullptr;
+        }
+    }
+    if (!ev[0] || !ev[1]) {
+        for (auto e : ev)
+            if (e)
+                ctx->pool.push_back(e);
+        return;
+    }
+    a = ev[0];
+    b = ev[1];
+    ctx->recs.push_back({a, b, kernel});
+}
+
+}  // namespace
+
+extern "C" {
+
+int fdfs_gpu_abi_version(void) { return FDFS_GPU_ABI_VERSION; }
+
+int fdfs_gpu_open(int device, unsigned flags, fdfs_gpu_ctx **out)
+{
+    if (!out)
+        return EINVAL;
+    *out = nullptr;
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0 || device < 0 || device >= ndev)
+        return ENODEV;
+    fdfs_gpu_ctx *ctx = new (std::nothrow) fdfs_gpu_ctx;
+    if (!ctx)
+        return ENOMEM;
+    ctx->device = device;
+    ctx->flags = flags;
+    ctx->sar = (flags & FDFS_GPU_FLAG_UNSIGNED_HASH) == 0;
+    DeviceGuard g(device);
+    if (!g.ok) {
+        delete ctx;
+        return ENODEV;
+    }
+    auto *h = new (std::nothrow) fdfs::DevTables;
+    if (!h) {
+        delete ctx;
+        return ENOMEM;
+    }
+    if (!fdfs::build_crc_tables(h->t, ctx->sar)) {
+        delete h;
+        delete ctx;
+        return EINVAL;
+    }
+    for (int p = 0; p < 16; p++)
+        for (int x = 0; x < 256; x++)
+            h->Dc[p][x] = h->t.D[p][x ^ 0xFF];
+    hipError_t e = hipMalloc(&ctx->d_tabs, sizeof(fdfs::DevTables));
+    if (e == hipSuccess)
+        e = hipMemcpy(ctx->d_tabs, h, sizeof(fdfs::DevTables), hipMemcpyHostToDevice);
+    delete h;
+    if (e != hipSuccess) {
+        if (ctx->d_tabs)
+            (void)hipFree(ctx->d_tabs);
+        delete ctx;
+        return EIO;
+    }
+    hipDeviceProp_t prop;
+    int ncu = 256;
+    if (hipGetDeviceProperties(&prop, device) == hipSuccess && prop.multiProcessorCount > 0)
+        ncu = prop.multiProcessorCount;
+    ctx->seg_grid = (unsigned)(ncu * fdfs::crc_seg_blocks_per_cu());
+    *out = ctx;
+    return 0;
+}
+
+int fdfs_gpu_close(fdfs_gpu_ctx *ctx)
+{
+    if (!ctx)
+        return EINVAL;
+    DeviceGuard g(ctx->device);
+    (void)hipDeviceSynchronize();
+    if (ctx->ws)
+        (void)hipFree(ctx->ws);
+    for (auto &r : ctx->recs) {
+        (void)hipEventDestroy(r.a);
+        (void)hipEventDestroy(r.b);
+    }
+    for (auto e : ctx->pool)
+        (void)hipEventDestroy(e);
+    if (ctx->d_tabs)
+        (void)hipFree(ctx->d_tabs);
+    delete ctx;
+    return 0;
+}
+
+int fdfs_gpu_reserve(fdfs_gpu_ctx *ctx, uint64_t max_files, uint64_t max_records)
+{
+    if (!ctx)
+        return EINVAL;
+    DeviceGuard g(ctx->device);
+    size_t a = sig_ws_bytes(max_files), b = dedup_ws_bytes(max_records);
+    return ensure_ws(ctx, a > b ? a : b, nullptr);
+}
+
+const char *fdfs_gpu_last_error(fdfs_gpu_ctx *ctx) { return ctx ? ctx->err : "null context"; }
+
+int fdfs_gpu_set_timing(fdfs_gpu_ctx *ctx, int enable)
+{
+    if (!ctx)
+        return EINVAL;
+    ctx->timing = enable != 0;
+    return 0;
+}
+
+int fdfs_gpu_read_timing(fdfs_gpu_ctx *ctx, int kernel, double *ms_out, uint64_t *launches_out)
+{
+    if (!ctx || kernel < 0 || kernel > 3)
+        return EINVAL;
+    DeviceGuard g(ctx->device);
+    for (auto &r : ctx->recs) {
+        float ms = 0.f;
+        hipError_t e = hipEventSynchronize(r.b);
+        if (e == hipSuccess)
+            e = hipEventElapsedTime(&ms, r.a, r.b);
+        if (e != hipSuccess)
+            return fail(ctx, e, "fdfs_gpu_read_timing");
+        ctx->acc_ms[r.kernel] += ms;
+        ctx->acc_n[r.kernel] += 1;
+        ctx->pool.push_back(r.a);
+        ctx->pool.push_back(r.b);
+    }
+    ctx->recs.clear();
+    if (ms_out)
+        *ms_out = ctx->acc_ms[kernel];
+    if (launches_out)
+        *launches_out = ctx->acc_n[kernel];
+    ctx->acc_ms[kernel] = 0;
+    ctx->acc_n[kernel] = 0;
+    return 0;
+}
+
+int fdfs_gpu_sig_batch(fdfs_gpu_ctx *ctx, const fdfs_gpu_batch *batch, int method,
+                       uint32_t *crc_out, uint8_t *sig_out, int32_t *codes_out, void *stream)
+{
+    if (!ctx || !batch)
+        return EINVAL;
+    if (method != FDFS_SIG_CRC_ONLY && method != FDFS_SIG_HASH && method != FDFS_SIG_MD5)
+        return EINVAL;
+    const uint32_t n = batch->n;
+    if (n == 0)
+        return 0;
+    if (!batch->base || !batch->offset || !batch->size || !crc_out)
+        return EINVAL;
+    DeviceGuard g(ctx->device);
+    if (!g.ok)
+        return ENODEV;
+    hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+    int rc = ensure_ws(ctx, sig_ws_bytes(n), st);
+    if (rc)
+        return rc;
+    Carve cv{static_cast<char *>(ctx->ws)};
+    const uint8_t *base = static_cast<const uint8_t *>(batch->base);
+    hipError_t e;
+    if (method == FDFS_SIG_CRC_ONLY) {
+        uint64_t *nseg = cv.take<uint64_t>(n);
+        uint64_t *first = cv.take<uint64_t>((size_t)n + 1);
+        uint64_t *bsum = cv.take<uint64_t>(fdfs::scan_workspace_elems(n));
+        hipEvent_t a, b;
+        timing_pair(ctx, FDFS_KERNEL_CRC_SEG, a, b);
+        e = fdfs::launch_crc_seg(ctx->sar, base, batch->offset, batch->size, n, nseg, first, bsum,
+                                 ctx->d_tabs, crc_out, ctx->seg_grid, st, a, b);
+    } else {
+        uint32_t *hist = cv.take<uint32_t>(2 * fdfs::kSizeBins);
+        uint32_t *order = cv.take<uint32_t>(n);
+        hipEvent_t a, b;
+        timing_pair(ctx, FDFS_KERNEL_SIG_LANE, a, b);
+        e = fdfs::launch_sig_lane(ctx->sar, method, base, batch->offset, batch->size, n, hist,
+                                  order, ctx->d_tabs, crc_out, sig_out, codes_out, st, a, b);
+    }
+    return e == hipSuccess ? 0 : fail(ctx, e, "sig_batch launch");
+}
+
+static int dedup_common(fdfs_gpu_ctx *ctx, const uint8_t *sig, uint32_t stride,
+                        const uint64_t *gidx, uint32_t gstride, uint64_t n, uint64_t *rep_out,
+                        uint32_t *ref_out, void *stream)
+{
+    if (!ctx)
+        return EINVAL;
+    if (n == 0)
+        return 0;
+    if (!sig || !rep_out || !ref_out || n >= 0xFFFFFFFFull)
+        return EINVAL;
+    DeviceGuard g(ctx->device);
+    if (!g.ok)
+        return ENODEV;
+    hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+    int rc = ensure_ws(ctx, dedup_ws_bytes(n), st);
+    if (rc)
+        return rc;
+    const uint64_t c = fdfs::dedup_table_slots(n);
+    Carve cv{static_cast<char *>(ctx->ws)};
+    uint32_t *slots = cv.take<uint32_t>(c);
+    uint64_t *minidx = cv.take<uint64_t>(c);
+    uint32_t *count = cv.take<uint32_t>(c);
+    uint32_t *slot_of = cv.take<uint32_t>(n);
+    hipEvent_t a, b;
+    timing_pair(ctx, FDFS_KERNEL_DEDUP, a, b);
+    hipError_t e = fdfs::launch_dedup_group(sig, stride, gidx, gstride, n, slots, minidx, count,
+                                            slot_of, c, rep_out, ref_out, st, a, b);
+    return e == hipSuccess ? 0 : fail(ctx, e, "dedup launch");
+}
+
+int fdfs_gpu_dedup(fdfs_gpu_ctx *ctx, const uint8_t *sig, const uint64_t *gidx, uint64_t n,
+                   uint64_t *rep_out, uint32_t *ref_out, void *stream)
+{
+    return dedup_common(ctx, sig, 24, gidx, gidx ? 1 : 0, n, rep_out, ref_out, stream);
+}
+
+int fdfs_gpu_dedup_group(fdfs_gpu_ctx *ctx, const uint8_t *records, uint64_t n, uint64_t *rep_out,
+                         uint32_t *ref_out, void *stream)
+{
+    // rows {sig[24], gidx}: gidx is the 4th uint64 of each 32-byte row
+    return dedup_common(ctx, records, 32, records ? reinterpret_cast<const uint64_t *>(records + 24) : nullptr,
+                        4, n, rep_out, ref_out, stream);
+}
+
+int fdfs_gpu_dedup_bucket(fdfs_gpu_ctx *ctx, const uint8_t *sig, const uint64_t *gidx, uint64_t n,
+                          uint32_t nranks, uint8_t *records_out, uint64_t *counts_out,
+                          uint64_t *row_of_out, void *stream)
+{
+    if (!ctx || nranks == 0 || nranks > 64 || !counts_out)
+        return EINVAL;
+    if (n && (!sig || !records_out))
+        return EINVAL;
+    DeviceGuard g(ctx->device);
+    if (!g.ok)
+        return ENODEV;
+    hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+    int rc = ensure_ws(ctx, align_up(8 * 64), st);
+    if (rc)
+        return rc;
+    uint64_t *cursor = static_cast<uint64_t *>(ctx->ws);
+    hipEvent_t a, b;
+    timing_pair(ctx, FDFS_KERNEL_BUCKET, a, b);
+    hipError_t e = fdfs::launch_dedup_bucket(sig, gidx, n, nranks, records_out, counts_out, cursor,
+                                             row_of_out, st, a, b);
+    return e == hipSuccess ? 0 : fail(ctx, e, "dedup_bucket launch");
+}
+
+}  // extern "C"

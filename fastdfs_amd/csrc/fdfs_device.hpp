@@ -1,0 +1,90 @@
+// Device-side building blocks shared by the libfdfs_gpu kernels (gfx950).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <cstdint>
+
+#include "fdfs_tables.hpp"
+
+namespace fdfs {
+
+// Device copy of the tables: CrcTables plus the complemented slice tables
+// used by the segmented kernel for the signed variant (see crc_seg_kernel).
+struct DevTables {
+    CrcTables t;
+    uint32_t Dc[16][256];   // Dc[p][x] = D[p][x ^ 0xFF]
+};
+
+constexpr int kWave = 64;
+
+__device__ __forceinline__ uint32_t shr8(uint32_t c, bool sar)
+{
+    return sar ? (uint32_t)((int32_t)c >> 8) : (c >> 8);
+}
+
+// One CRC32_ex byte step (storage/storage_dio.c:467) from an LDS table.
+template <bool SAR>
+__device__ __forceinline__ uint32_t crc_byte(const uint32_t *__restrict__ T, uint32_t c, uint32_t b)
+{
+    return T[(c ^ b) & 0xFFu] ^ shr8(c, SAR);
+}
+
+// 16 bytes (LE words w) chained onto state c with slice-by-16 tables D
+// (LDS, [16][256]).  SAR adds the sign term the arithmetic shift leaves.
+template <bool SAR>
+__device__ __forceinline__ uint32_t chain16(const uint32_t *__restrict__ D, uint32_t c, uint4 w,
+                                            uint32_t K16)
+{
+    const uint32_t x = c ^ w.x;
+    uint32_t r0 = D[0 * 256 + (x & 0xFFu)] ^ D[1 * 256 + ((x >> 8) & 0xFFu)];
+    uint32_t r1 = D[2 * 256 + ((x >> 16) & 0xFFu)] ^ D[3 * 256 + (x >> 24)];
+    uint32_t r2 = D[4 * 256 + (w.y & 0xFFu)] ^ D[5 * 256 + ((w.y >> 8) & 0xFFu)];
+    uint32_t r3 = D[6 * 256 + ((w.y >> 16) & 0xFFu)] ^ D[7 * 256 + (w.y >> 24)];
+    r0 ^= D[8 * 256 + (w.z & 0xFFu)] ^ D[9 * 256 + ((w.z >> 8) & 0xFFu)];
+    r1 ^= D[10 * 256 + ((w.z >> 16) & 0xFFu)] ^ D[11 * 256 + (w.z >> 24)];
+    r2 ^= D[12 * 256 + (w.w & 0xFFu)] ^ D[13 * 256 + ((w.w >> 8) & 0xFFu)];
+    r3 ^= D[14 * 256 + ((w.w >> 16) & 0xFFu)] ^ D[15 * 256 + (w.w >> 24)];
+    uint32_t r = (r0 ^ r1) ^ (r2 ^ r3);
+    if (SAR)
+        r ^= (uint32_t)((int32_t)c >> 31) & K16;
+    return r;
+}
+
+// Linear map given as 4 byte tables (LDS, [4][256]).
+__device__ __forceinline__ uint32_t apply4(const uint32_t *__restrict__ A, uint32_t v)
+{
+    return (A[v & 0xFFu] ^ A[256 + ((v >> 8) & 0xFFu)]) ^
+           (A[512 + ((v >> 16) & 0xFFu)] ^ A[768 + (v >> 24)]);
+}
+
+// ELFHash_ex / simple_hash_ex / Time33Hash_ex byte steps (the h[1..3] of
+// CALC_HASH_CODES4, storage/storage_dio.c:475).
+template <bool SAR>
+__device__ __forceinline__ void h3_byte(uint32_t b, uint32_t &e, uint32_t &s, uint32_t &t)
+{
+    e = (e << 4) + b;
+    const uint32_t x = e & 0xF0000000u;
+    e ^= SAR ? (uint32_t)((int32_t)x >> 24) : (x >> 24);
+    e &= ~x;
+    s = (s << 5) - s + b;
+    t = (t << 5) + t + b;
+}
+
+template <bool SAR>
+__device__ __forceinline__ void h3_word(uint32_t w, uint32_t &e, uint32_t &s, uint32_t &t)
+{
+    h3_byte<SAR>(w & 0xFFu, e, s, t);
+    h3_byte<SAR>((w >> 8) & 0xFFu, e, s, t);
+    h3_byte<SAR>((w >> 16) & 0xFFu, e, s, t);
+    h3_byte<SAR>(w >> 24, e, s, t);
+}
+
+__device__ __forceinline__ uint32_t bswap32(uint32_t v) { return __builtin_bswap32(v); }
+
+// Cooperative global -> LDS copy of `ndw` dwords.
+__device__ __forceinline__ void lds_fill(uint32_t *dst, const uint32_t *__restrict__ src, int ndw)
+{
+    for (int i = threadIdx.x; i < ndw; i += blockDim.x)
+        dst[i] = src[i];
+}
+
+}  // namespace fdfs

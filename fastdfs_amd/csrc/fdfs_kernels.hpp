@@ -1,0 +1,39 @@
+// Launcher declarations shared between the kernel TUs and the C-ABI layer.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <cstdint>
+
+namespace fdfs {
+
+struct DevTables;
+
+constexpr uint64_t kSegBytes = 64 * 1024;  // CRC segment owned by one wave
+constexpr int kSizeBins = 2048;            // size bins of the lane-path counting sort
+
+// signature path (fdfs_sig.hip)
+uint64_t scan_workspace_elems(uint64_t n);
+hipError_t launch_exclusive_scan(const uint64_t *in, uint64_t n, uint64_t *out, uint64_t *bsum,
+                                 hipStream_t st);
+hipError_t launch_sig_lane(bool sar, int method, const uint8_t *base, const uint64_t *offs,
+                           const uint64_t *sizes, uint32_t n, uint32_t *hist, uint32_t *order,
+                           const DevTables *tabs, uint32_t *crc_out, uint8_t *sig_out,
+                           int32_t *codes_out, hipStream_t st, hipEvent_t ev0, hipEvent_t ev1);
+hipError_t launch_crc_seg(bool sar, const uint8_t *base, const uint64_t *offs, const uint64_t *sizes,
+                          uint32_t n, uint64_t *nseg, uint64_t *seg_first, uint64_t *bsum,
+                          const DevTables *tabs, uint32_t *crc_out, unsigned grid, hipStream_t st,
+                          hipEvent_t ev0, hipEvent_t ev1);
+int crc_seg_blocks_per_cu();
+
+// dedup path (fdfs_dedup.hip)
+uint64_t dedup_table_slots(uint64_t n);
+hipError_t launch_dedup_group(const uint8_t *sig, uint32_t sig_stride, const uint64_t *gidx,
+                              uint32_t gidx_stride, uint64_t n, uint32_t *slots, uint64_t *minidx,
+                              uint32_t *count, uint32_t *slot_of, uint64_t nslots,
+                              uint64_t *rep_out, uint32_t *ref_out, hipStream_t st, hipEvent_t ev0,
+                              hipEvent_t ev1);
+hipError_t launch_dedup_bucket(const uint8_t *sig, const uint64_t *gidx, uint64_t n,
+                               uint32_t nranks, uint8_t *records_out, uint64_t *counts_out,
+                               uint64_t *cursor, uint64_t *row_of_out, hipStream_t st,
+                               hipEvent_t ev0, hipEvent_t ev1);
+
+}  // namespace fdfs

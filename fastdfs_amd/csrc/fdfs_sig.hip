@@ -1,0 +1,696 @@
+// libfdfs_gpu signature kernels (gfx950).
+//
+//  * sig_lane_kernel<SAR, METHOD>: one LANE per file (files size-sorted so a
+//    wave's 64 files have near-equal length).  Computes CRC32 + the 4-way
+//    hash codes (METHOD 1) or CRC32 + MD5 (METHOD 2) in one pass over the
+//    file and writes crc, the 24-byte signature and the raw codes.  ELFHash
+//    and MD5 are sequential per file, so a lane per file is the only
+//    decomposition that keeps them exact.
+//  * crc_seg_kernel<SAR>: CRC32 only (the default upload path), one WAVE per
+//    64 KiB segment of a file, coalesced 4 KiB strides, slice-by-16 tables in
+//    LDS, a 6-level GF(2) combine across the wave, and a GF(2) matrix-power
+//    advance to combine segments of large files.
+//  * planning kernels: size-bin counting sort (lane path), per-file segment
+//    counts + exclusive scan (segment path).
+//
+// Reference call sites replaced: storage/storage_dio.c:465-515 (CRC32_ex,
+// CALC_HASH_CODES4, my_md5_update, *_FINAL) and
+// storage/storage_service.c:106-120 (STORAGE_GEN_FILE_SIGNATURE).
+#include "fdfs_device.hpp"
+#include "fdfs_kernels.hpp"
+
+namespace fdfs {
+
+// ----------------------------------------------------------------- MD5 core
+
+__device__ __forceinline__ uint32_t rotl(uint32_t x, int s)
+{
+    return __builtin_amdgcn_alignbit(x, x, 32 - s);
+}
+
+#define MD5_F(b, c, d) ((d) ^ ((b) & ((c) ^ (d))))
+#define MD5_G(b, c, d) ((c) ^ ((d) & ((b) ^ (c))))
+#define MD5_H(b, c, d) ((b) ^ (c) ^ (d))
+#define MD5_I(b, c, d) ((c) ^ ((b) | ~(d)))
+#define MD5_STEP(FN, a, b, c, d, m, k, s) a = (b) + rotl((a) + FN(b, c, d) + (m) + (k), s)
+
+__device__ __forceinline__ void md5_compress(uint32_t st[4], const uint32_t m[16])
+{
+    uint32_t a = st[0], b = st[1], c = st[2], d = st[3];
+    MD5_STEP(MD5_F, a, b, c, d, m[0], 0xd76aa478u, 7);
+    MD5_STEP(MD5_F, d, a, b, c, m[1], 0xe8c7b756u, 12);
+    MD5_STEP(MD5_F, c, d, a, b, m[2], 0x242070dbu, 17);
+    MD5_STEP(MD5_F, b, c, d, a, m[3], 0xc1bdceeeu, 22);
+    MD5_STEP(MD5_F, a, b, c, d, m[4], 0xf57c0fafu, 7);
+    MD5_STEP(MD5_F, d, a, b, c, m[5], 0x4787c62au, 12);
+    MD5_STEP(MD5_F, c, d, a, b, m[6], 0xa8304613u, 17);
+    MD5_STEP(MD5_F, b, c, d, a, m[7], 0xfd469501u, 22);
+    MD5_STEP(MD5_F, a, b, c, d, m[8], 0x698098d8u, 7);
+    MD5_STEP(MD5_F, d, a, b, c, m[9], 0x8b44f7afu, 12);
+    MD5_STEP(MD5_F, c, d, a, b, m[10], 0xffff5bb1u, 17);
+    MD5_STEP(MD5_F, b, c, d, a, m[11], 0x895cd7beu, 22);
+    MD5_STEP(MD5_F, a, b, c, d, m[12], 0x6b901122u, 7);
+    MD5_STEP(MD5_F, d, a, b, c, m[13], 0xfd987193u, 12);
+    MD5_STEP(MD5_F, c, d, a, b, m[14], 0xa679438eu, 17);
+    MD5_STEP(MD5_F, b, c, d, a, m[15], 0x49b40821u, 22);
+
+    MD5_STEP(MD5_G, a, b, c, d, m[1], 0xf61e2562u, 5);
+    MD5_STEP(MD5_G, d, a, b, c, m[6], 0xc040b340u, 9);
+    MD5_STEP(MD5_G, c, d, a, b, m[11], 0x265e5a51u, 14);
+    MD5_STEP(MD5_G, b, c, d, a, m[0], 0xe9b6c7aau, 20);
+    MD5_STEP(MD5_G, a, b, c, d, m[5], 0xd62f105du, 5);
+    MD5_STEP(MD5_G, d, a, b, c, m[10], 0x02441453u, 9);
+    MD5_STEP(MD5_G, c, d, a, b, m[15], 0xd8a1e681u, 14);
+    MD5_STEP(MD5_G, b, c, d, a, m[4], 0xe7d3fbc8u, 20);
+    MD5_STEP(MD5_G, a, b, c, d, m[9], 0x21e1cde6u, 5);
+    MD5_STEP(MD5_G, d, a, b, c, m[14], 0xc33707d6u, 9);
+    MD5_STEP(MD5_G, c, d, a, b, m[3], 0xf4d50d87u, 14);
+    MD5_STEP(MD5_G, b, c, d, a, m[8], 0x455a14edu, 20);
+    MD5_STEP(MD5_G, a, b, c, d, m[13], 0xa9e3e905u, 5);
+    MD5_STEP(MD5_G, d, a, b, c, m[2], 0xfcefa3f8u, 9);
+    MD5_STEP(MD5_G, c, d, a, b, m[7], 0x676f02d9u, 14);
+    MD5_STEP(MD5_G, b, c, d, a, m[12], 0x8d2a4c8au, 20);
+
+    MD5_STEP(MD5_H, a, b, c, d, m[5], 0xfffa3942u, 4);
+    MD5_STEP(MD5_H, d, a, b, c, m[8], 0x8771f681u, 11);
+    MD5_STEP(MD5_H, c, d, a, b, m[11], 0x6d9d6122u, 16);
+    MD5_STEP(MD5_H, b, c, d, a, m[14], 0xfde5380cu, 23);
+    MD5_STEP(MD5_H, a, b, c, d, m[1], 0xa4beea44u, 4);
+    MD5_STEP(MD5_H, d, a, b, c, m[4], 0x4bdecfa9u, 11);
+    MD5_STEP(MD5_H, c, d, a, b, m[7], 0xf6bb4b60u, 16);
+    MD5_STEP(MD5_H, b, c, d, a, m[10], 0xbebfbc70u, 23);
+    MD5_STEP(MD5_H, a, b, c, d, m[13], 0x289b7ec6u, 4);
+    MD5_STEP(MD5_H, d, a, b, c, m[0], 0xeaa127fau, 11);
+    MD5_STEP(MD5_H, c, d, a, b, m[3], 0xd4ef3085u, 16);
+    MD5_STEP(MD5_H, b, c, d, a, m[6], 0x04881d05u, 23);
+    MD5_STEP(MD5_H, a, b, c, d, m[9], 0xd9d4d039u, 4);
+    MD5_STEP(MD5_H, d, a, b, c, m[12], 0xe6db99e5u, 11);
+    MD5_STEP(MD5_H, c, d, a, b, m[15], 0x1fa27cf8u, 16);
+    MD5_STEP(MD5_H, b, c, d, a, m[2], 0xc4ac5665u, 23);
+
+    MD5_STEP(MD5_I, a, b, c, d, m[0], 0xf4292244u, 6);
+    MD5_STEP(MD5_I, d, a, b, c, m[7], 0x432aff97u, 10);
+    MD5_STEP(MD5_I, c, d, a, b, m[14], 0xab9423a7u, 15);
+    MD5_STEP(MD5_I, b, c, d, a, m[5], 0xfc93a039u, 21);
+    MD5_STEP(MD5_I, a, b, c, d, m[12], 0x655b59c3u, 6);
+    MD5_STEP(MD5_I, d, a, b, c, m[3], 0x8f0ccc92u, 10);
+    MD5_STEP(MD5_I, c, d, a, b, m[10], 0xffeff47du, 15);
+    MD5_STEP(MD5_I, b, c, d, a, m[1], 0x85845dd1u, 21);
+    MD5_STEP(MD5_I, a, b, c, d, m[8], 0x6fa87e4fu, 6);
+    MD5_STEP(MD5_I, d, a, b, c, m[15], 0xfe2ce6e0u, 10);
+    MD5_STEP(MD5_I, c, d, a, b, m[6], 0xa3014314u, 15);
+    MD5_STEP(MD5_I, b, c, d, a, m[13], 0x4e0811a1u, 21);
+    MD5_STEP(MD5_I, a, b, c, d, m[4], 0xf7537e82u, 6);
+    MD5_STEP(MD5_I, d, a, b, c, m[11], 0xbd3af235u, 10);
+    MD5_STEP(MD5_I, c, d, a, b, m[2], 0x2ad7d2bbu, 15);
+    MD5_STEP(MD5_I, b, c, d, a, m[9], 0xeb86d391u, 21);
+    st[0] += a;
+    st[1] += b;
+    st[2] += c;
+    st[3] += d;
+}
+
+// 16 bytes at p; aligned -> one dwordx4, otherwise byte loads.
+__device__ __forceinline__ uint4 load16(const uint8_t *p, bool aligned)
+{
+    if (aligned)
+        return *reinterpret_cast<const uint4 *>(p);
+    uint32_t w[4];
+#pragma unroll
+    for (int d = 0; d < 4; d++)
+        w[d] = (uint32_t)p[4 * d] | ((uint32_t)p[4 * d + 1] << 8) |
+               ((uint32_t)p[4 * d + 2] << 16) | ((uint32_t)p[4 * d + 3] << 24);
+    return make_uint4(w[0], w[1], w[2], w[3]);
+}
+
+__device__ __forceinline__ void store_sig(uint8_t *sig, uint64_t L, uint32_t w2, uint32_t w3,
+                                          uint32_t w4, uint32_t w5)
+{
+    uint2 *sp = reinterpret_cast<uint2 *>(sig);
+    sp[0] = make_uint2(bswap32((uint32_t)(L >> 32)), bswap32((uint32_t)L));
+    sp[1] = make_uint2(w2, w3);
+    sp[2] = make_uint2(w4, w5);
+}
+
+// ------------------------------------------------------- lane-per-file path
+
+template <bool SAR, int METHOD>
+__global__ __launch_bounds__(256) void sig_lane_kernel(
+    const uint8_t *__restrict__ base, const uint64_t *__restrict__ offs,
+    const uint64_t *__restrict__ sizes, const uint32_t *__restrict__ order, uint32_t n,
+    const DevTables *__restrict__ tabs, uint32_t *__restrict__ crc_out,
+    uint8_t *__restrict__ sig_out, int32_t *__restrict__ codes_out)
+{
+    __shared__ uint32_t sD[16 * 256];
+    __shared__ uint32_t sT[256];
+    lds_fill(sD, &tabs->t.D[0][0], 16 * 256);
+    lds_fill(sT, tabs->t.T, 256);
+    __syncthreads();
+
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n)
+        return;
+    const uint32_t K16 = tabs->t.K16;
+    const uint32_t f = order ? order[i] : i;
+    const uint64_t L = sizes[f];
+    const uint8_t *p = base + offs[f];
+    uint32_t c = 0xFFFFFFFFu;  // CRC32_XINIT (storage/storage_service.c:7149)
+
+    if (METHOD == 1) {
+        uint32_t e = 0, s = 0, t = 0;  // INIT_HASH_CODES4 (storage/storage_service.c:7156)
+        uint64_t head = (16u - ((uintptr_t)p & 15u)) & 15u;
+        if (head > L)
+            head = L;
+        for (uint64_t k = 0; k < head; k++) {
+            const uint32_t b = p[k];
+            c = crc_byte<SAR>(sT, c, b);
+            h3_byte<SAR>(b, e, s, t);
+        }
+        const uint4 *v = reinterpret_cast<const uint4 *>(p + head);
+        const uint64_t nvec = (L - head) >> 4;
+        uint64_t j = 0;
+        if (nvec >= 4) {
+            uint4 a0 = v[0], a1 = v[1], a2 = v[2], a3 = v[3];
+            for (; j + 4 <= nvec; j += 4) {
+                // prefetch the next 64 B (clamped: the last group reloads itself)
+                const uint64_t nx = (j + 8 <= nvec) ? j + 4 : j;
+                const uint4 b0 = v[nx], b1 = v[nx + 1], b2 = v[nx + 2], b3 = v[nx + 3];
+                c = chain16<SAR>(sD, c, a0, K16);
+                h3_word<SAR>(a0.x, e, s, t);
+                h3_word<SAR>(a0.y, e, s, t);
+                h3_word<SAR>(a0.z, e, s, t);
+                h3_word<SAR>(a0.w, e, s, t);
+                c = chain16<SAR>(sD, c, a1, K16);
+                h3_word<SAR>(a1.x, e, s, t);
+                h3_word<SAR>(a1.y, e, s, t);
+                h3_word<SAR>(a1.z, e, s, t);
+                h3_word<SAR>(a1.w, e, s, t);
+                c = chain16<SAR>(sD, c, a2, K16);
+                h3_word<SAR>(a2.x, e, s, t);
+                h3_word<SAR>(a2.y, e, s, t);
+                h3_word<SAR>(a2.z, e, s, t);
+                h3_word<SAR>(a2.w, e, s, t);
+                c = chain16<SAR>(sD, c, a3, K16);
+                h3_word<SAR>(a3.x, e, s, t);
+                h3_word<SAR>(a3.y, e, s, t);
+                h3_word<SAR>(a3.z, e, s, t);
+                h3_word<SAR>(a3.w, e, s, t);
+                a0 = b0;
+                a1 = b1;
+                a2 = b2;
+                a3 = b3;
+            }
+        }
+        for (; j < nvec; j++) {
+            const uint4 a = v[j];
+            c = chain16<SAR>(sD, c, a, K16);
+            h3_word<SAR>(a.x, e, s, t);
+            h3_word<SAR>(a.y, e, s, t);
+            h3_word<SAR>(a.z, e, s, t);
+            h3_word<SAR>(a.w, e, s, t);
+        }
+        for (uint64_t k = head + (nvec << 4); k < L; k++) {
+            const uint32_t b = p[k];
+            c = crc_byte<SAR>(sT, c, b);
+            h3_byte<SAR>(b, e, s, t);
+        }
+        c ^= 0xFFFFFFFFu;  // CRC32_FINAL / FINISH_HASH_CODES4 (storage/storage_dio.c:500,508)
+        crc_out[f] = c;
+        if (sig_out)
+            store_sig(sig_out + 24ull * f, L, bswap32(c), bswap32(e), bswap32(s), bswap32(t));
+        if (codes_out)
+            reinterpret_cast<int4 *>(codes_out)[f] = make_int4((int)c, (int)e, (int)s, (int)t);
+    } else {
+        uint32_t st[4] = {0x67452301u, 0xefcdab89u, 0x98badcfeu, 0x10325476u};  // my_md5_init
+        const bool al = (((uintptr_t)p) & 15u) == 0;
+        const uint64_t nblk = L >> 6;
+        uint64_t j = 0;
+        if (nblk) {
+            uint4 a0 = load16(p, al), a1 = load16(p + 16, al), a2 = load16(p + 32, al),
+                  a3 = load16(p + 48, al);
+            for (; j < nblk; j++) {
+                const uint8_t *q = p + ((j + 1 < nblk) ? (j + 1) : j) * 64;
+                const uint4 b0 = load16(q, al), b1 = load16(q + 16, al), b2 = load16(q + 32, al),
+                            b3 = load16(q + 48, al);
+                c = chain16<SAR>(sD, c, a0, K16);
+                c = chain16<SAR>(sD, c, a1, K16);
+                c = chain16<SAR>(sD, c, a2, K16);
+                c = chain16<SAR>(sD, c, a3, K16);
+                const uint32_t m[16] = {a0.x, a0.y, a0.z, a0.w, a1.x, a1.y, a1.z, a1.w,
+                                        a2.x, a2.y, a2.z, a2.w, a3.x, a3.y, a3.z, a3.w};
+                md5_compress(st, m);
+                a0 = b0;
+                a1 = b1;
+                a2 = b2;
+                a3 = b3;
+            }
+        }
+        // final block(s): r tail bytes, 0x80, zero pad, 64-bit bit length (RFC 1321 3.1-3.2)
+        const uint8_t *tp = p + (nblk << 6);
+        const uint32_t r = (uint32_t)(L & 63u);
+        uint32_t m[16];
+#pragma unroll
+        for (int wd = 0; wd < 16; wd++) {
+            uint32_t word = 0;
+#pragma unroll
+            for (int q = 0; q < 4; q++) {
+                const uint32_t k = 4 * wd + q;
+                uint32_t b = 0;
+                if (k < r) {
+                    b = tp[k];
+                    c = crc_byte<SAR>(sT, c, b);
+                } else if (k == r) {
+                    b = 0x80u;
+                }
+                word |= b << (8 * q);
+            }
+            m[wd] = word;
+        }
+        const uint64_t bits = L << 3;
+        if (r < 56) {
+            m[14] = (uint32_t)bits;
+            m[15] = (uint32_t)(bits >> 32);
+            md5_compress(st, m);
+        } else {
+            md5_compress(st, m);
+#pragma unroll
+            for (int wd = 0; wd < 14; wd++)
+                m[wd] = 0;
+            m[14] = (uint32_t)bits;
+            m[15] = (uint32_t)(bits >> 32);
+            md5_compress(st, m);
+        }
+        c ^= 0xFFFFFFFFu;
+        crc_out[f] = c;
+        if (sig_out)  // memcpy(sig + 8, md5 digest, 16) (storage/storage_service.c:119)
+            store_sig(sig_out + 24ull * f, L, st[0], st[1], st[2], st[3]);
+        if (codes_out)
+            reinterpret_cast<int4 *>(codes_out)[f] =
+                make_int4((int)st[0], (int)st[1], (int)st[2], (int)st[3]);
+    }
+}
+
+// ------------------------------------------------------- segmented CRC path
+
+// Bytes at addresses [lo, lo+4) of the file's segment 0 are XOR 0xFF for the
+// unsigned variant; bytes below `valid` are replaced by the neutral byte.
+template <bool SAR>
+__device__ __noinline__ uint4 seg_fix_vector(uint4 w, uintptr_t va, uintptr_t valid, bool xor4)
+{
+    uint32_t d[4] = {w.x, w.y, w.z, w.w};
+#pragma unroll
+    for (int i = 0; i < 16; i++) {
+        const uintptr_t a = va + i;
+        const uint32_t sh = 8 * (i & 3);
+        uint32_t b = (d[i >> 2] >> sh) & 0xFFu;
+        if (a < valid)
+            b = SAR ? 0xFFu : 0u;
+        else if (!SAR && xor4 && a < valid + 4)
+            b ^= 0xFFu;
+        d[i >> 2] = (d[i >> 2] & ~(0xFFu << sh)) | (b << sh);
+    }
+    return make_uint4(d[0], d[1], d[2], d[3]);
+}
+
+// Zero-init CRC state of the (masked) bytes [A, E) of one segment, computed
+// by the whole wave.  See DESIGN.md "K2 segmented CRC" for the algebra.
+template <bool SAR>
+__device__ __forceinline__ uint32_t crc_segment(const uint32_t *sD, const uint32_t *sT,
+                                                const uint32_t *sA, const uint32_t *sR,
+                                                uint32_t K16, const uint8_t *Ap, const uint8_t *Ep,
+                                                bool first_seg, int lane)
+{
+    const uintptr_t A = (uintptr_t)Ap, E = (uintptr_t)Ep;
+    const uintptr_t s16 = A & ~(uintptr_t)15, e16 = E & ~(uintptr_t)15;
+    const bool xor4 = !SAR && first_seg;
+    uint32_t state = 0;
+    if (e16 > s16) {
+        const int64_t nvec = (int64_t)((e16 - s16) >> 4);
+        const int64_t J = (nvec + 255) >> 8;
+        const uint4 *v = reinterpret_cast<const uint4 *>(s16);
+        const uint4 neutral = SAR ? make_uint4(~0u, ~0u, ~0u, ~0u) : make_uint4(0, 0, 0, 0);
+        uint32_t acc = 0;
+        for (int64_t jb = 0; jb < J; jb++) {
+            const int64_t vb = nvec - 256 * (J - jb) + 4 * lane;
+            uint4 w[4];
+#pragma unroll
+            for (int q = 0; q < 4; q++)
+                w[q] = (vb + q >= 0) ? v[vb + q] : neutral;
+            if (jb)
+                acc = apply4(sA, acc);  // advance 4032 B to this lane's next piece
+#pragma unroll
+            for (int q = 0; q < 4; q++) {
+                const uintptr_t va = s16 + 16 * (uintptr_t)(vb + q);
+                if (vb + q >= 0 && va < A + 4)
+                    w[q] = seg_fix_vector<SAR>(w[q], va, A, xor4);
+                acc = chain16<SAR>(sD, acc, w[q], K16);
+            }
+        }
+        // wave reduction: lane group values relative to the group's end
+#pragma unroll
+        for (int lv = 0; lv < 6; lv++) {
+            const uint32_t u = apply4(sR + lv * 1024, acc);
+            const uint32_t o = __shfl_xor(u, 1 << lv);
+            if (lane & (1 << lv))
+                acc ^= o;
+        }
+        state = __shfl(acc, 63);
+    }
+    for (uintptr_t a = (e16 > A ? e16 : A); a < E; a++) {
+        uint32_t b = *reinterpret_cast<const uint8_t *>(a);
+        if (SAR || (xor4 && a < A + 4))
+            b ^= 0xFFu;
+        state = crc_byte<SAR>(sT, state, b);
+    }
+    return state;
+}
+
+// Constant making crc0(masked data) into CRC32_FINAL(CRC32_ex(data, XINIT)).
+template <bool SAR>
+__device__ __forceinline__ uint32_t crc_final_const(uint64_t L)
+{
+    if (SAR)
+        return 0;
+    return 0xFFFFFFFFu ^ (L < 4 ? (0xFFFFFFFFu >> (8 * (uint32_t)L)) : 0u);
+}
+
+template <bool SAR>
+__global__ __launch_bounds__(512) void crc_seg_kernel(
+    const uint8_t *__restrict__ base, const uint64_t *__restrict__ offs,
+    const uint64_t *__restrict__ sizes, const uint64_t *__restrict__ seg_first, uint32_t n,
+    const DevTables *__restrict__ tabs, uint32_t *__restrict__ crc_out)
+{
+    __shared__ uint32_t sD[16 * 256];
+    __shared__ uint32_t sT[256];
+    __shared__ uint32_t sA[4 * 256];
+    __shared__ uint32_t sR[6 * 4 * 256];
+    lds_fill(sD, SAR ? &tabs->Dc[0][0] : &tabs->t.D[0][0], 16 * 256);
+    lds_fill(sT, tabs->t.T, 256);
+    lds_fill(sA, &tabs->t.ADV4032[0][0], 4 * 256);
+    lds_fill(sR, &tabs->t.ADVRED[0][0][0], 6 * 4 * 256);
+    __syncthreads();
+
+    const uint32_t K16 = tabs->t.K16;
+    const int lane = threadIdx.x & 63;
+    const uint64_t wpb = blockDim.x >> 6;
+    const uint64_t w = (uint64_t)blockIdx.x * wpb + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const uint64_t nw = (uint64_t)gridDim.x * wpb;
+    const uint64_t total = seg_first[n];
+    uint64_t s = (total * w) / nw;
+    const uint64_t s_end = (total * (w + 1)) / nw;
+    if (s >= s_end)
+        return;
+    uint32_t lo = 0, hi = n;  // last f with seg_first[f] <= s
+    while (hi - lo > 1) {
+        const uint32_t mid = (lo + hi) >> 1;
+        if (seg_first[mid] <= s)
+            lo = mid;
+        else
+            hi = mid;
+    }
+    uint32_t f = lo;
+    for (; s < s_end; s++) {
+        while (seg_first[f + 1] <= s)
+            f++;
+        const uint64_t k = s - seg_first[f];
+        const uint64_t nseg = seg_first[f + 1] - seg_first[f];
+        const uint64_t L = sizes[f];
+        const uint8_t *fp = base + offs[f];
+        const uint64_t lo_b = k * kSegBytes;
+        const uint64_t hi_b = (L < lo_b + kSegBytes) ? L : lo_b + kSegBytes;
+        uint32_t v = crc_segment<SAR>(sD, sT, sA, sR, K16, fp + lo_b, fp + hi_b, k == 0, lane);
+        if (nseg == 1) {
+            if (lane == 0)
+                crc_out[f] = v ^ crc_final_const<SAR>(L);
+        } else {
+            // advance the segment state to the file end: product of M^(2^k)
+            uint64_t nadv = L - hi_b;
+            const int col = lane & 31;
+            for (int kk = 0; nadv; kk++, nadv >>= 1) {
+                if (!(nadv & 1))
+                    continue;
+                uint32_t part = ((v >> col) & 1u) ? tabs->t.MPOW[kk][col] : 0u;
+                part ^= __shfl_xor(part, 16);
+                part ^= __shfl_xor(part, 8);
+                part ^= __shfl_xor(part, 4);
+                part ^= __shfl_xor(part, 2);
+                part ^= __shfl_xor(part, 1);
+                v = part;
+            }
+            if (lane == 0)
+                atomicXor(&crc_out[f], v ^ (k == 0 ? crc_final_const<SAR>(L) : 0u));
+        }
+    }
+}
+
+// ---------------------------------------------------------------- planning
+
+__global__ void plan_nseg_kernel(const uint64_t *__restrict__ sizes, uint32_t n,
+                                 uint64_t *__restrict__ nseg, uint32_t *__restrict__ crc_out)
+{
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n)
+        return;
+    const uint64_t L = sizes[i];
+    nseg[i] = (L + kSegBytes - 1) / kSegBytes;
+    crc_out[i] = 0;  // empty files keep CRC 0; multi-segment files accumulate by XOR
+}
+
+__device__ __forceinline__ uint32_t size_bin(uint64_t L)
+{
+    if (L == 0)
+        return 0;
+    const uint32_t e = 63 - __builtin_clzll(L);
+    const uint32_t m = (e >= 5) ? (uint32_t)((L >> (e - 5)) & 31u) : (uint32_t)((L << (5 - e)) & 31u);
+    return e * 32 + m;  // < kSizeBins
+}
+
+__global__ void bin_hist_kernel(const uint64_t *__restrict__ sizes, uint32_t n,
+                                uint32_t *__restrict__ hist)
+{
+    __shared__ uint32_t h[kSizeBins];
+    for (int b = threadIdx.x; b < kSizeBins; b += blockDim.x)
+        h[b] = 0;
+    __syncthreads();
+    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x)
+        atomicAdd(&h[size_bin(sizes[i])], 1u);
+    __syncthreads();
+    for (int b = threadIdx.x; b < kSizeBins; b += blockDim.x)
+        if (h[b])
+            atomicAdd(&hist[b], h[b]);
+}
+
+// Descending exclusive scan of the bin histogram (one block of kSizeBins threads / 2).
+__global__ __launch_bounds__(1024) void bin_scan_kernel(const uint32_t *__restrict__ hist,
+                                                        uint32_t *__restrict__ cursor)
+{
+    __shared__ uint32_t s[kSizeBins];
+    for (int b = threadIdx.x; b < kSizeBins; b += blockDim.x)
+        s[b] = hist[kSizeBins - 1 - b];  // reversed: largest bin first
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        uint32_t run = 0;
+        for (int b = 0; b < kSizeBins; b++) {
+            const uint32_t c = s[b];
+            s[b] = run;
+            run += c;
+        }
+    }
+    __syncthreads();
+    for (int b = threadIdx.x; b < kSizeBins; b += blockDim.x)
+        cursor[kSizeBins - 1 - b] = s[b];
+}
+
+__global__ __launch_bounds__(1024) void bin_scatter_kernel(const uint64_t *__restrict__ sizes,
+                                                           uint32_t n, uint32_t *__restrict__ cursor,
+                                                           uint32_t *__restrict__ order)
+{
+    __shared__ uint32_t cnt[kSizeBins];
+    __shared__ uint32_t bas[kSizeBins];
+    for (int b = threadIdx.x; b < kSizeBins; b += blockDim.x)
+        cnt[b] = 0;
+    __syncthreads();
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    uint32_t bin = 0, rank = 0;
+    if (i < n) {
+        bin = size_bin(sizes[i]);
+        rank = atomicAdd(&cnt[bin], 1u);
+    }
+    __syncthreads();
+    for (int b = threadIdx.x; b < kSizeBins; b += blockDim.x)
+        if (cnt[b])
+            bas[b] = atomicAdd(&cursor[b], cnt[b]);
+    __syncthreads();
+    if (i < n)
+        order[bas[bin] + rank] = i;
+}
+
+// -------------------------------------------------------- exclusive scan u64
+
+constexpr int kScanBlock = 256;
+constexpr int kScanItems = 4;
+constexpr int kScanTile = kScanBlock * kScanItems;
+
+__device__ __forceinline__ uint64_t block_exclusive_scan(uint64_t v, uint64_t *wsum, uint64_t &total)
+{
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    uint64_t x = v;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint64_t y = __shfl_up(x, o);
+        if (lane >= o)
+            x += y;
+    }
+    if (lane == 63)
+        wsum[wid] = x;
+    __syncthreads();
+    uint64_t pre = 0, tot = 0;
+    for (int k = 0; k < (int)(blockDim.x >> 6); k++) {
+        if (k < wid)
+            pre += wsum[k];
+        tot += wsum[k];
+    }
+    __syncthreads();
+    total = tot;
+    return pre + x - v;
+}
+
+__global__ __launch_bounds__(kScanBlock) void scan_reduce_kernel(const uint64_t *__restrict__ in,
+                                                                 uint64_t n,
+                                                                 uint64_t *__restrict__ bsum)
+{
+    __shared__ uint64_t wsum[kScanBlock / 64];
+    const uint64_t b0 = (uint64_t)blockIdx.x * kScanTile + threadIdx.x * kScanItems;
+    uint64_t v = 0;
+#pragma unroll
+    for (int k = 0; k < kScanItems; k++)
+        if (b0 + k < n)
+            v += in[b0 + k];
+    uint64_t tot;
+    block_exclusive_scan(v, wsum, tot);
+    if (threadIdx.x == 0)
+        bsum[blockIdx.x] = tot;
+}
+
+__global__ __launch_bounds__(kScanBlock) void scan_sums_kernel(uint64_t *__restrict__ bsum,
+                                                               uint64_t nb)
+{
+    __shared__ uint64_t wsum[kScanBlock / 64];
+    uint64_t carry = 0;
+    for (uint64_t c0 = 0; c0 < nb; c0 += kScanBlock) {
+        const uint64_t i = c0 + threadIdx.x;
+        const uint64_t v = (i < nb) ? bsum[i] : 0;
+        uint64_t tot;
+        const uint64_t ex = block_exclusive_scan(v, wsum, tot);
+        if (i < nb)
+            bsum[i] = carry + ex;
+        carry += tot;
+    }
+}
+
+__global__ __launch_bounds__(kScanBlock) void scan_apply_kernel(const uint64_t *__restrict__ in,
+                                                                uint64_t n,
+                                                                const uint64_t *__restrict__ bsum,
+                                                                uint64_t *__restrict__ out)
+{
+    __shared__ uint64_t wsum[kScanBlock / 64];
+    const uint64_t b0 = (uint64_t)blockIdx.x * kScanTile + threadIdx.x * kScanItems;
+    uint64_t vals[kScanItems];
+    uint64_t v = 0;
+#pragma unroll
+    for (int k = 0; k < kScanItems; k++) {
+        vals[k] = (b0 + k < n) ? in[b0 + k] : 0;
+        v += vals[k];
+    }
+    uint64_t tot;
+    uint64_t run = bsum[blockIdx.x] + block_exclusive_scan(v, wsum, tot);
+#pragma unroll
+    for (int k = 0; k < kScanItems; k++) {
+        if (b0 + k < n)
+            out[b0 + k] = run;
+        run += vals[k];
+    }
+    if (b0 < n && b0 + kScanItems >= n)  // the thread holding the last element writes the total
+        out[n] = run;
+}
+
+// ------------------------------------------------------------------ launchers
+
+hipError_t launch_exclusive_scan(const uint64_t *in, uint64_t n, uint64_t *out, uint64_t *bsum,
+                                 hipStream_t st)
+{
+    if (n == 0)
+        return hipMemsetAsync(out, 0, sizeof(uint64_t), st);
+    const uint64_t nb = (n + kScanTile - 1) / kScanTile;
+    scan_reduce_kernel<<<(unsigned)nb, kScanBlock, 0, st>>>(in, n, bsum);
+    scan_sums_kernel<<<1, kScanBlock, 0, st>>>(bsum, nb);
+    scan_apply_kernel<<<(unsigned)nb, kScanBlock, 0, st>>>(in, n, bsum, out);
+    return hipGetLastError();
+}
+
+uint64_t scan_workspace_elems(uint64_t n) { return (n + kScanTile - 1) / kScanTile + 1; }
+
+hipError_t launch_sig_lane(bool sar, int method, const uint8_t *base, const uint64_t *offs,
+                           const uint64_t *sizes, uint32_t n, uint32_t *hist, uint32_t *order,
+                           const DevTables *tabs, uint32_t *crc_out, uint8_t *sig_out,
+                           int32_t *codes_out, hipStream_t st, hipEvent_t ev0, hipEvent_t ev1)
+{
+    hipError_t e = hipMemsetAsync(hist, 0, sizeof(uint32_t) * kSizeBins * 2, st);
+    if (e != hipSuccess)
+        return e;
+    uint32_t *cursor = hist + kSizeBins;
+    const unsigned hb = (n + 1023) / 1024;
+    bin_hist_kernel<<<hb < 1024 ? hb : 1024, 256, 0, st>>>(sizes, n, hist);
+    bin_scan_kernel<<<1, 1024, 0, st>>>(hist, cursor);
+    bin_scatter_kernel<<<hb, 1024, 0, st>>>(sizes, n, cursor, order);
+    const unsigned g = (n + 255) / 256;
+    if (ev0)
+        (void)hipEventRecord(ev0, st);
+#define LANE_LAUNCH(S, M) \
+    sig_lane_kernel<S, M><<<g, 256, 0, st>>>(base, offs, sizes, order, n, tabs, crc_out, sig_out, codes_out)
+    if (sar) {
+        if (method == 1)
+            LANE_LAUNCH(true, 1);
+        else
+            LANE_LAUNCH(true, 2);
+    } else {
+        if (method == 1)
+            LANE_LAUNCH(false, 1);
+        else
+            LANE_LAUNCH(false, 2);
+    }
+#undef LANE_LAUNCH
+    if (ev1)
+        (void)hipEventRecord(ev1, st);
+    return hipGetLastError();
+}
+
+hipError_t launch_crc_seg(bool sar, const uint8_t *base, const uint64_t *offs, const uint64_t *sizes,
+                          uint32_t n, uint64_t *nseg, uint64_t *seg_first, uint64_t *bsum,
+                          const DevTables *tabs, uint32_t *crc_out, unsigned grid, hipStream_t st,
+                          hipEvent_t ev0, hipEvent_t ev1)
+{
+    plan_nseg_kernel<<<(n + 255) / 256, 256, 0, st>>>(sizes, n, nseg, crc_out);
+    hipError_t e = launch_exclusive_scan(nseg, n, seg_first, bsum, st);
+    if (e != hipSuccess)
+        return e;
+    if (ev0)
+        (void)hipEventRecord(ev0, st);
+    if (sar)
+        crc_seg_kernel<true><<<grid, 512, 0, st>>>(base, offs, sizes, seg_first, n, tabs, crc_out);
+    else
+        crc_seg_kernel<false><<<grid, 512, 0, st>>>(base, offs, sizes, seg_first, n, tabs, crc_out);
+    if (ev1)
+        (void)hipEventRecord(ev1, st);
+    return hipGetLastError();
+}
+
+int crc_seg_blocks_per_cu()
+{
+    int nb = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, crc_seg_kernel<true>, 512, 0) != hipSuccess)
+        return 1;
+    return nb > 0 ? nb : 1;
+}
+
+}  // namespace fdfs

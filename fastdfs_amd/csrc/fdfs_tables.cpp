@@ -1,0 +1,108 @@
+// Table construction for the CRC kernels; see fdfs_tables.hpp.
+#include "fdfs_tables.hpp"
+
+#include <cstring>
+
+namespace fdfs {
+
+static inline uint32_t shr8(uint32_t c, int sar)
+{
+    uint32_t r = c >> 8;
+    if (sar && (c & 0x80000000u))
+        r |= 0xFF000000u;
+    return r;
+}
+
+uint32_t crc_step(const CrcTables &t, uint32_t c, uint8_t b)
+{
+    return t.T[(c ^ b) & 0xFFu] ^ shr8(c, t.sar);
+}
+
+static uint32_t adv_bytes(const CrcTables &t, uint32_t v, uint64_t n)
+{
+    for (uint64_t i = 0; i < n; i++)
+        v = crc_step(t, v, 0);
+    return v;
+}
+
+static uint32_t matvec(const uint32_t cols[32], uint32_t v)
+{
+    uint32_t r = 0;
+    for (int i = 0; i < 32; i++)
+        if (v & (1u << i))
+            r ^= cols[i];
+    return r;
+}
+
+uint32_t crc_advance(const CrcTables &t, uint32_t v, uint64_t nbytes)
+{
+    for (int k = 0; k < 48 && nbytes; k++, nbytes >>= 1)
+        if (nbytes & 1)
+            v = matvec(t.MPOW[k], v);
+    return v;
+}
+
+static void byte_tables_of(const CrcTables &t, uint32_t out[4][256], uint64_t n)
+{
+    // A linear map L splits into 4 byte tables: L(v) = sum_j L(byte_j(v) << 8j).
+    // Build from the 32 basis images, then expand (cheap and exact).
+    uint32_t img[32];
+    for (int i = 0; i < 32; i++)
+        img[i] = adv_bytes(t, 1u << i, n);
+    for (int j = 0; j < 4; j++)
+        for (uint32_t x = 0; x < 256; x++) {
+            uint32_t r = 0;
+            for (int b = 0; b < 8; b++)
+                if (x & (1u << b))
+                    r ^= img[8 * j + b];
+            out[j][x] = r;
+        }
+}
+
+bool build_crc_tables(CrcTables &t, bool arithmetic_shift)
+{
+    std::memset(&t, 0, sizeof(t));
+    t.sar = arithmetic_shift ? 1 : 0;
+    for (uint32_t i = 0; i < 256; i++) {
+        uint32_t c = i;
+        for (int k = 0; k < 8; k++)
+            c = (c & 1u) ? (0xEDB88320u ^ (c >> 1)) : (c >> 1);
+        t.T[i] = c;
+    }
+    // D[p][x]: 16-byte chunk from state 0, byte p = x, others 0.
+    for (int p = 0; p < 16; p++)
+        for (uint32_t x = 0; x < 256; x++)
+            t.D[p][x] = adv_bytes(t, crc_step(t, 0, (uint8_t)x), (uint64_t)(15 - p));
+
+    // Sign fix: M^16(e_i) must equal D[i/8][bit] for i < 31; the residue at
+    // i = 31 is K16 (0 for a logical shift).
+    for (int i = 0; i < 32; i++) {
+        uint32_t e = 1u << i;
+        uint32_t r = adv_bytes(t, e, 16) ^ t.D[i / 8][(e >> (8 * (i / 8))) & 0xFFu];
+        if (i < 31 && r != 0)
+            return false;
+        if (i == 31)
+            t.K16 = r;
+    }
+    if (!t.sar && t.K16 != 0)
+        return false;
+
+    byte_tables_of(t, t.ADV4032, 4032);
+    for (int l = 0; l < 6; l++)
+        byte_tables_of(t, t.ADVRED[l], (uint64_t)64 << l);
+
+    for (int i = 0; i < 32; i++)
+        t.MPOW[0][i] = crc_step(t, 1u << i, 0);
+    for (int k = 1; k < 48; k++)
+        for (int i = 0; i < 32; i++)
+            t.MPOW[k][i] = matvec(t.MPOW[k - 1], matvec(t.MPOW[k - 1], 1u << i));
+
+    // Self-check the power matrices against direct stepping.
+    for (uint64_t n : {1ull, 7ull, 64ull, 4032ull, 65536ull + 3})
+        for (uint32_t v : {0x80000000u, 0x12345678u, 0xFFFFFFFFu})
+            if (crc_advance(t, v, n) != adv_bytes(t, v, n))
+                return false;
+    return true;
+}
+
+}  // namespace fdfs

@@ -1,0 +1,33 @@
+// Host-side construction of every CRC table the kernels use.
+//
+// All of them are derived from ONE function, the single-byte step of
+// CRC32_ex (libfastcommon, called at storage/storage_dio.c:467):
+//     c' = crc_table[(c ^ b) & 0xFF] ^ (c >> 8)
+// where `>>` is arithmetic for the signed-int state libfastcommon declares
+// and logical for an unsigned state.  Flipping `sar` regenerates the slice,
+// advance and GF(2) power tables; no kernel code changes.
+#pragma once
+#include <cstdint>
+
+namespace fdfs {
+
+// Zero-input byte step M (advance by one zero byte) is GF(2)-linear in the
+// state for both shift semantics, which is what every table below relies on.
+struct CrcTables {
+    uint32_t T[256];          // byte step table (reflected 0xEDB88320)
+    uint32_t D[16][256];      // slice-by-16: byte x at chunk position p -> state at chunk end
+    uint32_t K16;             // chain16 sign fix: M^16(c) = sum_j D[j][byte_j(c)] ^ (c<0 ? K16 : 0)
+    uint32_t ADV4032[4][256]; // advance by 4032 zero bytes (wave stride - lane piece)
+    uint32_t ADVRED[6][4][256]; // advance by 64<<t bytes, t = 0..5 (wave reduction tree)
+    uint32_t MPOW[48][32];    // columns of M^(2^k), k = 0..47 (arbitrary advance)
+    int sar;                  // 1 = arithmetic shift (signed state)
+};
+
+// Returns false if an internal identity check fails (never expected).
+bool build_crc_tables(CrcTables &t, bool arithmetic_shift);
+
+// Host reference of the step (used by the table builder and self-checks).
+uint32_t crc_step(const CrcTables &t, uint32_t c, uint8_t b);
+uint32_t crc_advance(const CrcTables &t, uint32_t v, uint64_t nbytes);
+
+}  // namespace fdfs

@@ -1,0 +1,139 @@
+/*
+ * fdfs_gpu.h -- C ABI of libfdfs_gpu: MI355X (gfx950) batch implementation of
+ * FastDFS's upload-path CRC32 + duplicate-check signature, and of the bulk
+ * duplicate grouping that replaces per-file FastDHT lookups.
+ *
+ * Plain C types only: device pointers are `const void *` / `void *`, streams
+ * are hipStream_t passed as `void *` (NULL = the null stream).  Every call
+ * returns 0 or a positive errno value (EINVAL bad arguments, ENOMEM
+ * allocation failure, EIO a HIP error), the convention of the reference's
+ * storage daemon (e.g. storage/storage_dio.c:443).  Inputs are caller owned
+ * and never modified; outputs are preallocated by the caller.
+ *
+ * Interfaces replaced (reference file:line -> entry point):
+ *   CRC32_XINIT / CRC32_ex / CRC32_FINAL
+ *       storage/storage_service.c:7149, storage/storage_dio.c:467,500,
+ *       client/fdfs_crc32.c:67,91,99           -> fdfs_gpu_sig_batch(.., FDFS_SIG_CRC_ONLY, ..)
+ *   INIT/CALC/FINISH_HASH_CODES4 + STORAGE_GEN_FILE_SIGNATURE
+ *       storage/storage_service.c:7156, storage/storage_dio.c:475,508,
+ *       storage/storage_service.c:106-120,2635 -> fdfs_gpu_sig_batch(.., FDFS_SIG_HASH, ..)
+ *   my_md5_init/update/final + STORAGE_GEN_FILE_SIGNATURE
+ *       storage/storage_service.c:7160, storage/storage_dio.c:480,512  -> fdfs_gpu_sig_batch(.., FDFS_SIG_MD5, ..)
+ *   fdht_get_ex1 "fid" / fdht_set_ex / fdht_inc_ex "ref" dedup decision
+ *       storage/storage_service.c:2652,2714,2734,2984 -> fdfs_gpu_dedup (1 GPU)
+ *       or fdfs_gpu_dedup_bucket + exchange + fdfs_gpu_dedup_group (N GPUs)
+ */
+#ifndef FDFS_GPU_H
+#define FDFS_GPU_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define FDFS_GPU_ABI_VERSION 1
+
+/* Signature methods: values of STORAGE_FILE_SIGNATURE_METHOD_*
+ * (storage/storage_global.h:41-42); 0 = CRC32 only (check_file_duplicate=0,
+ * conf/storage.conf:195). */
+#define FDFS_SIG_CRC_ONLY 0
+#define FDFS_SIG_HASH     1
+#define FDFS_SIG_MD5      2
+
+#define FDFS_FILE_SIGNATURE_SIZE 24   /* storage/storage_service.c:106 */
+
+/* Context flags. */
+/* CRC32_ex / ELFHash_ex with an unsigned state (logical >>).  The default
+ * (flag clear) is the signed-int state libfastcommon declares (arithmetic >>),
+ * see DESIGN.md "Oracle" for why both exist. */
+#define FDFS_GPU_FLAG_UNSIGNED_HASH 0x1u
+
+typedef struct fdfs_gpu_ctx fdfs_gpu_ctx;
+
+/* A batch of files in device memory: file i is bytes
+ * [base + offset[i], base + offset[i] + size[i]).  offset/size are device
+ * arrays of n entries.  Any alignment is correct; 16-byte aligned file
+ * starts take the fast load path. */
+typedef struct {
+    const void     *base;
+    const uint64_t *offset;
+    const uint64_t *size;
+    uint32_t        n;
+} fdfs_gpu_batch;
+
+/* Version / capability probe; returns FDFS_GPU_ABI_VERSION. */
+int fdfs_gpu_abi_version(void);
+
+/* Open a context on HIP device `device`: builds and uploads the CRC tables
+ * for the selected hash semantics.  *out receives the handle. */
+int fdfs_gpu_open(int device, unsigned flags, fdfs_gpu_ctx **out);
+int fdfs_gpu_close(fdfs_gpu_ctx *ctx);
+
+/* Reserve device workspace for batches of up to max_files files and
+ * dedup of up to max_records records, so later calls do no allocation
+ * (and can be captured in a hipGraph).  Optional: calls grow it on demand. */
+int fdfs_gpu_reserve(fdfs_gpu_ctx *ctx, uint64_t max_files, uint64_t max_records);
+
+/* Per-file CRC32 (always, as uploads do: storage/storage_service.c:4533) and,
+ * for FDFS_SIG_HASH / FDFS_SIG_MD5, the 24-byte duplicate-check signature.
+ *   crc_out:   device uint32_t[n], the %u value fdfs_crc32 prints.
+ *   sig_out:   device uint8_t[n*24] or NULL (ignored for CRC_ONLY).
+ *   codes_out: device int32_t[n*4] or NULL: file_hash_codes after FINISH
+ *              (HASH) or the raw MD5 digest (MD5), as StorageFileContext holds
+ *              them (storage/storage_nio.h:94).
+ * Asynchronous on `stream`. */
+int fdfs_gpu_sig_batch(fdfs_gpu_ctx *ctx, const fdfs_gpu_batch *batch, int method,
+                       uint32_t *crc_out, uint8_t *sig_out, int32_t *codes_out,
+                       void *stream);
+
+/* Single-GPU duplicate grouping over n records in ingest order.
+ *   sig:  device uint8_t[n*24]; gidx: device uint64_t[n] global ingest index
+ *         of each record, or NULL for 0..n-1.
+ *   rep_out: device uint64_t[n], ingest index of the class's first file
+ *            (the FastDHT "fid" source, storage/storage_service.c:2714).
+ *   ref_out: device uint32_t[n], class size (the "ref" count after all
+ *            links, storage/storage_service.c:2734,2984). */
+int fdfs_gpu_dedup(fdfs_gpu_ctx *ctx, const uint8_t *sig, const uint64_t *gidx,
+                   uint64_t n, uint64_t *rep_out, uint32_t *ref_out, void *stream);
+
+/* Multi-GPU dedup building blocks (one process per GPU; the exchange between
+ * the two calls is the caller's all-to-all over RCCL/xGMI).
+ * Bucket: packs records {sig[24], gidx (uint64 LE)} into 32-byte rows grouped
+ * by owner rank (owner = hash(sig) mod nranks, nranks <= 64):
+ *   records_out: device uint8_t[n*32], rows of owner 0 first, then owner 1 ..
+ *   counts_out:  device uint64_t[nranks], rows per owner;
+ *   row_of_out:  device uint64_t[n] or NULL, row index of record i (to route
+ *                the owner's answers back). */
+int fdfs_gpu_dedup_bucket(fdfs_gpu_ctx *ctx, const uint8_t *sig, const uint64_t *gidx,
+                          uint64_t n, uint32_t nranks, uint8_t *records_out,
+                          uint64_t *counts_out, uint64_t *row_of_out, void *stream);
+/* Group: the owner's records (n rows of 32 B, device) -> per-row rep (min gidx
+ * of its class) and ref (class size), in row order. */
+int fdfs_gpu_dedup_group(fdfs_gpu_ctx *ctx, const uint8_t *records, uint64_t n,
+                         uint64_t *rep_out, uint32_t *ref_out, void *stream);
+
+/* Kernel timing (for benchmarks and profiling).  When enabled, every call
+ * records a HIP event pair on its stream around its main kernel:
+ *   FDFS_KERNEL_SIG_LANE  sig_lane_kernel   (FDFS_SIG_HASH / FDFS_SIG_MD5)
+ *   FDFS_KERNEL_CRC_SEG   crc_seg_kernel    (FDFS_SIG_CRC_ONLY)
+ *   FDFS_KERNEL_DEDUP     insert + emit     (fdfs_gpu_dedup / _group)
+ *   FDFS_KERNEL_BUCKET    count + scatter   (fdfs_gpu_dedup_bucket)
+ * fdfs_gpu_read_timing waits for the recorded events, returns the summed
+ * milliseconds and launch count for `kernel` since the last read, and resets
+ * them. */
+#define FDFS_KERNEL_SIG_LANE 0
+#define FDFS_KERNEL_CRC_SEG  1
+#define FDFS_KERNEL_DEDUP    2
+#define FDFS_KERNEL_BUCKET   3
+int fdfs_gpu_set_timing(fdfs_gpu_ctx *ctx, int enable);
+int fdfs_gpu_read_timing(fdfs_gpu_ctx *ctx, int kernel, double *ms_out, uint64_t *launches_out);
+
+/* Last HIP error string of this context (for logging), never NULL. */
+const char *fdfs_gpu_last_error(fdfs_gpu_ctx *ctx);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,449 @@
+/*
+ * fdfs_oracle.c -- CPU restatement of the FastDFS upload-path CRC32 /
+ * dedup-signature arithmetic.  TEST INFRASTRUCTURE ONLY (see header).
+ *
+ * The arithmetic lives in libfastcommon (hash.c / md5.c), which the
+ * reference links with -lfastcommon (storage/Makefile.in:5,
+ * client/Makefile.in:7) but does not vendor.  Each function below names the
+ * reference call site whose behaviour it restates.  All integer arithmetic
+ * is done on uint32_t with the shift semantics spelled out, so the C here
+ * has no undefined or implementation-defined behaviour.
+ */
+#define _GNU_SOURCE
+#include "fdfs_oracle.h"
+
+#include <pthread.h>
+#include <stdlib.h>
+#include <string.h>
+
+/* ------------------------------------------------------------------ CRC32 */
+
+static uint32_t g_crc_table[256];
+static pthread_once_t g_crc_once = PTHREAD_ONCE_INIT;
+
+/* Reflected CRC-32 table, polynomial 0xEDB88320 (libfastcommon hash.c
+ * crc_table, the table CRC32_ex indexes). */
+static void crc_table_build(void)
+{
+    for (uint32_t i = 0; i < 256; i++) {
+        uint32_t c = i;
+        for (int k = 0; k < 8; k++)
+            c = (c & 1u) ? (0xEDB88320u ^ (c >> 1)) : (c >> 1);
+        g_crc_table[i] = c;
+    }
+}
+
+uint32_t orc_crc_table_entry(int i)
+{
+    pthread_once(&g_crc_once, crc_table_build);
+    return g_crc_table[i & 0xFF];
+}
+
+/* x >> k on a signed 32-bit int as gcc compiles it (arithmetic). */
+static inline uint32_t sar32(uint32_t x, int k)
+{
+    uint32_t r = x >> k;
+    if (x & 0x80000000u)
+        r |= ~(0xFFFFFFFFu >> k);
+    return r;
+}
+
+/* CRC32_ex(key, key_len, init_value), called at storage/storage_dio.c:467
+ * and client/fdfs_crc32.c:91:  int crc;  crc = crc_table[(crc ^ *p) & 0xFF]
+ * ^ (crc >> 8);  -- with `int crc` the >> is arithmetic (variant SIGNED). */
+int32_t orc_crc32_ex(const void *buf, size_t len, int32_t init, int variant)
+{
+    pthread_once(&g_crc_once, crc_table_build);
+    const uint8_t *p = (const uint8_t *)buf;
+    uint32_t c = (uint32_t)init;
+    if (variant == ORC_VARIANT_SIGNED) {
+        for (size_t i = 0; i < len; i++)
+            c = g_crc_table[(c ^ p[i]) & 0xFFu] ^ sar32(c, 8);
+    } else {
+        for (size_t i = 0; i < len; i++)
+            c = g_crc_table[(c ^ p[i]) & 0xFFu] ^ (c >> 8);
+    }
+    return (int32_t)c;
+}
+
+/* CRC32_FINAL(crc) = crc ^ 0xFFFFFFFF: storage/storage_dio.c:500,
+ * client/fdfs_crc32.c:99. */
+int32_t orc_crc32_final(int32_t crc)
+{
+    return (int32_t)((uint32_t)crc ^ 0xFFFFFFFFu);
+}
+
+/* ----------------------------------------------------- the other 3 hashes */
+
+/* ELFHash_ex, the h[1] of CALC_HASH_CODES4 (storage/storage_dio.c:475):
+ *   h = (h << 4) + b;  if ((x = h & 0xF0000000) != 0) { h ^= x >> 24; h &= ~x; }
+ * with int h, int x  -> x >> 24 arithmetic (variant SIGNED). */
+int32_t orc_elf_ex(const void *buf, size_t len, int32_t init, int variant)
+{
+    const uint8_t *p = (const uint8_t *)buf;
+    uint32_t h = (uint32_t)init;
+    for (size_t i = 0; i < len; i++) {
+        h = (h << 4) + p[i];
+        uint32_t x = h & 0xF0000000u;
+        if (x != 0) {
+            h ^= (variant == ORC_VARIANT_SIGNED) ? sar32(x, 24) : (x >> 24);
+            h &= ~x;
+        }
+    }
+    return (int32_t)h;
+}
+
+/* simple_hash_ex, h[2] of CALC_HASH_CODES4: h = 31 * h + b (mod 2^32). */
+int32_t orc_simple_ex(const void *buf, size_t len, int32_t init)
+{
+    const uint8_t *p = (const uint8_t *)buf;
+    uint32_t h = (uint32_t)init;
+    for (size_t i = 0; i < len; i++)
+        h = 31u * h + p[i];
+    return (int32_t)h;
+}
+
+/* Time33Hash_ex, h[3] of CALC_HASH_CODES4: h += (h << 5) + b (mod 2^32). */
+int32_t orc_time33_ex(const void *buf, size_t len, int32_t init)
+{
+    const uint8_t *p = (const uint8_t *)buf;
+    uint32_t h = (uint32_t)init;
+    for (size_t i = 0; i < len; i++)
+        h += (h << 5) + p[i];
+    return (int32_t)h;
+}
+
+/* INIT_HASH_CODES4 (storage/storage_service.c:7156). */
+void orc_hash4_init(int32_t h[4])
+{
+    h[0] = (int32_t)ORC_CRC32_XINIT;
+    h[1] = 0;
+    h[2] = 0;
+    h[3] = 0;
+}
+
+/* CALC_HASH_CODES4 (storage/storage_dio.c:475): four separate byte passes. */
+void orc_hash4_calc(const void *buf, size_t len, int32_t h[4], int variant)
+{
+    h[0] = orc_crc32_ex(buf, len, h[0], variant);
+    h[1] = orc_elf_ex(buf, len, h[1], variant);
+    h[2] = orc_simple_ex(buf, len, h[2]);
+    h[3] = orc_time33_ex(buf, len, h[3]);
+}
+
+/* FINISH_HASH_CODES4 (storage/storage_dio.c:508): only h[0] is finalised. */
+void orc_hash4_finish(int32_t h[4])
+{
+    h[0] = orc_crc32_final(h[0]);
+}
+
+/* -------------------------------------------------------------------- MD5 */
+/* my_md5_init / my_md5_update / my_md5_final (storage/storage_service.c:7160,
+ * storage/storage_dio.c:480,512): the RSA reference MD5 of RFC 1321,
+ * restated here from the RFC's algorithm description (sections 3.1-3.5). */
+
+static inline uint32_t rol32(uint32_t x, int s)
+{
+    return (x << s) | (x >> (32 - s));
+}
+
+static const uint32_t MD5_K[64] = {
+    0xd76aa478, 0xe8c7b756, 0x242070db, 0xc1bdceee, 0xf57c0faf, 0x4787c62a,
+    0xa8304613, 0xfd469501, 0x698098d8, 0x8b44f7af, 0xffff5bb1, 0x895cd7be,
+    0x6b901122, 0xfd987193, 0xa679438e, 0x49b40821, 0xf61e2562, 0xc040b340,
+    0x265e5a51, 0xe9b6c7aa, 0xd62f105d, 0x02441453, 0xd8a1e681, 0xe7d3fbc8,
+    0x21e1cde6, 0xc33707d6, 0xf4d50d87, 0x455a14ed, 0xa9e3e905, 0xfcefa3f8,
+    0x676f02d9, 0x8d2a4c8a, 0xfffa3942, 0x8771f681, 0x6d9d6122, 0xfde5380c,
+    0xa4beea44, 0x4bdecfa9, 0xf6bb4b60, 0xbebfbc70, 0x289b7ec6, 0xeaa127fa,
+    0xd4ef3085, 0x04881d05, 0xd9d4d039, 0xe6db99e5, 0x1fa27cf8, 0xc4ac5665,
+    0xf4292244, 0x432aff97, 0xab9423a7, 0xfc93a039, 0x655b59c3, 0x8f0ccc92,
+    0xffeff47d, 0x85845dd1, 0x6fa87e4f, 0xfe2ce6e0, 0xa3014314, 0x4e0811a1,
+    0xf7537e82, 0xbd3af235, 0x2ad7d2bb, 0xeb86d391};
+
+static const int MD5_S[64] = {
+    7, 12, 17, 22, 7, 12, 17, 22, 7, 12, 17, 22, 7, 12, 17, 22,
+    5, 9,  14, 20, 5, 9,  14, 20, 5, 9,  14, 20, 5, 9,  14, 20,
+    4, 11, 16, 23, 4, 11, 16, 23, 4, 11, 16, 23, 4, 11, 16, 23,
+    6, 10, 15, 21, 6, 10, 15, 21, 6, 10, 15, 21, 6, 10, 15, 21};
+
+static void md5_block(uint32_t st[4], const uint8_t blk[64])
+{
+    uint32_t m[16];
+    for (int i = 0; i < 16; i++)
+        m[i] = (uint32_t)blk[4 * i] | ((uint32_t)blk[4 * i + 1] << 8) |
+               ((uint32_t)blk[4 * i + 2] << 16) |
+               ((uint32_t)blk[4 * i + 3] << 24);
+    uint32_t a = st[0], b = st[1], c = st[2], d = st[3];
+    for (int i = 0; i < 64; i++) {
+        uint32_t f;
+        int g;
+        if (i < 16) {
+            f = (b & c) | (~b & d);
+            g = i;
+        } else if (i < 32) {
+            f = (d & b) | (~d & c);
+            g = (5 * i + 1) & 15;
+        } else if (i < 48) {
+            f = b ^ c ^ d;
+            g = (3 * i + 5) & 15;
+        } else {
+            f = c ^ (b | ~d);
+            g = (7 * i) & 15;
+        }
+        uint32_t t = d;
+        d = c;
+        c = b;
+        b = b + rol32(a + f + MD5_K[i] + m[g], MD5_S[i]);
+        a = t;
+    }
+    st[0] += a;
+    st[1] += b;
+    st[2] += c;
+    st[3] += d;
+}
+
+void orc_md5_init(orc_md5_ctx *ctx)
+{
+    ctx->state[0] = 0x67452301u;
+    ctx->state[1] = 0xefcdab89u;
+    ctx->state[2] = 0x98badcfeu;
+    ctx->state[3] = 0x10325476u;
+    ctx->count = 0;
+}
+
+void orc_md5_update(orc_md5_ctx *ctx, const void *buf, size_t len)
+{
+    const uint8_t *p = (const uint8_t *)buf;
+    size_t have = (size_t)(ctx->count & 63u);
+    ctx->count += len;
+    if (have) {
+        size_t need = 64 - have;
+        if (len < need) {
+            memcpy(ctx->buffer + have, p, len);
+            return;
+        }
+        memcpy(ctx->buffer + have, p, need);
+        md5_block(ctx->state, ctx->buffer);
+        p += need;
+        len -= need;
+    }
+    while (len >= 64) {
+        md5_block(ctx->state, p);
+        p += 64;
+        len -= 64;
+    }
+    if (len)
+        memcpy(ctx->buffer, p, len);
+}
+
+void orc_md5_final(uint8_t digest[16], orc_md5_ctx *ctx)
+{
+    uint64_t bits = ctx->count * 8u;
+    uint8_t pad[72];
+    size_t have = (size_t)(ctx->count & 63u);
+    size_t padlen = (have < 56) ? (56 - have) : (120 - have);
+    memset(pad, 0, sizeof(pad));
+    pad[0] = 0x80;
+    uint8_t lenb[8];
+    for (int i = 0; i < 8; i++)
+        lenb[i] = (uint8_t)(bits >> (8 * i));
+    uint64_t saved = ctx->count;
+    orc_md5_update(ctx, pad, padlen);
+    orc_md5_update(ctx, lenb, 8);
+    ctx->count = saved;
+    for (int i = 0; i < 4; i++)
+        for (int k = 0; k < 4; k++)
+            digest[4 * i + k] = (uint8_t)(ctx->state[i] >> (8 * k));
+}
+
+/* ------------------------------------------------------------- signature */
+
+/* STORAGE_GEN_FILE_SIGNATURE (storage/storage_service.c:108-120):
+ * long2buff(size) big-endian, then int2buff(h[i]) big-endian x4 for the
+ * hash method, or the 16 raw digest bytes for MD5. */
+void orc_sig_pack(int64_t file_size, int method, const int32_t codes[4],
+                  uint8_t sig[24])
+{
+    uint64_t s = (uint64_t)file_size;
+    for (int i = 0; i < 8; i++)
+        sig[i] = (uint8_t)(s >> (56 - 8 * i));
+    if (method == ORC_METHOD_HASH) {
+        for (int k = 0; k < 4; k++) {
+            uint32_t v = (uint32_t)codes[k];
+            sig[8 + 4 * k] = (uint8_t)(v >> 24);
+            sig[9 + 4 * k] = (uint8_t)(v >> 16);
+            sig[10 + 4 * k] = (uint8_t)(v >> 8);
+            sig[11 + 4 * k] = (uint8_t)v;
+        }
+    } else {
+        memcpy(sig + 8, codes, 16);
+    }
+}
+
+/* -------------------------------------------------------- dio file driver */
+
+/* storage_write_to_file (storage/storage_service.c:7147-7161) initialises
+ * the state, dio_write_file (storage/storage_dio.c:465-483) updates it once
+ * per received chunk, and finalises after the last one (:498-515). */
+void orc_dio_file(const uint8_t *buf, size_t len, size_t chunk, int method,
+                  int variant, uint32_t *crc_out, uint8_t *sig_out,
+                  int32_t *codes_out)
+{
+    int32_t crc = (int32_t)ORC_CRC32_XINIT;
+    int32_t h[4];
+    orc_md5_ctx md5;
+    if (chunk == 0)
+        chunk = len ? len : 1;
+    if (method == ORC_METHOD_HASH)
+        orc_hash4_init(h);
+    else if (method == ORC_METHOD_MD5)
+        orc_md5_init(&md5);
+
+    for (size_t off = 0; off < len; off += chunk) {
+        size_t n = (len - off < chunk) ? (len - off) : chunk;
+        crc = orc_crc32_ex(buf + off, n, crc, variant);
+        if (method == ORC_METHOD_HASH)
+            orc_hash4_calc(buf + off, n, h, variant);
+        else if (method == ORC_METHOD_MD5)
+            orc_md5_update(&md5, buf + off, n);
+    }
+    crc = orc_crc32_final(crc);
+    if (method == ORC_METHOD_HASH)
+        orc_hash4_finish(h);
+    else if (method == ORC_METHOD_MD5)
+        orc_md5_final((uint8_t *)h, &md5);
+
+    if (crc_out)
+        *crc_out = (uint32_t)crc;
+    if (method != ORC_METHOD_CRC_ONLY) {
+        if (sig_out)
+            orc_sig_pack((int64_t)len, method, h, sig_out);
+        if (codes_out)
+            memcpy(codes_out, h, 16);
+    }
+}
+
+typedef struct {
+    const uint8_t *base;
+    const uint64_t *offset, *size;
+    uint64_t n;
+    size_t chunk;
+    int method, variant;
+    uint32_t *crc_out;
+    uint8_t *sig_out;
+    uint64_t next;  /* shared work counter */
+} batch_job;
+
+static void *batch_worker(void *arg)
+{
+    batch_job *j = (batch_job *)arg;
+    for (;;) {
+        uint64_t i = __atomic_fetch_add(&j->next, 1, __ATOMIC_RELAXED);
+        if (i >= j->n)
+            break;
+        orc_dio_file(j->base + j->offset[i], (size_t)j->size[i], j->chunk,
+                     j->method, j->variant, j->crc_out ? j->crc_out + i : NULL,
+                     j->sig_out ? j->sig_out + 24 * i : NULL, NULL);
+    }
+    return NULL;
+}
+
+int orc_dio_batch(const uint8_t *base, const uint64_t *offset,
+                  const uint64_t *size, uint64_t n, size_t chunk, int method,
+                  int variant, uint32_t *crc_out, uint8_t *sig_out,
+                  int nthreads)
+{
+    batch_job j = {base, offset, size, n, chunk, method, variant,
+                   crc_out, sig_out, 0};
+    if (nthreads <= 1) {
+        batch_worker(&j);
+        return 0;
+    }
+    pthread_t *th = (pthread_t *)malloc(sizeof(pthread_t) * (size_t)nthreads);
+    if (!th)
+        return 12;
+    for (int t = 0; t < nthreads; t++)
+        pthread_create(&th[t], NULL, batch_worker, &j);
+    for (int t = 0; t < nthreads; t++)
+        pthread_join(th[t], NULL);
+    free(th);
+    return 0;
+}
+
+/* ------------------------------------------------------ gen_files corpus */
+
+/* test/gen_files.c:14-21 sizes, test/test_types.h:19 seed. */
+static const uint32_t GEN_SIZES[6] = {5 * 1024, 50 * 1024, 200 * 1024,
+                                      1 * 1024 * 1024, 10 * 1024 * 1024,
+                                      100 * 1024 * 1024};
+#define GEN_SRAND_SEED 1225420780u
+#define GEN_BLOCK 1024
+
+uint64_t orc_gen_files_total(void)
+{
+    uint64_t t = 0;
+    for (int i = 0; i < 6; i++)
+        t += GEN_SIZES[i];
+    return t;
+}
+
+/* test/gen_files.c:34,46-64: one glibc rand() stream across all six files;
+ * each file is (bytes/1024 - 1) random 1 KiB blocks, byte =
+ * (int)(255 * ((double)rand() / RAND_MAX)), then one 1 KiB block of 0xFF. */
+void orc_gen_files(uint8_t *out)
+{
+    srand(GEN_SRAND_SEED);
+    uint8_t *p = out;
+    for (int f = 0; f < 6; f++) {
+        int loop = (int)(GEN_SIZES[f] / GEN_BLOCK);
+        for (int k = 0; k < loop - 1; k++)
+            for (int b = 0; b < GEN_BLOCK; b++)
+                *p++ = (uint8_t)(int)(255 * ((double)rand() / RAND_MAX));
+        memset(p, 0xFF, GEN_BLOCK);
+        p += GEN_BLOCK;
+    }
+}
+
+/* ------------------------------------------------------------------ dedup */
+
+static const uint8_t *g_sort_sig;
+
+static int sig_idx_cmp(const void *a, const void *b)
+{
+    uint64_t ia = *(const uint64_t *)a, ib = *(const uint64_t *)b;
+    int c = memcmp(g_sort_sig + 24 * ia, g_sort_sig + 24 * ib, 24);
+    if (c)
+        return c;
+    return (ia > ib) - (ia < ib);
+}
+
+/* Sequential FastDHT semantics of storage_service_upload_file_done
+ * (storage/storage_service.c:2652 get "fid": hit -> link to source;
+ * :2714 miss -> this file becomes the source) and storage_set_link_file_meta
+ * (:2984 fdht_inc "ref" +1 per link): after ingesting all n files in order,
+ * every file links to the first file with its signature and the class's ref
+ * equals its size.  Not thread-safe (qsort comparator global). */
+int orc_dedup(const uint8_t *sig, uint64_t n, uint64_t *rep_out,
+              uint32_t *ref_out)
+{
+    uint64_t *ord = (uint64_t *)malloc(sizeof(uint64_t) * (n ? n : 1));
+    if (!ord)
+        return 12;
+    for (uint64_t i = 0; i < n; i++)
+        ord[i] = i;
+    g_sort_sig = sig;
+    qsort(ord, (size_t)n, sizeof(uint64_t), sig_idx_cmp);
+    uint64_t s = 0;
+    while (s < n) {
+        uint64_t e = s + 1;
+        while (e < n && memcmp(sig + 24 * ord[s], sig + 24 * ord[e], 24) == 0)
+            e++;
+        for (uint64_t k = s; k < e; k++) {
+            rep_out[ord[k]] = ord[s];
+            ref_out[ord[k]] = (uint32_t)(e - s);
+        }
+        s = e;
+    }
+    free(ord);
+    return 0;
+}

@@ -1,0 +1,107 @@
+"""CPU: the multi-rank paths over gloo (world_size 2 and 3).
+
+The exchange logic of fastdfs_amd.dist.dedup_global (counts all-to-all, row
+all-to-all, answers back, routing by row_of) runs for real over gloo; the two
+device kernels it calls are replaced by a CPU test double that follows the
+same contract (bucket rows by owner; group rows by 24-byte key).  The double
+lives here, in tests/, and is never reachable from the product.
+"""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from fastdfs_amd.dist import dedup_global, shard_lpt
+
+
+class CpuKernelsDouble:
+    """Test double of Context.dedup_bucket / dedup_group (owner = first byte mod n)."""
+
+    def dedup_bucket(self, sig, gidx, nranks):
+        sig_np = sig.numpy()
+        own = sig_np[:, 8].astype(np.int64) % nranks
+        order = np.argsort(own, kind="stable")
+        rows = np.zeros((len(sig_np), 32), np.uint8)
+        rows[:, :24] = sig_np[order]
+        rows[:, 24:] = gidx.numpy()[order].astype("<i8").view(np.uint8).reshape(-1, 8)
+        row_of = np.empty(len(sig_np), np.int64)
+        row_of[order] = np.arange(len(sig_np))
+        counts = np.bincount(own, minlength=nranks).astype(np.int64)
+        return torch.from_numpy(rows), torch.from_numpy(counts), torch.from_numpy(row_of)
+
+    def dedup_group(self, rows):
+        r = rows.numpy()
+        g = r[:, 24:].copy().view("<i8").reshape(-1)
+        keys = [bytes(x) for x in r[:, :24]]
+        mins, cnt = {}, {}
+        for k, gi in zip(keys, g):
+            mins[k] = min(mins.get(k, 1 << 62), int(gi))
+            cnt[k] = cnt.get(k, 0) + 1
+        return (torch.tensor([mins[k] for k in keys], dtype=torch.int64),
+                torch.tensor([cnt[k] for k in keys], dtype=torch.int32))
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, world, port, sig_all, out_q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        shards = np.array_split(np.arange(len(sig_all)), world)
+        mine = shards[rank]
+        sig = torch.from_numpy(sig_all[mine].copy())
+        gidx = torch.from_numpy(mine.astype(np.int64))
+        rep, ref = dedup_global(CpuKernelsDouble(), sig, gidx)
+        out_q.put((rank, rep.numpy(), ref.numpy()))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_dedup_global_gloo(oracle, world):
+    rng = np.random.default_rng(world)
+    base = rng.integers(0, 256, size=(300, 24), dtype=np.uint8)
+    sig_all = base[rng.integers(0, 300, size=2000)]
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, sig_all, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    got = dict((r, (rep, ref)) for r, rep, ref in (q.get(timeout=120) for _ in range(world)))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    orep, oref = oracle.dedup(sig_all)
+    shards = np.array_split(np.arange(len(sig_all)), world)
+    for r in range(world):
+        assert np.array_equal(got[r][0], orep[shards[r]].astype(np.int64))
+        assert np.array_equal(got[r][1], oref[shards[r]].astype(np.int32))
+
+
+def test_shard_lpt_balances_and_covers():
+    rng = np.random.default_rng(0)
+    sizes = rng.integers(4096, 1 << 20, size=5000)
+    parts = shard_lpt(sizes, 8)
+    allidx = np.concatenate(parts)
+    assert np.array_equal(np.sort(allidx), np.arange(5000))
+    loads = [sizes[p].sum() for p in parts]
+    assert max(loads) / min(loads) < 1.01
+    for p in parts:
+        assert np.all(np.diff(p) > 0)
+
+
+def test_shard_lpt_huge_file_alone():
+    parts = shard_lpt(np.array([1 << 30, 10, 10, 10]), 2)
+    assert [len(p) for p in parts] in ([1, 3], [3, 1])
