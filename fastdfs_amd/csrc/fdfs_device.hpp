@@ -56,6 +56,17 @@ __device__ __forceinline__ uint32_t apply4(const uint32_t *__restrict__ A, uint3
            (A[512 + ((v >> 16) & 0xFFu)] ^ A[768 + (v >> 24)]);
 }
 
+// (a << SH) + b as one full-rate v_lshl_add_u32.  Written as asm because
+// hipcc otherwise folds 31*h + b / 33*h + b into v_mad_u64_u32 (a 64-bit
+// multiply at a fraction of the VALU rate that also takes register pairs).
+template <int SH>
+__device__ __forceinline__ uint32_t lshl_add(uint32_t a, uint32_t b)
+{
+    uint32_t r;
+    asm("v_lshl_add_u32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "i"(SH), "v"(b));
+    return r;
+}
+
 // ELFHash_ex / simple_hash_ex / Time33Hash_ex byte steps (the h[1..3] of
 // CALC_HASH_CODES4, storage/storage_dio.c:475).
 template <bool SAR>
@@ -65,8 +76,8 @@ __device__ __forceinline__ void h3_byte(uint32_t b, uint32_t &e, uint32_t &s, ui
     const uint32_t x = e & 0xF0000000u;
     e ^= SAR ? (uint32_t)((int32_t)x >> 24) : (x >> 24);
     e &= ~x;
-    s = (s << 5) - s + b;
-    t = (t << 5) + t + b;
+    s = lshl_add<5>(s, b) - s;  // 31*s + b
+    t = lshl_add<5>(t, t) + b;  // 33*t + b
 }
 
 template <bool SAR>

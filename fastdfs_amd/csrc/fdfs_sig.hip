@@ -168,46 +168,26 @@ __global__ __launch_bounds__(256) void sig_lane_kernel(
         }
         const uint4 *v = reinterpret_cast<const uint4 *>(p + head);
         const uint64_t nvec = (L - head) >> 4;
-        uint64_t j = 0;
-        if (nvec >= 4) {
-            uint4 a0 = v[0], a1 = v[1], a2 = v[2], a3 = v[3];
-            for (; j + 4 <= nvec; j += 4) {
-                // prefetch the next 64 B (clamped: the last group reloads itself)
-                const uint64_t nx = (j + 8 <= nvec) ? j + 4 : j;
-                const uint4 b0 = v[nx], b1 = v[nx + 1], b2 = v[nx + 2], b3 = v[nx + 3];
-                c = chain16<SAR>(sD, c, a0, K16);
-                h3_word<SAR>(a0.x, e, s, t);
-                h3_word<SAR>(a0.y, e, s, t);
-                h3_word<SAR>(a0.z, e, s, t);
-                h3_word<SAR>(a0.w, e, s, t);
-                c = chain16<SAR>(sD, c, a1, K16);
-                h3_word<SAR>(a1.x, e, s, t);
-                h3_word<SAR>(a1.y, e, s, t);
-                h3_word<SAR>(a1.z, e, s, t);
-                h3_word<SAR>(a1.w, e, s, t);
-                c = chain16<SAR>(sD, c, a2, K16);
-                h3_word<SAR>(a2.x, e, s, t);
-                h3_word<SAR>(a2.y, e, s, t);
-                h3_word<SAR>(a2.z, e, s, t);
-                h3_word<SAR>(a2.w, e, s, t);
-                c = chain16<SAR>(sD, c, a3, K16);
-                h3_word<SAR>(a3.x, e, s, t);
-                h3_word<SAR>(a3.y, e, s, t);
-                h3_word<SAR>(a3.z, e, s, t);
-                h3_word<SAR>(a3.w, e, s, t);
-                a0 = b0;
-                a1 = b1;
-                a2 = b2;
-                a3 = b3;
+        if (nvec) {
+            // 16 B per step, loads running kLanePrefetch vectors ahead (the
+            // index is clamped so the tail re-reads the last vector: no
+            // conditional loads in the loop).
+            const uint64_t last = nvec - 1;
+            uint4 q0 = v[0];
+            uint4 q1 = v[last < 1 ? last : 1];
+            uint4 q2 = v[last < 2 ? last : 2];
+            for (uint64_t j = 0; j < nvec; j++) {
+                const uint64_t nj = j + 3;
+                const uint4 q3 = v[nj < last ? nj : last];
+                c = chain16<SAR>(sD, c, q0, K16);
+                h3_word<SAR>(q0.x, e, s, t);
+                h3_word<SAR>(q0.y, e, s, t);
+                h3_word<SAR>(q0.z, e, s, t);
+                h3_word<SAR>(q0.w, e, s, t);
+                q0 = q1;
+                q1 = q2;
+                q2 = q3;
             }
-        }
-        for (; j < nvec; j++) {
-            const uint4 a = v[j];
-            c = chain16<SAR>(sD, c, a, K16);
-            h3_word<SAR>(a.x, e, s, t);
-            h3_word<SAR>(a.y, e, s, t);
-            h3_word<SAR>(a.z, e, s, t);
-            h3_word<SAR>(a.w, e, s, t);
         }
         for (uint64_t k = head + (nvec << 4); k < L; k++) {
             const uint32_t b = p[k];
@@ -292,59 +272,86 @@ __global__ __launch_bounds__(256) void sig_lane_kernel(
 
 // ------------------------------------------------------- segmented CRC path
 
-// Bytes at addresses [lo, lo+4) of the file's segment 0 are XOR 0xFF for the
-// unsigned variant; bytes below `valid` are replaced by the neutral byte.
+// 0xFF in every byte of the dword at byte offset `off` that lies in [lo, hi).
+__device__ __forceinline__ uint32_t byte_range_mask(int64_t off, int64_t lo, int64_t hi)
+{
+    const int64_t a = lo - off < 0 ? 0 : lo - off;
+    const int64_t b = hi - off > 4 ? 4 : hi - off;
+    if (b <= a)
+        return 0;
+    const uint32_t upto_b = b >= 4 ? 0xFFFFFFFFu : ((1u << (8 * b)) - 1u);
+    const uint32_t upto_a = (1u << (8 * a)) - 1u;  // a < 4 here
+    return upto_b & ~upto_a;
+}
+
+// First vector(s) of a segment: bytes before the segment start (offset a0)
+// become the neutral byte (0xFF in the complemented SAR domain, 0 otherwise);
+// for the unsigned variant the file's bytes 0..3 are XOR 0xFF (the XINIT
+// identity, DESIGN.md "K2 segmented CRC").
 template <bool SAR>
-__device__ __noinline__ uint4 seg_fix_vector(uint4 w, uintptr_t va, uintptr_t valid, bool xor4)
+__device__ __forceinline__ uint4 seg_fix_vector(uint4 w, int64_t off, int64_t a0, bool xor4)
 {
     uint32_t d[4] = {w.x, w.y, w.z, w.w};
 #pragma unroll
-    for (int i = 0; i < 16; i++) {
-        const uintptr_t a = va + i;
-        const uint32_t sh = 8 * (i & 3);
-        uint32_t b = (d[i >> 2] >> sh) & 0xFFu;
-        if (a < valid)
-            b = SAR ? 0xFFu : 0u;
-        else if (!SAR && xor4 && a < valid + 4)
-            b ^= 0xFFu;
-        d[i >> 2] = (d[i >> 2] & ~(0xFFu << sh)) | (b << sh);
+    for (int k = 0; k < 4; k++) {
+        const int64_t o = off + 4 * k;
+        const uint32_t inv = byte_range_mask(o, INT64_MIN / 2, a0);
+        d[k] = SAR ? (d[k] | inv) : (d[k] & ~inv);
+        if (!SAR && xor4)
+            d[k] ^= byte_range_mask(o, a0, a0 + 4);
     }
     return make_uint4(d[0], d[1], d[2], d[3]);
 }
 
-// Zero-init CRC state of the (masked) bytes [A, E) of one segment, computed
-// by the whole wave.  See DESIGN.md "K2 segmented CRC" for the algebra.
+// Zero-init CRC state of the (masked) bytes [Ap, Ap+len) of one segment,
+// computed by the whole wave.  Vectors are 16-byte aligned in memory and the
+// 4 KiB block grid is aligned to the segment's last full vector, so the only
+// partial vector is the first (leading neutral bytes do not change a
+// zero-init state).  See DESIGN.md "K2 segmented CRC" for the algebra.
 template <bool SAR>
 __device__ __forceinline__ uint32_t crc_segment(const uint32_t *sD, const uint32_t *sT,
                                                 const uint32_t *sA, const uint32_t *sR,
-                                                uint32_t K16, const uint8_t *Ap, const uint8_t *Ep,
+                                                uint32_t K16, const uint8_t *Ap, uint64_t len,
                                                 bool first_seg, int lane)
 {
-    const uintptr_t A = (uintptr_t)Ap, E = (uintptr_t)Ep;
-    const uintptr_t s16 = A & ~(uintptr_t)15, e16 = E & ~(uintptr_t)15;
+    const int64_t a0 = (int64_t)((uintptr_t)Ap & 15u);  // segment start within its vector
+    const uint4 *v = reinterpret_cast<const uint4 *>(Ap - a0);
+    const int64_t e_off = a0 + (int64_t)len;
+    const int64_t nvec = e_off >> 4;  // full vectors ending at or before the end
     const bool xor4 = !SAR && first_seg;
     uint32_t state = 0;
-    if (e16 > s16) {
-        const int64_t nvec = (int64_t)((e16 - s16) >> 4);
+    if (nvec > 0) {
         const int64_t J = (nvec + 255) >> 8;
-        const uint4 *v = reinterpret_cast<const uint4 *>(s16);
         const uint4 neutral = SAR ? make_uint4(~0u, ~0u, ~0u, ~0u) : make_uint4(0, 0, 0, 0);
         uint32_t acc = 0;
-        for (int64_t jb = 0; jb < J; jb++) {
-            const int64_t vb = nvec - 256 * (J - jb) + 4 * lane;
+        {  // first (partial) block: vectors before index 0 are neutral
+            const int64_t vb = nvec - 256 * J + 4 * lane;
+            uint4 w[4];
+#pragma unroll
+            for (int q = 0; q < 4; q++) {
+                const int64_t vi = vb + q;
+                w[q] = v[vi < 0 ? 0 : vi];
+                if (vi < 0)
+                    w[q] = neutral;
+                else if (16 * vi < a0 + 4)
+                    w[q] = seg_fix_vector<SAR>(w[q], 16 * vi, a0, xor4);
+            }
+#pragma unroll
+            for (int q = 0; q < 4; q++)
+                acc = chain16<SAR>(sD, acc, w[q], K16);
+        }
+        for (int64_t jb = 1; jb < J; jb++) {
+            const uint4 *vp = v + (nvec - 256 * (J - jb) + 4 * lane);
             uint4 w[4];
 #pragma unroll
             for (int q = 0; q < 4; q++)
-                w[q] = (vb + q >= 0) ? v[vb + q] : neutral;
-            if (jb)
-                acc = apply4(sA, acc);  // advance 4032 B to this lane's next piece
+                w[q] = vp[q];
+            acc = apply4(sA, acc);  // advance 4032 B to this lane's next piece
+            if (jb == 1 && nvec - 256 * (J - 1) == 1 && lane == 0)
+                w[0] = seg_fix_vector<SAR>(w[0], 16, a0, xor4);  // vector 1 opens block 1
 #pragma unroll
-            for (int q = 0; q < 4; q++) {
-                const uintptr_t va = s16 + 16 * (uintptr_t)(vb + q);
-                if (vb + q >= 0 && va < A + 4)
-                    w[q] = seg_fix_vector<SAR>(w[q], va, A, xor4);
+            for (int q = 0; q < 4; q++)
                 acc = chain16<SAR>(sD, acc, w[q], K16);
-            }
         }
         // wave reduction: lane group values relative to the group's end
 #pragma unroll
@@ -356,9 +363,10 @@ __device__ __forceinline__ uint32_t crc_segment(const uint32_t *sD, const uint32
         }
         state = __shfl(acc, 63);
     }
-    for (uintptr_t a = (e16 > A ? e16 : A); a < E; a++) {
-        uint32_t b = *reinterpret_cast<const uint8_t *>(a);
-        if (SAR || (xor4 && a < A + 4))
+    const int64_t t0 = (16 * nvec > a0) ? 16 * nvec : a0;
+    for (int64_t o = t0; o < e_off; o++) {
+        uint32_t b = Ap[o - a0];
+        if (SAR || (xor4 && o < a0 + 4))
             b ^= 0xFFu;
         state = crc_byte<SAR>(sT, state, b);
     }
@@ -418,7 +426,7 @@ __global__ __launch_bounds__(512) void crc_seg_kernel(
         const uint8_t *fp = base + offs[f];
         const uint64_t lo_b = k * kSegBytes;
         const uint64_t hi_b = (L < lo_b + kSegBytes) ? L : lo_b + kSegBytes;
-        uint32_t v = crc_segment<SAR>(sD, sT, sA, sR, K16, fp + lo_b, fp + hi_b, k == 0, lane);
+        uint32_t v = crc_segment<SAR>(sD, sT, sA, sR, K16, fp + lo_b, hi_b - lo_b, k == 0, lane);
         if (nseg == 1) {
             if (lane == 0)
                 crc_out[f] = v ^ crc_final_const<SAR>(L);

@@ -90,11 +90,11 @@ def test_gen_files_corpus(oracle, ctxs, corpus, kat, variant):
     assert ["%08X" % c for c in crc] == kat["corpus"][key]
     crc1, sig1, codes1 = _gpu(ctx, dev_batch, 1)
     assert np.array_equal(crc1, crc)
-    assert ["%08X" % (c & 0xFFFFFFFF) for c in codes1[:, 2]] == kat["corpus"]["simple"]
-    assert ["%08X" % (c & 0xFFFFFFFF) for c in codes1[:, 3]] == kat["corpus"]["time33"]
+    assert ["%08X" % (int(c) & 0xFFFFFFFF) for c in codes1[:, 2]] == kat["corpus"]["simple"]
+    assert ["%08X" % (int(c) & 0xFFFFFFFF) for c in codes1[:, 3]] == kat["corpus"]["time33"]
     elf = kat["corpus"]["elf_signed" if variant == 0 else "elf_unsigned"]
     for i, v in elf.items():
-        assert "%08X" % (codes1[int(i), 1] & 0xFFFFFFFF) == v
+        assert "%08X" % (int(codes1[int(i), 1]) & 0xFFFFFFFF) == v
     crc2, sig2, _ = _gpu(ctx, dev_batch, 2)
     assert np.array_equal(crc2, crc)
     assert [bytes(s[8:]).hex() for s in sig2] == kat["corpus"]["md5"]
