@@ -181,6 +181,13 @@ int fdfs_gpu_open(int device, unsigned flags, fdfs_gpu_ctx **out)
     for (int p = 0; p < 16; p++)
         for (int x = 0; x < 256; x++)
             h->Dc[p][x] = h->t.D[p][x ^ 0xFF];
+    for (int p = 0; p < 16; p++)
+        for (int x = 0; x < 16; x++) {
+            h->N[2 * p][x] = h->t.D[p][x];
+            h->N[2 * p + 1][x] = h->t.D[p][x << 4];
+            h->Nc[2 * p][x] = h->Dc[p][x];
+            h->Nc[2 * p + 1][x] = h->Dc[p][x << 4] ^ h->Dc[p][0];
+        }
     hipError_t e = hipMalloc(&ctx->d_tabs, sizeof(fdfs::DevTables));
     if (e == hipSuccess)
         e = hipMemcpy(ctx->d_tabs, h, sizeof(fdfs::DevTables), hipMemcpyHostToDevice);

@@ -12,7 +12,45 @@ namespace fdfs {
 struct DevTables {
     CrcTables t;
     uint32_t Dc[16][256];   // Dc[p][x] = D[p][x ^ 0xFF]
+    // nibble form of D / Dc: N[2p+h][x] = D[p][x << 4h]; replicated 32x per
+    // lane bank in LDS by the kernels (conflict-free lookups)
+    uint32_t N[32][16];
+    uint32_t Nc[32][16];
 };
+
+constexpr int kNibTables = 32;
+constexpr int kNibDwords = kNibTables * 16 * 32;  // 64 KiB of LDS
+
+// Fill the lane-bank-replicated nibble tables: dword t*512 + x*32 + r = src[t][x].
+__device__ __forceinline__ void lds_fill_nib(uint32_t *dst, const uint32_t *__restrict__ src)
+{
+    for (int i = threadIdx.x; i < kNibDwords; i += blockDim.x)
+        dst[i] = src[(i >> 9) * 16 + ((i >> 5) & 15)];
+}
+
+// chain16 through the replicated nibble tables: lane l reads only bank l%32.
+// lb = (lane & 31) * 4.  32 lookups per 16 bytes, no bank conflicts.
+template <bool SAR>
+__device__ __forceinline__ uint32_t chain16n(const uint32_t *sN, uint32_t lb, uint32_t c, uint4 w,
+                                             uint32_t K16)
+{
+    const char *base = reinterpret_cast<const char *>(sN);
+    const uint32_t x = c ^ w.x;
+    const uint32_t words[4] = {x, w.y, w.z, w.w};
+    uint32_t r[4] = {0, 0, 0, 0};
+#pragma unroll
+    for (int wi = 0; wi < 4; wi++) {
+#pragma unroll
+        for (int k = 0; k < 8; k++) {
+            const uint32_t a = (((words[wi] >> (4 * k)) & 0xFu) << 7) | lb;
+            r[k & 3] ^= *reinterpret_cast<const uint32_t *>(base + a + (wi * 8 + k) * 2048);
+        }
+    }
+    uint32_t v = (r[0] ^ r[1]) ^ (r[2] ^ r[3]);
+    if (SAR)
+        v ^= (uint32_t)((int32_t)c >> 31) & K16;
+    return v;
+}
 
 constexpr int kWave = 64;
 

@@ -23,6 +23,7 @@ hipError_t launch_crc_seg(bool sar, const uint8_t *base, const uint64_t *offs, c
                           const DevTables *tabs, uint32_t *crc_out, unsigned grid, hipStream_t st,
                           hipEvent_t ev0, hipEvent_t ev1);
 int crc_seg_blocks_per_cu();
+bool crc_tables_nibble();
 
 // dedup path (fdfs_dedup.hip)
 uint64_t dedup_table_slots(uint64_t n);

@@ -19,6 +19,8 @@
 #include "fdfs_device.hpp"
 #include "fdfs_kernels.hpp"
 
+#include <cstdlib>
+
 namespace fdfs {
 
 // ----------------------------------------------------------------- MD5 core
@@ -134,7 +136,19 @@ __device__ __forceinline__ void store_sig(uint8_t *sig, uint64_t L, uint32_t w2,
 
 // ------------------------------------------------------- lane-per-file path
 
-template <bool SAR, int METHOD>
+// One 16-byte vector through all four CALC_HASH_CODES4 hashes.
+template <bool SAR>
+__device__ __forceinline__ void h4_vec(const uint32_t *sD, uint32_t K16, uint4 q, uint32_t &c,
+                                       uint32_t &e, uint32_t &s, uint32_t &t)
+{
+    c = chain16<SAR>(sD, c, q, K16);
+    h3_word<SAR>(q.x, e, s, t);
+    h3_word<SAR>(q.y, e, s, t);
+    h3_word<SAR>(q.z, e, s, t);
+    h3_word<SAR>(q.w, e, s, t);
+}
+
+template <bool SAR, int METHOD, int VAR>
 __global__ __launch_bounds__(256) void sig_lane_kernel(
     const uint8_t *__restrict__ base, const uint64_t *__restrict__ offs,
     const uint64_t *__restrict__ sizes, const uint32_t *__restrict__ order, uint32_t n,
@@ -168,27 +182,56 @@ __global__ __launch_bounds__(256) void sig_lane_kernel(
         }
         const uint4 *v = reinterpret_cast<const uint4 *>(p + head);
         const uint64_t nvec = (L - head) >> 4;
-        if (nvec) {
-            // 16 B per step, loads running kLanePrefetch vectors ahead (the
-            // index is clamped so the tail re-reads the last vector: no
-            // conditional loads in the loop).
-            const uint64_t last = nvec - 1;
-            uint4 q0 = v[0];
-            uint4 q1 = v[last < 1 ? last : 1];
-            uint4 q2 = v[last < 2 ? last : 2];
-            for (uint64_t j = 0; j < nvec; j++) {
-                const uint64_t nj = j + 3;
-                const uint4 q3 = v[nj < last ? nj : last];
-                c = chain16<SAR>(sD, c, q0, K16);
-                h3_word<SAR>(q0.x, e, s, t);
-                h3_word<SAR>(q0.y, e, s, t);
-                h3_word<SAR>(q0.z, e, s, t);
-                h3_word<SAR>(q0.w, e, s, t);
-                q0 = q1;
-                q1 = q2;
-                q2 = q3;
+        uint64_t j = 0;
+        if constexpr (VAR == 0) {
+            if (nvec) {
+                // 16 B per step, loads running 3 vectors ahead (the index is
+                // clamped so the tail re-reads the last vector: no
+                // conditional loads in the loop).
+                const uint64_t last = nvec - 1;
+                uint4 q0 = v[0];
+                uint4 q1 = v[last < 1 ? last : 1];
+                uint4 q2 = v[last < 2 ? last : 2];
+                for (; j < nvec; j++) {
+                    const uint64_t nj = j + 3;
+                    const uint4 q3 = v[nj < last ? nj : last];
+                    h4_vec<SAR>(sD, K16, q0, c, e, s, t);
+                    q0 = q1;
+                    q1 = q2;
+                    q2 = q3;
+                }
+            }
+        } else if constexpr (VAR == 1) {
+            // 64 B per step, the next 64 B loaded while this one is hashed
+            if (nvec >= 4) {
+                uint4 a0 = v[0], a1 = v[1], a2 = v[2], a3 = v[3];
+                for (; j + 4 <= nvec; j += 4) {
+                    const uint64_t nx = (j + 8 <= nvec) ? j + 4 : j;
+                    const uint4 b0 = v[nx], b1 = v[nx + 1], b2 = v[nx + 2], b3 = v[nx + 3];
+                    h4_vec<SAR>(sD, K16, a0, c, e, s, t);
+                    h4_vec<SAR>(sD, K16, a1, c, e, s, t);
+                    h4_vec<SAR>(sD, K16, a2, c, e, s, t);
+                    h4_vec<SAR>(sD, K16, a3, c, e, s, t);
+                    a0 = b0;
+                    a1 = b1;
+                    a2 = b2;
+                    a3 = b3;
+                }
+            }
+        } else {
+            // 128 B (one cache line) per step, no register prefetch
+            for (; j + 8 <= nvec; j += 8) {
+                uint4 a[8];
+#pragma unroll
+                for (int q = 0; q < 8; q++)
+                    a[q] = v[j + q];
+#pragma unroll
+                for (int q = 0; q < 8; q++)
+                    h4_vec<SAR>(sD, K16, a[q], c, e, s, t);
             }
         }
+        for (; j < nvec; j++)
+            h4_vec<SAR>(sD, K16, v[j], c, e, s, t);
         for (uint64_t k = head + (nvec << 4); k < L; k++) {
             const uint32_t b = p[k];
             c = crc_byte<SAR>(sT, c, b);
@@ -308,12 +351,23 @@ __device__ __forceinline__ uint4 seg_fix_vector(uint4 w, int64_t off, int64_t a0
 // 4 KiB block grid is aligned to the segment's last full vector, so the only
 // partial vector is the first (leading neutral bytes do not change a
 // zero-init state).  See DESIGN.md "K2 segmented CRC" for the algebra.
-template <bool SAR>
+template <bool SAR, bool NIB>
+__device__ __forceinline__ uint32_t chain16x(const uint32_t *sD, uint32_t lb, uint32_t c, uint4 w,
+                                             uint32_t K16)
+{
+    if constexpr (NIB)
+        return chain16n<SAR>(sD, lb, c, w, K16);
+    else
+        return chain16<SAR>(sD, c, w, K16);
+}
+
+template <bool SAR, bool NIB>
 __device__ __forceinline__ uint32_t crc_segment(const uint32_t *sD, const uint32_t *sT,
                                                 const uint32_t *sA, const uint32_t *sR,
                                                 uint32_t K16, const uint8_t *Ap, uint64_t len,
                                                 bool first_seg, int lane)
 {
+    const uint32_t lb = (uint32_t)(lane & 31) * 4u;
     const int64_t a0 = (int64_t)((uintptr_t)Ap & 15u);  // segment start within its vector
     const uint4 *v = reinterpret_cast<const uint4 *>(Ap - a0);
     const int64_t e_off = a0 + (int64_t)len;
@@ -338,20 +392,33 @@ __device__ __forceinline__ uint32_t crc_segment(const uint32_t *sD, const uint32
             }
 #pragma unroll
             for (int q = 0; q < 4; q++)
-                acc = chain16<SAR>(sD, acc, w[q], K16);
+                acc = chain16x<SAR, NIB>(sD, lb, acc, w[q], K16);
+        }
+        // blocks 1..J-1: the next block's 64 B per lane is loaded while this
+        // one is folded (index clamped on the last block: no branch)
+        uint4 nx[4];
+        if (J > 1) {
+            const uint4 *vp = v + (nvec - 256 * (J - 1) + 4 * lane);
+#pragma unroll
+            for (int q = 0; q < 4; q++)
+                nx[q] = vp[q];
         }
         for (int64_t jb = 1; jb < J; jb++) {
-            const uint4 *vp = v + (nvec - 256 * (J - jb) + 4 * lane);
             uint4 w[4];
 #pragma unroll
             for (int q = 0; q < 4; q++)
-                w[q] = vp[q];
+                w[q] = nx[q];
+            const int64_t jn = (jb + 1 < J) ? jb + 1 : jb;
+            const uint4 *vp = v + (nvec - 256 * (J - jn) + 4 * lane);
+#pragma unroll
+            for (int q = 0; q < 4; q++)
+                nx[q] = vp[q];
             acc = apply4(sA, acc);  // advance 4032 B to this lane's next piece
             if (jb == 1 && nvec - 256 * (J - 1) == 1 && lane == 0)
                 w[0] = seg_fix_vector<SAR>(w[0], 16, a0, xor4);  // vector 1 opens block 1
 #pragma unroll
             for (int q = 0; q < 4; q++)
-                acc = chain16<SAR>(sD, acc, w[q], K16);
+                acc = chain16x<SAR, NIB>(sD, lb, acc, w[q], K16);
         }
         // wave reduction: lane group values relative to the group's end
 #pragma unroll
@@ -382,20 +449,27 @@ __device__ __forceinline__ uint32_t crc_final_const(uint64_t L)
     return 0xFFFFFFFFu ^ (L < 4 ? (0xFFFFFFFFu >> (8 * (uint32_t)L)) : 0u);
 }
 
-template <bool SAR>
+template <bool SAR, bool NIB>
 __global__ __launch_bounds__(512) void crc_seg_kernel(
     const uint8_t *__restrict__ base, const uint64_t *__restrict__ offs,
     const uint64_t *__restrict__ sizes, const uint64_t *__restrict__ seg_first, uint32_t n,
     const DevTables *__restrict__ tabs, uint32_t *__restrict__ crc_out)
 {
-    __shared__ uint32_t sD[16 * 256];
-    __shared__ uint32_t sT[256];
-    __shared__ uint32_t sA[4 * 256];
-    __shared__ uint32_t sR[6 * 4 * 256];
-    lds_fill(sD, SAR ? &tabs->Dc[0][0] : &tabs->t.D[0][0], 16 * 256);
+    // NIB: lane-bank-replicated nibble tables (64 KiB), the reduction tables
+    // stay in global memory (24 lookups per segment).  !NIB: 8-bit tables.
+    constexpr int kD = NIB ? kNibDwords : 16 * 256;
+    constexpr int kR = NIB ? 0 : 6 * 4 * 256;
+    __shared__ uint32_t smem[kD + 256 + 4 * 256 + kR];
+    uint32_t *sD = smem, *sT = smem + kD, *sA = sT + 256;
+    const uint32_t *sR = NIB ? &tabs->t.ADVRED[0][0][0] : sA + 1024;
+    if constexpr (NIB)
+        lds_fill_nib(sD, SAR ? &tabs->Nc[0][0] : &tabs->N[0][0]);
+    else
+        lds_fill(sD, SAR ? &tabs->Dc[0][0] : &tabs->t.D[0][0], 16 * 256);
     lds_fill(sT, tabs->t.T, 256);
     lds_fill(sA, &tabs->t.ADV4032[0][0], 4 * 256);
-    lds_fill(sR, &tabs->t.ADVRED[0][0][0], 6 * 4 * 256);
+    if constexpr (!NIB)
+        lds_fill(sA + 1024, &tabs->t.ADVRED[0][0][0], 6 * 4 * 256);
     __syncthreads();
 
     const uint32_t K16 = tabs->t.K16;
@@ -426,7 +500,7 @@ __global__ __launch_bounds__(512) void crc_seg_kernel(
         const uint8_t *fp = base + offs[f];
         const uint64_t lo_b = k * kSegBytes;
         const uint64_t hi_b = (L < lo_b + kSegBytes) ? L : lo_b + kSegBytes;
-        uint32_t v = crc_segment<SAR>(sD, sT, sA, sR, K16, fp + lo_b, hi_b - lo_b, k == 0, lane);
+        uint32_t v = crc_segment<SAR, NIB>(sD, sT, sA, sR, K16, fp + lo_b, hi_b - lo_b, k == 0, lane);
         if (nseg == 1) {
             if (lane == 0)
                 crc_out[f] = v ^ crc_final_const<SAR>(L);
@@ -654,18 +728,34 @@ hipError_t launch_sig_lane(bool sar, int method, const uint8_t *base, const uint
     const unsigned g = (n + 255) / 256;
     if (ev0)
         (void)hipEventRecord(ev0, st);
-#define LANE_LAUNCH(S, M) \
-    sig_lane_kernel<S, M><<<g, 256, 0, st>>>(base, offs, sizes, order, n, tabs, crc_out, sig_out, codes_out)
-    if (sar) {
-        if (method == 1)
-            LANE_LAUNCH(true, 1);
+#define LANE_LAUNCH(S, M, V) \
+    sig_lane_kernel<S, M, V><<<g, 256, 0, st>>>(base, offs, sizes, order, n, tabs, crc_out, sig_out, codes_out)
+    static int var = -1;
+    if (var < 0) {  // FDFS_GPU_LANE_VARIANT: A/B of the hash-path load schedule
+        const char *ev = getenv("FDFS_GPU_LANE_VARIANT");
+        var = ev ? (ev[0] - '0') : 2;
+        if (var < 0 || var > 2)
+            var = 1;
+    }
+    if (method == 2) {
+        if (sar)
+            LANE_LAUNCH(true, 2, 0);
         else
-            LANE_LAUNCH(true, 2);
+            LANE_LAUNCH(false, 2, 0);
+    } else if (sar) {
+        if (var == 0)
+            LANE_LAUNCH(true, 1, 0);
+        else if (var == 1)
+            LANE_LAUNCH(true, 1, 1);
+        else
+            LANE_LAUNCH(true, 1, 2);
     } else {
-        if (method == 1)
-            LANE_LAUNCH(false, 1);
+        if (var == 0)
+            LANE_LAUNCH(false, 1, 0);
+        else if (var == 1)
+            LANE_LAUNCH(false, 1, 1);
         else
-            LANE_LAUNCH(false, 2);
+            LANE_LAUNCH(false, 1, 2);
     }
 #undef LANE_LAUNCH
     if (ev1)
@@ -684,19 +774,39 @@ hipError_t launch_crc_seg(bool sar, const uint8_t *base, const uint64_t *offs, c
         return e;
     if (ev0)
         (void)hipEventRecord(ev0, st);
-    if (sar)
-        crc_seg_kernel<true><<<grid, 512, 0, st>>>(base, offs, sizes, seg_first, n, tabs, crc_out);
+    const bool nib = crc_tables_nibble();
+    if (sar && nib)
+        crc_seg_kernel<true, true><<<grid, 512, 0, st>>>(base, offs, sizes, seg_first, n, tabs, crc_out);
+    else if (sar)
+        crc_seg_kernel<true, false><<<grid, 512, 0, st>>>(base, offs, sizes, seg_first, n, tabs, crc_out);
+    else if (nib)
+        crc_seg_kernel<false, true><<<grid, 512, 0, st>>>(base, offs, sizes, seg_first, n, tabs, crc_out);
     else
-        crc_seg_kernel<false><<<grid, 512, 0, st>>>(base, offs, sizes, seg_first, n, tabs, crc_out);
+        crc_seg_kernel<false, false><<<grid, 512, 0, st>>>(base, offs, sizes, seg_first, n, tabs, crc_out);
     if (ev1)
         (void)hipEventRecord(ev1, st);
     return hipGetLastError();
 }
 
+// Table form of the segmented CRC kernel: 8-bit (default) or nibble.
+// FDFS_GPU_CRC_TABLES=nib selects the nibble tables (A/B measurement only).
+bool crc_tables_nibble()
+{
+    static int v = -1;
+    if (v < 0) {
+        const char *e = getenv("FDFS_GPU_CRC_TABLES");
+        v = (e && e[0] == 'n') ? 1 : 0;
+    }
+    return v == 1;
+}
+
 int crc_seg_blocks_per_cu()
 {
     int nb = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, crc_seg_kernel<true>, 512, 0) != hipSuccess)
+    hipError_t e = crc_tables_nibble()
+                       ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, crc_seg_kernel<true, true>, 512, 0)
+                       : hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, crc_seg_kernel<true, false>, 512, 0);
+    if (e != hipSuccess)
         return 1;
     return nb > 0 ? nb : 1;
 }
