@@ -52,6 +52,60 @@ __device__ __forceinline__ uint32_t chain16n(const uint32_t *sN, uint32_t lb, ui
     return v;
 }
 
+// ---- nibble tables addressed with one v_perm_b32 per lookup ------------
+// Layout (64 KiB): table pair q = t/2 occupies 4 KiB; entry x of table t,
+// replica r (= lane % 32) sits at byte q*4096 + x*256 + (t&1)*128 + r*4.
+// Every lane reads only its own bank, and the address lb + (nibble << 8) is a
+// single byte permute of {nibble byte, lb byte}: v_perm_b32(v, lb, sel).
+constexpr int kNibPDwords = 16 * 1024;
+
+__device__ __forceinline__ void lds_fill_nibp(uint32_t *dst, const uint32_t *__restrict__ src)
+{
+    for (int i = threadIdx.x; i < kNibPDwords; i += blockDim.x) {
+        const int q = i >> 10, x = (i >> 6) & 15, h = (i >> 5) & 1;
+        dst[i] = src[(2 * q + h) * 16 + x];
+    }
+}
+
+// a ^ b ^ c in one VALU op (gfx950 v_bitop3_b32, truth table 0x96).
+__device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c)
+{
+    uint32_t r;
+    asm("v_bitop3_b32 %0, %1, %2, %3 bitop3:0x96" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+    return r;
+}
+
+template <bool SAR>
+__device__ __forceinline__ uint32_t chain16p(const uint32_t *sN, uint32_t lb, uint32_t c, uint4 w,
+                                             uint32_t K16)
+{
+    const char *base = reinterpret_cast<const char *>(sN);
+    const uint32_t words[4] = {c ^ w.x, w.y, w.z, w.w};
+    uint32_t r0 = 0, r1 = 0;
+#pragma unroll
+    for (int wi = 0; wi < 4; wi++) {
+        const uint32_t lo = words[wi] & 0x0F0F0F0Fu;
+        const uint32_t hi = (words[wi] >> 4) & 0x0F0F0F0Fu;
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+            const int p = 4 * wi + j;  // byte position in the 16-byte chunk
+            const uint32_t sel = 0x0C0C0000u | ((4u + j) << 8);
+            const uint32_t alo = __builtin_amdgcn_perm(lo, lb, sel);
+            const uint32_t ahi = __builtin_amdgcn_perm(hi, lb, sel);
+            const uint32_t vlo = *reinterpret_cast<const uint32_t *>(base + alo + p * 4096);
+            const uint32_t vhi = *reinterpret_cast<const uint32_t *>(base + ahi + p * 4096 + 128);
+            if (j & 1)
+                r1 = xor3(r1, vlo, vhi);
+            else
+                r0 = xor3(r0, vlo, vhi);
+        }
+    }
+    uint32_t v = r0 ^ r1;
+    if (SAR)
+        v ^= (uint32_t)((int32_t)c >> 31) & K16;
+    return v;
+}
+
 constexpr int kWave = 64;
 
 __device__ __forceinline__ uint32_t shr8(uint32_t c, bool sar)

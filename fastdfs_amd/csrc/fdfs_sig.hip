@@ -356,7 +356,7 @@ __device__ __forceinline__ uint32_t chain16x(const uint32_t *sD, uint32_t lb, ui
                                              uint32_t K16)
 {
     if constexpr (NIB)
-        return chain16n<SAR>(sD, lb, c, w, K16);
+        return chain16p<SAR>(sD, lb, c, w, K16);
     else
         return chain16<SAR>(sD, c, w, K16);
 }
@@ -440,6 +440,29 @@ __device__ __forceinline__ uint32_t crc_segment(const uint32_t *sD, const uint32
     return state;
 }
 
+static_assert(kSegBytes == 65536, "CrcTables::ADVSEG is built for 64 KiB segments");
+
+// Advance state v by n zero bytes (v -> M^n v) with the GF(2) matrix powers
+// M^(2^k): lane c (< 32) holds column c, one 5-step XOR reduction per set
+// bit of n.  Wave-uniform v and n; returns the advanced state in every lane.
+__device__ __forceinline__ uint32_t advance_any(const DevTables *__restrict__ tabs, uint32_t v,
+                                                uint64_t n, int lane)
+{
+    const int col = lane & 31;
+    for (int kk = 0; n; kk++, n >>= 1) {
+        if (!(n & 1))
+            continue;
+        uint32_t part = ((v >> col) & 1u) ? tabs->t.MPOW[kk][col] : 0u;
+        part ^= __shfl_xor(part, 16);
+        part ^= __shfl_xor(part, 8);
+        part ^= __shfl_xor(part, 4);
+        part ^= __shfl_xor(part, 2);
+        part ^= __shfl_xor(part, 1);
+        v = part;
+    }
+    return v;
+}
+
 // Constant making crc0(masked data) into CRC32_FINAL(CRC32_ex(data, XINIT)).
 template <bool SAR>
 __device__ __forceinline__ uint32_t crc_final_const(uint64_t L)
@@ -455,21 +478,23 @@ __global__ __launch_bounds__(512) void crc_seg_kernel(
     const uint64_t *__restrict__ sizes, const uint64_t *__restrict__ seg_first, uint32_t n,
     const DevTables *__restrict__ tabs, uint32_t *__restrict__ crc_out)
 {
-    // NIB: lane-bank-replicated nibble tables (64 KiB), the reduction tables
-    // stay in global memory (24 lookups per segment).  !NIB: 8-bit tables.
-    constexpr int kD = NIB ? kNibDwords : 16 * 256;
+    // NIB: lane-bank-replicated nibble tables (64 KiB, v_perm addressed, no
+    // bank conflicts); the reduction tables stay in global memory (24 lookups
+    // per segment).  !NIB: 8-bit slice-by-16 tables.
+    constexpr int kD = NIB ? kNibPDwords : 16 * 256;
     constexpr int kR = NIB ? 0 : 6 * 4 * 256;
-    __shared__ uint32_t smem[kD + 256 + 4 * 256 + kR];
-    uint32_t *sD = smem, *sT = smem + kD, *sA = sT + 256;
-    const uint32_t *sR = NIB ? &tabs->t.ADVRED[0][0][0] : sA + 1024;
+    __shared__ uint32_t smem[kD + 256 + 2 * 4 * 256 + kR];
+    uint32_t *sD = smem, *sT = smem + kD, *sA = sT + 256, *sS = sA + 1024;
+    const uint32_t *sR = NIB ? &tabs->t.ADVRED[0][0][0] : sS + 1024;
+    lds_fill(sS, &tabs->t.ADVSEG[0][0], 4 * 256);
     if constexpr (NIB)
-        lds_fill_nib(sD, SAR ? &tabs->Nc[0][0] : &tabs->N[0][0]);
+        lds_fill_nibp(sD, SAR ? &tabs->Nc[0][0] : &tabs->N[0][0]);
     else
         lds_fill(sD, SAR ? &tabs->Dc[0][0] : &tabs->t.D[0][0], 16 * 256);
     lds_fill(sT, tabs->t.T, 256);
     lds_fill(sA, &tabs->t.ADV4032[0][0], 4 * 256);
     if constexpr (!NIB)
-        lds_fill(sA + 1024, &tabs->t.ADVRED[0][0][0], 6 * 4 * 256);
+        lds_fill(sS + 1024, &tabs->t.ADVRED[0][0][0], 6 * 4 * 256);
     __syncthreads();
 
     const uint32_t K16 = tabs->t.K16;
@@ -491,37 +516,53 @@ __global__ __launch_bounds__(512) void crc_seg_kernel(
             hi = mid;
     }
     uint32_t f = lo;
-    for (; s < s_end; s++) {
-        while (seg_first[f + 1] <= s)
-            f++;
+    // The wave's segments are consecutive, so a run of segments of one file
+    // is chained in place (state = ADV_seg(state) ^ crc0(seg), one 4-lookup
+    // advance per segment); only when the run ends is the state advanced to
+    // the file end (GF(2) matrix powers) and merged into crc_out.
+    uint32_t run_f = 0xFFFFFFFFu, run_state = 0;
+    uint64_t run_end = 0;
+    bool run_has_first = false, run_whole = false;
+    for (;; s++) {
+        const bool more = s < s_end;
+        if (more) {
+            while (seg_first[f + 1] <= s)
+                f++;
+        }
+        if (run_f != 0xFFFFFFFFu && (!more || f != run_f)) {  // flush the finished run
+            const uint64_t L = sizes[run_f];
+            const uint32_t cl = run_has_first ? crc_final_const<SAR>(L) : 0u;
+            if (run_whole) {
+                if (lane == 0)
+                    crc_out[run_f] = run_state ^ cl;
+            } else {
+                const uint32_t v = advance_any(tabs, run_state, L - run_end, lane);
+                if (lane == 0)
+                    atomicXor(&crc_out[run_f], v ^ cl);
+            }
+            run_f = 0xFFFFFFFFu;
+        }
+        if (!more)
+            break;
         const uint64_t k = s - seg_first[f];
         const uint64_t nseg = seg_first[f + 1] - seg_first[f];
         const uint64_t L = sizes[f];
         const uint8_t *fp = base + offs[f];
         const uint64_t lo_b = k * kSegBytes;
         const uint64_t hi_b = (L < lo_b + kSegBytes) ? L : lo_b + kSegBytes;
-        uint32_t v = crc_segment<SAR, NIB>(sD, sT, sA, sR, K16, fp + lo_b, hi_b - lo_b, k == 0, lane);
-        if (nseg == 1) {
-            if (lane == 0)
-                crc_out[f] = v ^ crc_final_const<SAR>(L);
+        const uint32_t v = crc_segment<SAR, NIB>(sD, sT, sA, sR, K16, fp + lo_b, hi_b - lo_b, k == 0, lane);
+        if (run_f == f) {
+            const uint64_t len = hi_b - lo_b;
+            const uint32_t adv = (len == kSegBytes) ? apply4(sS, run_state)
+                                                    : advance_any(tabs, run_state, len, lane);
+            run_state = adv ^ v;
         } else {
-            // advance the segment state to the file end: product of M^(2^k)
-            uint64_t nadv = L - hi_b;
-            const int col = lane & 31;
-            for (int kk = 0; nadv; kk++, nadv >>= 1) {
-                if (!(nadv & 1))
-                    continue;
-                uint32_t part = ((v >> col) & 1u) ? tabs->t.MPOW[kk][col] : 0u;
-                part ^= __shfl_xor(part, 16);
-                part ^= __shfl_xor(part, 8);
-                part ^= __shfl_xor(part, 4);
-                part ^= __shfl_xor(part, 2);
-                part ^= __shfl_xor(part, 1);
-                v = part;
-            }
-            if (lane == 0)
-                atomicXor(&crc_out[f], v ^ (k == 0 ? crc_final_const<SAR>(L) : 0u));
+            run_f = f;
+            run_state = v;
+            run_has_first = (k == 0);
         }
+        run_end = hi_b;
+        run_whole = run_has_first && (k + 1 == nseg);
     }
 }
 

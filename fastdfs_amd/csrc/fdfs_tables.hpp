@@ -19,6 +19,7 @@ struct CrcTables {
     uint32_t K16;             // chain16 sign fix: M^16(c) = sum_j D[j][byte_j(c)] ^ (c<0 ? K16 : 0)
     uint32_t ADV4032[4][256]; // advance by 4032 zero bytes (wave stride - lane piece)
     uint32_t ADVRED[6][4][256]; // advance by 64<<t bytes, t = 0..5 (wave reduction tree)
+    uint32_t ADVSEG[4][256];  // advance by one 64 KiB segment (kSegBytes)
     uint32_t MPOW[48][32];    // columns of M^(2^k), k = 0..47 (arbitrary advance)
     int sar;                  // 1 = arithmetic shift (signed state)
 };
