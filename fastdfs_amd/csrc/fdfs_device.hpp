@@ -127,15 +127,17 @@ __device__ __forceinline__ uint32_t chain16(const uint32_t *__restrict__ D, uint
                                             uint32_t K16)
 {
     const uint32_t x = c ^ w.x;
-    uint32_t r0 = D[0 * 256 + (x & 0xFFu)] ^ D[1 * 256 + ((x >> 8) & 0xFFu)];
-    uint32_t r1 = D[2 * 256 + ((x >> 16) & 0xFFu)] ^ D[3 * 256 + (x >> 24)];
-    uint32_t r2 = D[4 * 256 + (w.y & 0xFFu)] ^ D[5 * 256 + ((w.y >> 8) & 0xFFu)];
-    uint32_t r3 = D[6 * 256 + ((w.y >> 16) & 0xFFu)] ^ D[7 * 256 + (w.y >> 24)];
-    r0 ^= D[8 * 256 + (w.z & 0xFFu)] ^ D[9 * 256 + ((w.z >> 8) & 0xFFu)];
-    r1 ^= D[10 * 256 + ((w.z >> 16) & 0xFFu)] ^ D[11 * 256 + (w.z >> 24)];
-    r2 ^= D[12 * 256 + (w.w & 0xFFu)] ^ D[13 * 256 + ((w.w >> 8) & 0xFFu)];
-    r3 ^= D[14 * 256 + ((w.w >> 16) & 0xFFu)] ^ D[15 * 256 + (w.w >> 24)];
-    uint32_t r = (r0 ^ r1) ^ (r2 ^ r3);
+    uint32_t r0 = xor3(D[0 * 256 + (x & 0xFFu)], D[1 * 256 + ((x >> 8) & 0xFFu)],
+                       D[2 * 256 + ((x >> 16) & 0xFFu)]);
+    uint32_t r1 = xor3(D[3 * 256 + (x >> 24)], D[4 * 256 + (w.y & 0xFFu)],
+                       D[5 * 256 + ((w.y >> 8) & 0xFFu)]);
+    uint32_t r2 = xor3(D[6 * 256 + ((w.y >> 16) & 0xFFu)], D[7 * 256 + (w.y >> 24)],
+                       D[8 * 256 + (w.z & 0xFFu)]);
+    uint32_t r3 = xor3(D[9 * 256 + ((w.z >> 8) & 0xFFu)], D[10 * 256 + ((w.z >> 16) & 0xFFu)],
+                       D[11 * 256 + (w.z >> 24)]);
+    r0 = xor3(r0, D[12 * 256 + (w.w & 0xFFu)], D[13 * 256 + ((w.w >> 8) & 0xFFu)]);
+    r1 = xor3(r1, D[14 * 256 + ((w.w >> 16) & 0xFFu)], D[15 * 256 + (w.w >> 24)]);
+    uint32_t r = xor3(r0, r1, r2) ^ r3;
     if (SAR)
         r ^= (uint32_t)((int32_t)c >> 31) & K16;
     return r;
@@ -179,6 +181,67 @@ __device__ __forceinline__ void h3_word(uint32_t w, uint32_t &e, uint32_t &s, ui
     h3_byte<SAR>((w >> 8) & 0xFFu, e, s, t);
     h3_byte<SAR>((w >> 16) & 0xFFu, e, s, t);
     h3_byte<SAR>(w >> 24, e, s, t);
+}
+
+// ---- simple_hash / Time33 over 16 bytes at once ------------------------
+// Both are linear recurrences h = m*h + b over Z/2^32 (m = 31 / 33), so
+//   h_16 = m^16 * h_0 + sum_p m^(15-p) * b_p   (mod 2^32).
+// Each coefficient is split into byte planes; plane j of the sum is
+// sum_p byte_j(m^(15-p)) * b_p, four bytes at a time with v_dot4_u32_u8.
+// Planes whose coefficients are all zero are folded away at compile time.
+constexpr uint32_t pow_mod32(uint32_t m, int e)
+{
+    uint32_t r = 1;
+    for (int i = 0; i < e; i++)
+        r *= m;
+    return r;
+}
+
+template <uint32_t M>
+struct Poly16 {
+    // packed[w][j] = bytes k=0..3 of plane j of the coefficients of word w
+    static constexpr uint32_t coef(int w, int j)
+    {
+        uint32_t r = 0;
+        for (int k = 0; k < 4; k++)
+            r |= ((pow_mod32(M, 15 - (4 * w + k)) >> (8 * j)) & 0xFFu) << (8 * k);
+        return r;
+    }
+    static constexpr uint32_t m16 = pow_mod32(M, 16);
+};
+
+template <uint32_t M>
+__device__ __forceinline__ uint32_t poly16_step(uint32_t h, uint4 q)
+{
+    const uint32_t w[4] = {q.x, q.y, q.z, q.w};
+    uint32_t a[4] = {0, 0, 0, 0};
+#pragma unroll
+    for (int j = 0; j < 4; j++)
+#pragma unroll
+        for (int i = 0; i < 4; i++)
+            if (Poly16<M>::coef(i, j) != 0)
+                a[j] = __builtin_amdgcn_udot4(w[i], Poly16<M>::coef(i, j), a[j], false);
+    const uint32_t sum = a[0] + (a[1] << 8) + (a[2] << 16) + (a[3] << 24);
+    return h * Poly16<M>::m16 + sum;
+}
+
+// ELFHash_ex alone (the one hash of CALC_HASH_CODES4 with no parallel form).
+template <bool SAR>
+__device__ __forceinline__ void elf_byte(uint32_t b, uint32_t &e)
+{
+    e = (e << 4) + b;
+    const uint32_t x = e & 0xF0000000u;
+    e ^= SAR ? (uint32_t)((int32_t)x >> 24) : (x >> 24);
+    e &= ~x;
+}
+
+template <bool SAR>
+__device__ __forceinline__ void elf_word(uint32_t w, uint32_t &e)
+{
+    elf_byte<SAR>(w & 0xFFu, e);
+    elf_byte<SAR>((w >> 8) & 0xFFu, e);
+    elf_byte<SAR>((w >> 16) & 0xFFu, e);
+    elf_byte<SAR>(w >> 24, e);
 }
 
 __device__ __forceinline__ uint32_t bswap32(uint32_t v) { return __builtin_bswap32(v); }

@@ -137,33 +137,55 @@ __device__ __forceinline__ void store_sig(uint8_t *sig, uint64_t L, uint32_t w2,
 // ------------------------------------------------------- lane-per-file path
 
 // One 16-byte vector through all four CALC_HASH_CODES4 hashes.
-template <bool SAR>
-__device__ __forceinline__ void h4_vec(const uint32_t *sD, uint32_t K16, uint4 q, uint32_t &c,
-                                       uint32_t &e, uint32_t &s, uint32_t &t)
+// PL: simple_hash / Time33 as 16-byte polynomial steps on v_dot4_u32_u8
+// (poly16_step) instead of byte-serial shift-adds; ELF stays byte-serial.
+template <bool SAR, bool NP, bool PL>
+__device__ __forceinline__ void h4_vec(const uint32_t *sD, uint32_t lb, uint32_t K16, uint4 q,
+                                       uint32_t &c, uint32_t &e, uint32_t &s, uint32_t &t)
 {
-    c = chain16<SAR>(sD, c, q, K16);
-    h3_word<SAR>(q.x, e, s, t);
-    h3_word<SAR>(q.y, e, s, t);
-    h3_word<SAR>(q.z, e, s, t);
-    h3_word<SAR>(q.w, e, s, t);
+    if constexpr (NP)
+        c = chain16p<SAR>(sD, lb, c, q, K16);
+    else
+        c = chain16<SAR>(sD, c, q, K16);
+    if constexpr (PL) {
+        elf_word<SAR>(q.x, e);
+        elf_word<SAR>(q.y, e);
+        elf_word<SAR>(q.z, e);
+        elf_word<SAR>(q.w, e);
+        s = poly16_step<31>(s, q);
+        t = poly16_step<33>(t, q);
+    } else {
+        h3_word<SAR>(q.x, e, s, t);
+        h3_word<SAR>(q.y, e, s, t);
+        h3_word<SAR>(q.z, e, s, t);
+        h3_word<SAR>(q.w, e, s, t);
+    }
 }
 
 template <bool SAR, int METHOD, int VAR>
-__global__ __launch_bounds__(256) void sig_lane_kernel(
+__global__ __launch_bounds__(1024) void sig_lane_kernel(
     const uint8_t *__restrict__ base, const uint64_t *__restrict__ offs,
     const uint64_t *__restrict__ sizes, const uint32_t *__restrict__ order, uint32_t n,
     const DevTables *__restrict__ tabs, uint32_t *__restrict__ crc_out,
     uint8_t *__restrict__ sig_out, int32_t *__restrict__ codes_out)
 {
-    __shared__ uint32_t sD[16 * 256];
+    // VAR 4: the VAR 2 load schedule with the CRC through the conflict-free
+    // v_perm nibble tables (64 KiB of LDS) instead of 8-bit slice tables.
+    constexpr bool NP = (VAR == 4);
+    constexpr bool PL = (VAR == 5);
+    __shared__ uint32_t sD[NP ? kNibPDwords : 16 * 256];
     __shared__ uint32_t sT[256];
-    lds_fill(sD, &tabs->t.D[0][0], 16 * 256);
+    if constexpr (NP)
+        lds_fill_nibp(sD, &tabs->N[0][0]);
+    else
+        lds_fill(sD, &tabs->t.D[0][0], 16 * 256);
     lds_fill(sT, tabs->t.T, 256);
     __syncthreads();
 
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n)
         return;
+    const uint32_t lb = (threadIdx.x & 31) * 4u;
     const uint32_t K16 = tabs->t.K16;
     const uint32_t f = order ? order[i] : i;
     const uint64_t L = sizes[f];
@@ -195,7 +217,7 @@ __global__ __launch_bounds__(256) void sig_lane_kernel(
                 for (; j < nvec; j++) {
                     const uint64_t nj = j + 3;
                     const uint4 q3 = v[nj < last ? nj : last];
-                    h4_vec<SAR>(sD, K16, q0, c, e, s, t);
+                    h4_vec<SAR, NP, PL>(sD, lb, K16,q0, c, e, s, t);
                     q0 = q1;
                     q1 = q2;
                     q2 = q3;
@@ -208,15 +230,26 @@ __global__ __launch_bounds__(256) void sig_lane_kernel(
                 for (; j + 4 <= nvec; j += 4) {
                     const uint64_t nx = (j + 8 <= nvec) ? j + 4 : j;
                     const uint4 b0 = v[nx], b1 = v[nx + 1], b2 = v[nx + 2], b3 = v[nx + 3];
-                    h4_vec<SAR>(sD, K16, a0, c, e, s, t);
-                    h4_vec<SAR>(sD, K16, a1, c, e, s, t);
-                    h4_vec<SAR>(sD, K16, a2, c, e, s, t);
-                    h4_vec<SAR>(sD, K16, a3, c, e, s, t);
+                    h4_vec<SAR, NP, PL>(sD, lb, K16,a0, c, e, s, t);
+                    h4_vec<SAR, NP, PL>(sD, lb, K16,a1, c, e, s, t);
+                    h4_vec<SAR, NP, PL>(sD, lb, K16,a2, c, e, s, t);
+                    h4_vec<SAR, NP, PL>(sD, lb, K16,a3, c, e, s, t);
                     a0 = b0;
                     a1 = b1;
                     a2 = b2;
                     a3 = b3;
                 }
+            }
+        } else if constexpr (VAR == 3) {
+            // 64 B per step, no register prefetch (fewer VGPRs, more waves)
+            for (; j + 4 <= nvec; j += 4) {
+                uint4 a[4];
+#pragma unroll
+                for (int q = 0; q < 4; q++)
+                    a[q] = v[j + q];
+#pragma unroll
+                for (int q = 0; q < 4; q++)
+                    h4_vec<SAR, NP, PL>(sD, lb, K16,a[q], c, e, s, t);
             }
         } else {
             // 128 B (one cache line) per step, no register prefetch
@@ -227,11 +260,11 @@ __global__ __launch_bounds__(256) void sig_lane_kernel(
                     a[q] = v[j + q];
 #pragma unroll
                 for (int q = 0; q < 8; q++)
-                    h4_vec<SAR>(sD, K16, a[q], c, e, s, t);
+                    h4_vec<SAR, NP, PL>(sD, lb, K16,a[q], c, e, s, t);
             }
         }
         for (; j < nvec; j++)
-            h4_vec<SAR>(sD, K16, v[j], c, e, s, t);
+            h4_vec<SAR, NP, PL>(sD, lb, K16,v[j], c, e, s, t);
         for (uint64_t k = head + (nvec << 4); k < L; k++) {
             const uint32_t b = p[k];
             c = crc_byte<SAR>(sT, c, b);
@@ -766,17 +799,18 @@ hipError_t launch_sig_lane(bool sar, int method, const uint8_t *base, const uint
     bin_hist_kernel<<<hb < 1024 ? hb : 1024, 256, 0, st>>>(sizes, n, hist);
     bin_scan_kernel<<<1, 1024, 0, st>>>(hist, cursor);
     bin_scatter_kernel<<<hb, 1024, 0, st>>>(sizes, n, cursor, order);
-    const unsigned g = (n + 255) / 256;
+    const unsigned g = (n + 255) / 256, g4 = (n + 1023) / 1024;
     if (ev0)
         (void)hipEventRecord(ev0, st);
 #define LANE_LAUNCH(S, M, V) \
-    sig_lane_kernel<S, M, V><<<g, 256, 0, st>>>(base, offs, sizes, order, n, tabs, crc_out, sig_out, codes_out)
+    sig_lane_kernel<S, M, V><<<(V == 4) ? g4 : g, (V == 4) ? 1024 : 256, 0, st>>>( \
+        base, offs, sizes, order, n, tabs, crc_out, sig_out, codes_out)
     static int var = -1;
     if (var < 0) {  // FDFS_GPU_LANE_VARIANT: A/B of the hash-path load schedule
         const char *ev = getenv("FDFS_GPU_LANE_VARIANT");
-        var = ev ? (ev[0] - '0') : 2;
-        if (var < 0 || var > 2)
-            var = 1;
+        var = ev ? (ev[0] - '0') : 5;
+        if (var != 2 && var != 4)
+            var = 5;
     }
     if (method == 2) {
         if (sar)
@@ -784,17 +818,17 @@ hipError_t launch_sig_lane(bool sar, int method, const uint8_t *base, const uint
         else
             LANE_LAUNCH(false, 2, 0);
     } else if (sar) {
-        if (var == 0)
-            LANE_LAUNCH(true, 1, 0);
-        else if (var == 1)
-            LANE_LAUNCH(true, 1, 1);
+        if (var == 5)
+            LANE_LAUNCH(true, 1, 5);
+        else if (var == 4)
+            LANE_LAUNCH(true, 1, 4);
         else
             LANE_LAUNCH(true, 1, 2);
     } else {
-        if (var == 0)
-            LANE_LAUNCH(false, 1, 0);
-        else if (var == 1)
-            LANE_LAUNCH(false, 1, 1);
+        if (var == 5)
+            LANE_LAUNCH(false, 1, 5);
+        else if (var == 4)
+            LANE_LAUNCH(false, 1, 4);
         else
             LANE_LAUNCH(false, 1, 2);
     }
