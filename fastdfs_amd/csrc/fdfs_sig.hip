@@ -252,7 +252,13 @@ __global__ __launch_bounds__(1024) void sig_lane_kernel(
                     h4_vec<SAR, NP, PL>(sD, lb, K16,a[q], c, e, s, t);
             }
         } else {
-            // 128 B (one cache line) per step, no register prefetch
+            // 128 B (one cache line) per step, no register prefetch.  Single
+            // vectors first until the window is 128-byte aligned, so every
+            // step reads exactly one whole line (an unaligned window splits
+            // two lines across steps, and the second touch misses L2).
+            const uint64_t lead = ((128u - ((uintptr_t)v & 127u)) & 127u) >> 4;
+            for (; j < lead && j < nvec; j++)
+                h4_vec<SAR, NP, PL>(sD, lb, K16, v[j], c, e, s, t);
             for (; j + 8 <= nvec; j += 8) {
                 uint4 a[8];
 #pragma unroll
