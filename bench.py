@@ -183,7 +183,7 @@ def main():
             workload = ("config 2: 1M files/GPU of U[4,64] KiB, CRC32 + HASH_CODES4 signature "
                         "+ bulk dedup per step")
         elif args.config == "c3":
-            n = args.files or 24_000
+            n = args.files or 100_000  # the full config (~262 GB resident in HBM)
             sizes = C.photo_sizes(n, seed=3 + 1000 * rank)
             method, kernel, kname = F.SIG_MD5, _lib.KERNEL_SIG_LANE, "sig_lane_kernel<SAR,2>"
             workload = f"config 3: {n} files/GPU of U[1,4] MiB, CRC32 + MD5 signature + dedup"

@@ -163,7 +163,7 @@ __device__ __forceinline__ void h4_vec(const uint32_t *sD, uint32_t lb, uint32_t
 }
 
 template <bool SAR, int METHOD, int VAR>
-__global__ __launch_bounds__(1024) void sig_lane_kernel(
+__global__ __launch_bounds__(VAR == 4 ? 1024 : 256, VAR == 6 ? 8 : 1) void sig_lane_kernel(
     const uint8_t *__restrict__ base, const uint64_t *__restrict__ offs,
     const uint64_t *__restrict__ sizes, const uint32_t *__restrict__ order, uint32_t n,
     const DevTables *__restrict__ tabs, uint32_t *__restrict__ crc_out,
@@ -172,15 +172,17 @@ __global__ __launch_bounds__(1024) void sig_lane_kernel(
     // VAR 4: the VAR 2 load schedule with the CRC through the conflict-free
     // v_perm nibble tables (64 KiB of LDS) instead of 8-bit slice tables.
     constexpr bool NP = (VAR == 4);
-    constexpr bool PL = (VAR == 5);
+    constexpr bool PL = (VAR == 5 || VAR == 6);  // VAR 6: VAR 5 capped at 64 VGPRs
     __shared__ uint32_t sD[NP ? kNibPDwords : 16 * 256];
     __shared__ uint32_t sT[256];
-    if constexpr (NP)
-        lds_fill_nibp(sD, &tabs->N[0][0]);
-    else
-        lds_fill(sD, &tabs->t.D[0][0], 16 * 256);
-    lds_fill(sT, tabs->t.T, 256);
-    __syncthreads();
+    if constexpr (METHOD == 1) {  // the MD5 path uses no tables
+        if constexpr (NP)
+            lds_fill_nibp(sD, &tabs->N[0][0]);
+        else
+            lds_fill(sD, &tabs->t.D[0][0], 16 * 256);
+        lds_fill(sT, tabs->t.T, 256);
+        __syncthreads();
+    }
 
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n)
@@ -287,17 +289,67 @@ __global__ __launch_bounds__(1024) void sig_lane_kernel(
         const bool al = (((uintptr_t)p) & 15u) == 0;
         const uint64_t nblk = L >> 6;
         uint64_t j = 0;
-        if (nblk) {
+        // MD5 only: the file CRC of the MD5 method comes from crc_seg_kernel
+        // on a forked stream (launch_sig_lane).  A lane-serial CRC here put
+        // LDS-latency waits into the in-order MD5 chain of a wave that has
+        // no partner wave to hide them (1-2 waves per SIMD at 1-4 MiB files).
+        auto md5_block = [&](uint4 a0, uint4 a1, uint4 a2, uint4 a3) {
+            const uint32_t m[16] = {a0.x, a0.y, a0.z, a0.w, a1.x, a1.y, a1.z, a1.w,
+                                    a2.x, a2.y, a2.z, a2.w, a3.x, a3.y, a3.z, a3.w};
+            md5_compress(st, m);
+        };
+        if (al) {
+            // The MD5 chain is serial per file, and a batch of 1-4 MiB files
+            // leaves ~1-2 waves per SIMD: deep register prefetch (the next
+            // 4 blocks load while 4 are hashed) hides HBM latency instead.
+            // hipcc sinks ordinary prefetch loads to their use (it re-issues
+            // invariant loads instead of keeping 64 VGPRs live), so the next
+            // group is loaded with asm loads that it cannot move, and waited
+            // for by one asm wait that names every destination.
+            const uint4 *v = reinterpret_cast<const uint4 *>(p);
+            constexpr int G = 4;
+            if (nblk >= G) {
+                uint4 A[4 * G];
+#pragma unroll
+                for (int q = 0; q < 4 * G; q++)
+                    A[q] = v[q];
+                for (; j + G <= nblk; j += G) {
+                    const uint64_t nx = (j + 2 * G <= nblk) ? j + G : j;
+                    const uint4 *np = v + 4 * nx;
+                    typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+                    u32x4 b0, b1, b2, b3, b4, b5, b6, b7, b8, b9, b10, b11, b12, b13, b14, b15;
+#define MD5_PF(x, q) asm volatile("global_load_dwordx4 %0, %1, off offset:%2" \
+                                  : "=v"(x) : "v"(np), "i"(16 * (q)) : "memory")
+                    MD5_PF(b0, 0); MD5_PF(b1, 1); MD5_PF(b2, 2); MD5_PF(b3, 3);
+                    MD5_PF(b4, 4); MD5_PF(b5, 5); MD5_PF(b6, 6); MD5_PF(b7, 7);
+                    MD5_PF(b8, 8); MD5_PF(b9, 9); MD5_PF(b10, 10); MD5_PF(b11, 11);
+                    MD5_PF(b12, 12); MD5_PF(b13, 13); MD5_PF(b14, 14); MD5_PF(b15, 15);
+#undef MD5_PF
+#pragma unroll
+                    for (int b = 0; b < G; b++)
+                        md5_block(A[4 * b], A[4 * b + 1], A[4 * b + 2], A[4 * b + 3]);
+                    asm volatile("s_waitcnt vmcnt(0)"
+                                 : "+v"(b0), "+v"(b1), "+v"(b2), "+v"(b3) :: "memory");
+                    asm volatile("" : "+v"(b4), "+v"(b5), "+v"(b6), "+v"(b7));
+                    asm volatile("" : "+v"(b8), "+v"(b9), "+v"(b10), "+v"(b11));
+                    asm volatile("" : "+v"(b12), "+v"(b13), "+v"(b14), "+v"(b15));
+#define MD5_MV(q) A[q] = make_uint4(b##q[0], b##q[1], b##q[2], b##q[3])
+                    MD5_MV(0); MD5_MV(1); MD5_MV(2); MD5_MV(3);
+                    MD5_MV(4); MD5_MV(5); MD5_MV(6); MD5_MV(7);
+                    MD5_MV(8); MD5_MV(9); MD5_MV(10); MD5_MV(11);
+                    MD5_MV(12); MD5_MV(13); MD5_MV(14); MD5_MV(15);
+#undef MD5_MV
+                }
+            }
+            for (; j < nblk; j++)
+                md5_block(v[4 * j], v[4 * j + 1], v[4 * j + 2], v[4 * j + 3]);
+        } else if (nblk) {
             uint4 a0 = load16(p, al), a1 = load16(p + 16, al), a2 = load16(p + 32, al),
                   a3 = load16(p + 48, al);
             for (; j < nblk; j++) {
                 const uint8_t *q = p + ((j + 1 < nblk) ? (j + 1) : j) * 64;
                 const uint4 b0 = load16(q, al), b1 = load16(q + 16, al), b2 = load16(q + 32, al),
                             b3 = load16(q + 48, al);
-                c = chain16<SAR>(sD, c, a0, K16);
-                c = chain16<SAR>(sD, c, a1, K16);
-                c = chain16<SAR>(sD, c, a2, K16);
-                c = chain16<SAR>(sD, c, a3, K16);
                 const uint32_t m[16] = {a0.x, a0.y, a0.z, a0.w, a1.x, a1.y, a1.z, a1.w,
                                         a2.x, a2.y, a2.z, a2.w, a3.x, a3.y, a3.z, a3.w};
                 md5_compress(st, m);
@@ -320,7 +372,6 @@ __global__ __launch_bounds__(1024) void sig_lane_kernel(
                 uint32_t b = 0;
                 if (k < r) {
                     b = tp[k];
-                    c = crc_byte<SAR>(sT, c, b);
                 } else if (k == r) {
                     b = 0x80u;
                 }
@@ -342,8 +393,6 @@ __global__ __launch_bounds__(1024) void sig_lane_kernel(
             m[15] = (uint32_t)(bits >> 32);
             md5_compress(st, m);
         }
-        c ^= 0xFFFFFFFFu;
-        crc_out[f] = c;
         if (sig_out)  // memcpy(sig + 8, md5 digest, 16) (storage/storage_service.c:119)
             store_sig(sig_out + 24ull * f, L, st[0], st[1], st[2], st[3]);
         if (codes_out)
@@ -815,7 +864,7 @@ hipError_t launch_sig_lane(bool sar, int method, const uint8_t *base, const uint
     if (var < 0) {  // FDFS_GPU_LANE_VARIANT: A/B of the hash-path load schedule
         const char *ev = getenv("FDFS_GPU_LANE_VARIANT");
         var = ev ? (ev[0] - '0') : 5;
-        if (var != 2 && var != 4)
+        if (var != 2 && var != 6)
             var = 5;
     }
     if (method == 2) {
@@ -826,15 +875,15 @@ hipError_t launch_sig_lane(bool sar, int method, const uint8_t *base, const uint
     } else if (sar) {
         if (var == 5)
             LANE_LAUNCH(true, 1, 5);
-        else if (var == 4)
-            LANE_LAUNCH(true, 1, 4);
+        else if (var == 6)
+            LANE_LAUNCH(true, 1, 6);
         else
             LANE_LAUNCH(true, 1, 2);
     } else {
         if (var == 5)
             LANE_LAUNCH(false, 1, 5);
-        else if (var == 4)
-            LANE_LAUNCH(false, 1, 4);
+        else if (var == 6)
+            LANE_LAUNCH(false, 1, 6);
         else
             LANE_LAUNCH(false, 1, 2);
     }
