@@ -106,6 +106,73 @@ __device__ __forceinline__ uint32_t chain16p(const uint32_t *sN, uint32_t lb, ui
     return v;
 }
 
+// ---- conflict-free slice-by-8: rotated, replicated byte tables ----------
+// A ds_read_b32 serves lanes 0-31 and 32-63 as two groups over 32 banks
+// (bank = dword address mod 32); random byte lookups into one shared table
+// put ~3.5 lanes on the busiest bank (measured: 2/3 of all LDS cycles were
+// conflicts).  Here lane l reads byte position (k + (l & 3)) & 3 of a data
+// word at step k (a per-lane byte rotation, free inside v_perm_b32), from
+// its own copy (l >> 2) & 7 of the table for that position.  Table t, copy c
+// is slot t*8 + c of a 64-dword row per byte value (row e = 256 bytes), so at
+// every step the 32 lanes of a group hit 32 distinct banks.
+//   LDS image: dword e*64 + t*8 + c = D[8 + t][e]   (64 KiB)
+//   address  = e << 8 | slot << 2  = v_perm_b32(word, off, sel): byte 1 is
+//              the data byte, byte 0 the lane's slot offset.
+constexpr int kRep8Dwords = 256 * 64;
+
+// src: the 16 slice-by-16 tables (D or Dc); positions 8..15 are slice-by-8.
+__device__ __forceinline__ void lds_fill_rep8(uint32_t *dst, const uint32_t *__restrict__ src)
+{
+    for (int i = threadIdx.x; i < kRep8Dwords; i += blockDim.x)
+        dst[i] = src[(8 + ((i >> 3) & 7)) * 256 + (i >> 6)];
+}
+
+struct Rep8Lane {
+    uint32_t off0, off1;  // slot byte offsets for word 0 / word 1, byte k = step k
+    uint32_t sel[4];      // v_perm selectors for steps k = 0..3
+};
+
+__device__ __forceinline__ Rep8Lane rep8_lane(int lane)
+{
+    Rep8Lane r;
+    const uint32_t b = lane & 3, c = (lane >> 2) & 7;
+    r.off0 = r.off1 = 0;
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+        const uint32_t kk = (k + b) & 3;
+        r.off0 |= (((0 + kk) * 8 + c) * 4) << (8 * k);
+        r.off1 |= (((4 + kk) * 8 + c) * 4) << (8 * k);
+        r.sel[k] = 0x0C0C0000u | ((4u + kk) << 8) | (uint32_t)k;
+    }
+    return r;
+}
+
+// 8 bytes (LE words w0, w1) chained onto state c.  SAR adds the sign term.
+template <bool SAR>
+__device__ __forceinline__ uint32_t chain8r(const uint32_t *sR, const Rep8Lane &R, uint32_t c,
+                                            uint32_t w0, uint32_t w1, uint32_t K8)
+{
+    const char *base = reinterpret_cast<const char *>(sR);
+    const uint32_t x0 = c ^ w0;
+    uint32_t v[8];
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+        v[k] = *reinterpret_cast<const uint32_t *>(base + __builtin_amdgcn_perm(x0, R.off0, R.sel[k]));
+        v[4 + k] = *reinterpret_cast<const uint32_t *>(base + __builtin_amdgcn_perm(w1, R.off1, R.sel[k]));
+    }
+    const uint32_t s = SAR ? ((uint32_t)((int32_t)c >> 31) & K8) : 0u;
+    return xor3(xor3(v[0], v[1], v[2]), xor3(v[3], v[4], v[5]), xor3(v[6], v[7], s));
+}
+
+// 16 bytes = two slice-by-8 steps.
+template <bool SAR>
+__device__ __forceinline__ uint32_t chain16r(const uint32_t *sR, const Rep8Lane &R, uint32_t c,
+                                             uint4 w, uint32_t K8)
+{
+    c = chain8r<SAR>(sR, R, c, w.x, w.y, K8);
+    return chain8r<SAR>(sR, R, c, w.z, w.w, K8);
+}
+
 constexpr int kWave = 64;
 
 __device__ __forceinline__ uint32_t shr8(uint32_t c, bool sar)

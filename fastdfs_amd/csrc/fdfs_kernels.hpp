@@ -8,6 +8,7 @@ namespace fdfs {
 struct DevTables;
 
 constexpr uint64_t kSegBytes = 64 * 1024;  // CRC segment owned by one wave
+constexpr int kSegBlock = 512;             // threads per crc_seg_kernel workgroup
 constexpr int kSizeBins = 2048;            // size bins of the lane-path counting sort
 
 // signature path (fdfs_sig.hip)
@@ -23,7 +24,7 @@ hipError_t launch_crc_seg(bool sar, const uint8_t *base, const uint64_t *offs, c
                           const DevTables *tabs, uint32_t *crc_out, unsigned grid, hipStream_t st,
                           hipEvent_t ev0, hipEvent_t ev1);
 int crc_seg_blocks_per_cu();
-bool crc_tables_nibble();
+int crc_table_mode();
 
 // dedup path (fdfs_dedup.hip)
 uint64_t dedup_table_slots(uint64_t n);

@@ -134,6 +134,47 @@ __device__ __forceinline__ void store_sig(uint8_t *sig, uint64_t L, uint32_t w2,
     sp[2] = make_uint2(w4, w5);
 }
 
+// Final block(s) of a file whose first nblk full 64-byte blocks are already
+// folded into st: the L & 63 tail bytes, 0x80, zero pad and the 64-bit bit
+// length (RFC 1321 3.1-3.2; my_md5_final at storage/storage_dio.c:512).
+__device__ __forceinline__ void md5_finish(uint32_t st[4], const uint8_t *p, uint64_t nblk,
+                                           uint64_t L)
+{
+    const uint8_t *tp = p + (nblk << 6);
+    const uint32_t r = (uint32_t)(L & 63u);
+    uint32_t m[16];
+#pragma unroll
+    for (int wd = 0; wd < 16; wd++) {
+        uint32_t word = 0;
+#pragma unroll
+        for (int q = 0; q < 4; q++) {
+            const uint32_t k = 4 * wd + q;
+            uint32_t b = 0;
+            if (k < r) {
+                b = tp[k];
+            } else if (k == r) {
+                b = 0x80u;
+            }
+            word |= b << (8 * q);
+        }
+        m[wd] = word;
+    }
+    const uint64_t bits = L << 3;
+    if (r < 56) {
+        m[14] = (uint32_t)bits;
+        m[15] = (uint32_t)(bits >> 32);
+        md5_compress(st, m);
+    } else {
+        md5_compress(st, m);
+#pragma unroll
+        for (int wd = 0; wd < 14; wd++)
+            m[wd] = 0;
+        m[14] = (uint32_t)bits;
+        m[15] = (uint32_t)(bits >> 32);
+        md5_compress(st, m);
+    }
+}
+
 // ------------------------------------------------------- lane-per-file path
 
 // One 16-byte vector through all four CALC_HASH_CODES4 hashes.
@@ -162,8 +203,25 @@ __device__ __forceinline__ void h4_vec(const uint32_t *sD, uint32_t lb, uint32_t
     }
 }
 
+// The same with the CRC through the conflict-free rotated slice-by-8 tables.
+template <bool SAR, bool PL>
+__device__ __forceinline__ void h4_vec_r(const uint32_t *sR, const Rep8Lane &R, uint32_t K8,
+                                         uint4 q, uint32_t &c, uint32_t &e, uint32_t &s,
+                                         uint32_t &t)
+{
+    c = chain16r<SAR>(sR, R, c, q, K8);
+    elf_word<SAR>(q.x, e);
+    elf_word<SAR>(q.y, e);
+    elf_word<SAR>(q.z, e);
+    elf_word<SAR>(q.w, e);
+    s = poly16_step<31>(s, q);
+    t = poly16_step<33>(t, q);
+}
+
+constexpr int kLaneBlock7 = 768;
+
 template <bool SAR, int METHOD, int VAR>
-__global__ __launch_bounds__(VAR == 4 ? 1024 : 256, VAR == 6 ? 8 : 1) void sig_lane_kernel(
+__global__ __launch_bounds__(VAR == 4 ? 1024 : (VAR == 7 ? kLaneBlock7 : 256), VAR == 6 ? 8 : 1) void sig_lane_kernel(
     const uint8_t *__restrict__ base, const uint64_t *__restrict__ offs,
     const uint64_t *__restrict__ sizes, const uint32_t *__restrict__ order, uint32_t n,
     const DevTables *__restrict__ tabs, uint32_t *__restrict__ crc_out,
@@ -172,12 +230,15 @@ __global__ __launch_bounds__(VAR == 4 ? 1024 : 256, VAR == 6 ? 8 : 1) void sig_l
     // VAR 4: the VAR 2 load schedule with the CRC through the conflict-free
     // v_perm nibble tables (64 KiB of LDS) instead of 8-bit slice tables.
     constexpr bool NP = (VAR == 4);
-    constexpr bool PL = (VAR == 5 || VAR == 6);  // VAR 6: VAR 5 capped at 64 VGPRs
-    __shared__ uint32_t sD[NP ? kNibPDwords : 16 * 256];
+    constexpr bool RP = (VAR == 7);  // rotated replicated slice-by-8 CRC tables
+    constexpr bool PL = (VAR == 5 || VAR == 6 || VAR == 7);  // VAR 6: VAR 5 capped at 64 VGPRs
+    __shared__ uint32_t sD[NP ? kNibPDwords : (RP ? kRep8Dwords : 16 * 256)];
     __shared__ uint32_t sT[256];
     if constexpr (METHOD == 1) {  // the MD5 path uses no tables
         if constexpr (NP)
             lds_fill_nibp(sD, &tabs->N[0][0]);
+        else if constexpr (RP)
+            lds_fill_rep8(sD, &tabs->t.D[0][0]);
         else
             lds_fill(sD, &tabs->t.D[0][0], 16 * 256);
         lds_fill(sT, tabs->t.T, 256);
@@ -188,7 +249,8 @@ __global__ __launch_bounds__(VAR == 4 ? 1024 : 256, VAR == 6 ? 8 : 1) void sig_l
     if (i >= n)
         return;
     const uint32_t lb = (threadIdx.x & 31) * 4u;
-    const uint32_t K16 = tabs->t.K16;
+    const uint32_t K16 = RP ? tabs->t.K8 : tabs->t.K16;
+    const Rep8Lane R8 = rep8_lane(threadIdx.x & 63);
     const uint32_t f = order ? order[i] : i;
     const uint64_t L = sizes[f];
     const uint8_t *p = base + offs[f];
@@ -204,6 +266,13 @@ __global__ __launch_bounds__(VAR == 4 ? 1024 : 256, VAR == 6 ? 8 : 1) void sig_l
             c = crc_byte<SAR>(sT, c, b);
             h3_byte<SAR>(b, e, s, t);
         }
+#define H4V(Q, C, E, S, T)                                      \
+    do {                                                        \
+        if constexpr (RP)                                       \
+            h4_vec_r<SAR, PL>(sD, R8, K16, (Q), C, E, S, T);     \
+        else                                                    \
+            h4_vec<SAR, NP, PL>(sD, lb, K16, (Q), C, E, S, T);   \
+    } while (0)
         const uint4 *v = reinterpret_cast<const uint4 *>(p + head);
         const uint64_t nvec = (L - head) >> 4;
         uint64_t j = 0;
@@ -219,7 +288,7 @@ __global__ __launch_bounds__(VAR == 4 ? 1024 : 256, VAR == 6 ? 8 : 1) void sig_l
                 for (; j < nvec; j++) {
                     const uint64_t nj = j + 3;
                     const uint4 q3 = v[nj < last ? nj : last];
-                    h4_vec<SAR, NP, PL>(sD, lb, K16,q0, c, e, s, t);
+                    H4V(q0, c, e, s, t);
                     q0 = q1;
                     q1 = q2;
                     q2 = q3;
@@ -232,10 +301,10 @@ __global__ __launch_bounds__(VAR == 4 ? 1024 : 256, VAR == 6 ? 8 : 1) void sig_l
                 for (; j + 4 <= nvec; j += 4) {
                     const uint64_t nx = (j + 8 <= nvec) ? j + 4 : j;
                     const uint4 b0 = v[nx], b1 = v[nx + 1], b2 = v[nx + 2], b3 = v[nx + 3];
-                    h4_vec<SAR, NP, PL>(sD, lb, K16,a0, c, e, s, t);
-                    h4_vec<SAR, NP, PL>(sD, lb, K16,a1, c, e, s, t);
-                    h4_vec<SAR, NP, PL>(sD, lb, K16,a2, c, e, s, t);
-                    h4_vec<SAR, NP, PL>(sD, lb, K16,a3, c, e, s, t);
+                    H4V(a0, c, e, s, t);
+                    H4V(a1, c, e, s, t);
+                    H4V(a2, c, e, s, t);
+                    H4V(a3, c, e, s, t);
                     a0 = b0;
                     a1 = b1;
                     a2 = b2;
@@ -251,7 +320,7 @@ __global__ __launch_bounds__(VAR == 4 ? 1024 : 256, VAR == 6 ? 8 : 1) void sig_l
                     a[q] = v[j + q];
 #pragma unroll
                 for (int q = 0; q < 4; q++)
-                    h4_vec<SAR, NP, PL>(sD, lb, K16,a[q], c, e, s, t);
+                    H4V(a[q], c, e, s, t);
             }
         } else {
             // 128 B (one cache line) per step, no register prefetch.  Single
@@ -260,7 +329,7 @@ __global__ __launch_bounds__(VAR == 4 ? 1024 : 256, VAR == 6 ? 8 : 1) void sig_l
             // two lines across steps, and the second touch misses L2).
             const uint64_t lead = ((128u - ((uintptr_t)v & 127u)) & 127u) >> 4;
             for (; j < lead && j < nvec; j++)
-                h4_vec<SAR, NP, PL>(sD, lb, K16, v[j], c, e, s, t);
+                H4V( v[j], c, e, s, t);
             for (; j + 8 <= nvec; j += 8) {
                 uint4 a[8];
 #pragma unroll
@@ -268,16 +337,17 @@ __global__ __launch_bounds__(VAR == 4 ? 1024 : 256, VAR == 6 ? 8 : 1) void sig_l
                     a[q] = v[j + q];
 #pragma unroll
                 for (int q = 0; q < 8; q++)
-                    h4_vec<SAR, NP, PL>(sD, lb, K16,a[q], c, e, s, t);
+                    H4V(a[q], c, e, s, t);
             }
         }
         for (; j < nvec; j++)
-            h4_vec<SAR, NP, PL>(sD, lb, K16,v[j], c, e, s, t);
+            H4V(v[j], c, e, s, t);
         for (uint64_t k = head + (nvec << 4); k < L; k++) {
             const uint32_t b = p[k];
             c = crc_byte<SAR>(sT, c, b);
             h3_byte<SAR>(b, e, s, t);
         }
+#undef H4V
         c ^= 0xFFFFFFFFu;  // CRC32_FINAL / FINISH_HASH_CODES4 (storage/storage_dio.c:500,508)
         crc_out[f] = c;
         if (sig_out)
@@ -359,46 +429,132 @@ __global__ __launch_bounds__(VAR == 4 ? 1024 : 256, VAR == 6 ? 8 : 1) void sig_l
                 a3 = b3;
             }
         }
-        // final block(s): r tail bytes, 0x80, zero pad, 64-bit bit length (RFC 1321 3.1-3.2)
-        const uint8_t *tp = p + (nblk << 6);
-        const uint32_t r = (uint32_t)(L & 63u);
-        uint32_t m[16];
-#pragma unroll
-        for (int wd = 0; wd < 16; wd++) {
-            uint32_t word = 0;
-#pragma unroll
-            for (int q = 0; q < 4; q++) {
-                const uint32_t k = 4 * wd + q;
-                uint32_t b = 0;
-                if (k < r) {
-                    b = tp[k];
-                } else if (k == r) {
-                    b = 0x80u;
-                }
-                word |= b << (8 * q);
-            }
-            m[wd] = word;
-        }
-        const uint64_t bits = L << 3;
-        if (r < 56) {
-            m[14] = (uint32_t)bits;
-            m[15] = (uint32_t)(bits >> 32);
-            md5_compress(st, m);
-        } else {
-            md5_compress(st, m);
-#pragma unroll
-            for (int wd = 0; wd < 14; wd++)
-                m[wd] = 0;
-            m[14] = (uint32_t)bits;
-            m[15] = (uint32_t)(bits >> 32);
-            md5_compress(st, m);
-        }
+        md5_finish(st, p, nblk, L);
         if (sig_out)  // memcpy(sig + 8, md5 digest, 16) (storage/storage_service.c:119)
             store_sig(sig_out + 24ull * f, L, st[0], st[1], st[2], st[3]);
         if (codes_out)
             reinterpret_cast<int4 *>(codes_out)[f] =
                 make_int4((int)st[0], (int)st[1], (int)st[2], (int)st[3]);
     }
+}
+
+// ------------------------------------------------ MD5 path, staged loads
+//
+// MD5 is serial per file, so it stays one LANE per file, but the bytes do not
+// travel lane-per-file.  A lane-per-file load touches 64 files (64 pages) per
+// wave-instruction; over a batch of 100K 1-4 MiB files that is ~100K
+// concurrently open pages and the address translation, not the MD5 chain or
+// HBM, set the time.  Here each round the wave loads
+// CH bytes of each of its 64 files cooperatively: every load instruction
+// reads whole 256-byte runs of 4 files (16 lanes x 16 B each), the data is
+// written to LDS as one padded row per file, and each lane then hashes its
+// own row.  The next round's loads are in flight (asm, so hipcc cannot sink
+// them to their use) while this round is hashed.
+//
+// LDS row stride CH+16: ds_write_b128 groups (8 lanes = 128 contiguous bytes
+// of one row) and ds_read_b128 groups (16 lanes, rows l..l+15 at quad
+// (l + const) mod 16) are both conflict-free.
+constexpr int kMd5Chunk = 256;
+
+template <int CH>
+__global__ __launch_bounds__(64) void md5_stage_kernel(
+    const uint8_t *__restrict__ base, const uint64_t *__restrict__ offs,
+    const uint64_t *__restrict__ sizes, const uint32_t *__restrict__ order, uint32_t n,
+    const uint8_t *__restrict__ safe, uint8_t *__restrict__ sig_out, int32_t *__restrict__ codes_out)
+{
+    constexpr int PIECES = CH / 16;   // 16-byte pieces of one file's chunk
+    constexpr int FPI = 64 / PIECES;  // files per load instruction
+    constexpr int NLD = 64 / FPI;     // load instructions per round
+    constexpr int STRIDE = CH + 16;   // padded LDS row per file
+    constexpr int BPR = CH / 64;      // MD5 blocks per round
+    static_assert(CH == 256 && NLD == 16, "the asm wait below names 16 registers");
+    __shared__ __attribute__((aligned(16))) uint8_t sbuf[64 * STRIDE];
+    typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+
+    const int lane = threadIdx.x;
+    const uint32_t i = blockIdx.x * 64 + lane;
+    const bool valid = i < n;
+    const uint32_t f = valid ? order[i] : 0;
+    const uint64_t L = valid ? sizes[f] : 0;
+    const uint8_t *p = valid ? base + offs[f] : safe;
+    const uint64_t nblk = L >> 6;
+    uint32_t st[4] = {0x67452301u, 0xefcdab89u, 0x98badcfeu, 0x10325476u};  // my_md5_init
+
+    if (__all((((uintptr_t)p) & 15u) == 0)) {
+        uint64_t mx = nblk;
+#pragma unroll
+        for (int o = 32; o; o >>= 1) {
+            const uint64_t y = __shfl_xor(mx, o);
+            mx = y > mx ? y : mx;
+        }
+        const uint64_t rounds = (mx + BPR - 1) / BPR;
+        const int piece = lane % PIECES, fsub = lane / PIECES;
+        const uint8_t *lp[NLD];
+        uint32_t lim[NLD];  // valid 16-byte pieces (full blocks) of the loaded file
+#pragma unroll
+        for (int k = 0; k < NLD; k++) {
+            const int src = k * FPI + fsub;
+            lp[k] = reinterpret_cast<const uint8_t *>(__shfl((uintptr_t)p, src)) + piece * 16;
+            const uint64_t nb = __shfl(nblk, src);
+            lim[k] = nb >= (1ull << 30) ? 0xFFFFFFFFu : (uint32_t)(nb * 4);
+        }
+        u32x4 R[NLD];
+        auto issue = [&](uint64_t r) {
+            const uint32_t rp = (uint32_t)r * PIECES + piece;
+            const uint64_t roff = r * CH;
+#pragma unroll
+            for (int k = 0; k < NLD; k++) {
+                const uint8_t *a = (rp < lim[k]) ? lp[k] + roff : safe;
+                asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(R[k]) : "v"(a) : "memory");
+            }
+        };
+        if (rounds)
+            issue(0);
+        const uint8_t *mine = sbuf + lane * STRIDE;
+        for (uint64_t r = 0; r < rounds; r++) {
+            __syncthreads();  // the previous round's row reads precede these writes
+            asm volatile("s_waitcnt vmcnt(0)"
+                         : "+v"(R[0]), "+v"(R[1]), "+v"(R[2]), "+v"(R[3]), "+v"(R[4]), "+v"(R[5]),
+                           "+v"(R[6]), "+v"(R[7]), "+v"(R[8]), "+v"(R[9]), "+v"(R[10]),
+                           "+v"(R[11]), "+v"(R[12]), "+v"(R[13]), "+v"(R[14]), "+v"(R[15])
+                         :: "memory");
+#pragma unroll
+            for (int k = 0; k < NLD; k++)
+                *reinterpret_cast<u32x4 *>(sbuf + (k * FPI + fsub) * STRIDE + piece * 16) = R[k];
+            __syncthreads();
+            if (r + 1 < rounds)
+                issue(r + 1);
+#pragma unroll
+            for (int b = 0; b < BPR; b++) {
+                if (r * BPR + b < nblk) {
+                    const uint4 *q = reinterpret_cast<const uint4 *>(mine + b * 64);
+                    const uint4 a0 = q[0], a1 = q[1], a2 = q[2], a3 = q[3];
+                    const uint32_t m[16] = {a0.x, a0.y, a0.z, a0.w, a1.x, a1.y, a1.z, a1.w,
+                                            a2.x, a2.y, a2.z, a2.w, a3.x, a3.y, a3.z, a3.w};
+                    md5_compress(st, m);
+                }
+            }
+        }
+    } else {
+        // some file of this wave starts off a 16-byte boundary: lane-serial
+        // byte-assembled loads (rare; bulk-ingest batches are aligned)
+        for (uint64_t j = 0; j < nblk; j++) {
+            const uint8_t *q = p + j * 64;
+            const uint4 a0 = load16(q, false), a1 = load16(q + 16, false),
+                        a2 = load16(q + 32, false), a3 = load16(q + 48, false);
+            const uint32_t m[16] = {a0.x, a0.y, a0.z, a0.w, a1.x, a1.y, a1.z, a1.w,
+                                    a2.x, a2.y, a2.z, a2.w, a3.x, a3.y, a3.z, a3.w};
+            md5_compress(st, m);
+        }
+    }
+    if (!valid)
+        return;
+    md5_finish(st, p, nblk, L);
+    if (sig_out)  // memcpy(sig + 8, md5 digest, 16) (storage/storage_service.c:119)
+        store_sig(sig_out + 24ull * f, L, st[0], st[1], st[2], st[3]);
+    if (codes_out)
+        reinterpret_cast<int4 *>(codes_out)[f] =
+            make_int4((int)st[0], (int)st[1], (int)st[2], (int)st[3]);
 }
 
 // ------------------------------------------------------- segmented CRC path
@@ -439,21 +595,27 @@ __device__ __forceinline__ uint4 seg_fix_vector(uint4 w, int64_t off, int64_t a0
 // 4 KiB block grid is aligned to the segment's last full vector, so the only
 // partial vector is the first (leading neutral bytes do not change a
 // zero-init state).  See DESIGN.md "K2 segmented CRC" for the algebra.
-template <bool SAR, bool NIB>
-__device__ __forceinline__ uint32_t chain16x(const uint32_t *sD, uint32_t lb, uint32_t c, uint4 w,
-                                             uint32_t K16)
+// Table modes of the segmented kernel: 0 = 8-bit slice-by-16 (16 KiB),
+// 1 = nibble tables (64 KiB, v_perm addressed), 2 = rotated replicated
+// slice-by-8 (64 KiB, conflict-free; K is then K8).
+template <bool SAR, int TM>
+__device__ __forceinline__ uint32_t chain16x(const uint32_t *sD, uint32_t lb, const Rep8Lane &R,
+                                             uint32_t c, uint4 w, uint32_t K)
 {
-    if constexpr (NIB)
-        return chain16p<SAR>(sD, lb, c, w, K16);
+    if constexpr (TM == 1)
+        return chain16p<SAR>(sD, lb, c, w, K);
+    else if constexpr (TM == 2)
+        return chain16r<SAR>(sD, R, c, w, K);
     else
-        return chain16<SAR>(sD, c, w, K16);
+        return chain16<SAR>(sD, c, w, K);
 }
 
-template <bool SAR, bool NIB>
+template <bool SAR, int TM>
 __device__ __forceinline__ uint32_t crc_segment(const uint32_t *sD, const uint32_t *sT,
                                                 const uint32_t *sA, const uint32_t *sR,
-                                                uint32_t K16, const uint8_t *Ap, uint64_t len,
-                                                bool first_seg, int lane)
+                                                const Rep8Lane &R8, uint32_t K16,
+                                                const uint8_t *Ap, uint64_t len, bool first_seg,
+                                                int lane)
 {
     const uint32_t lb = (uint32_t)(lane & 31) * 4u;
     const int64_t a0 = (int64_t)((uintptr_t)Ap & 15u);  // segment start within its vector
@@ -480,7 +642,7 @@ __device__ __forceinline__ uint32_t crc_segment(const uint32_t *sD, const uint32
             }
 #pragma unroll
             for (int q = 0; q < 4; q++)
-                acc = chain16x<SAR, NIB>(sD, lb, acc, w[q], K16);
+                acc = chain16x<SAR, TM>(sD, lb, R8, acc, w[q], K16);
         }
         // blocks 1..J-1: the next block's 64 B per lane is loaded while this
         // one is folded (index clamped on the last block: no branch)
@@ -506,7 +668,7 @@ __device__ __forceinline__ uint32_t crc_segment(const uint32_t *sD, const uint32
                 w[0] = seg_fix_vector<SAR>(w[0], 16, a0, xor4);  // vector 1 opens block 1
 #pragma unroll
             for (int q = 0; q < 4; q++)
-                acc = chain16x<SAR, NIB>(sD, lb, acc, w[q], K16);
+                acc = chain16x<SAR, TM>(sD, lb, R8, acc, w[q], K16);
         }
         // wave reduction: lane group values relative to the group's end
 #pragma unroll
@@ -560,32 +722,34 @@ __device__ __forceinline__ uint32_t crc_final_const(uint64_t L)
     return 0xFFFFFFFFu ^ (L < 4 ? (0xFFFFFFFFu >> (8 * (uint32_t)L)) : 0u);
 }
 
-template <bool SAR, bool NIB>
-__global__ __launch_bounds__(512) void crc_seg_kernel(
+template <bool SAR, int TM>
+__global__ __launch_bounds__(kSegBlock) void crc_seg_kernel(
     const uint8_t *__restrict__ base, const uint64_t *__restrict__ offs,
     const uint64_t *__restrict__ sizes, const uint64_t *__restrict__ seg_first, uint32_t n,
     const DevTables *__restrict__ tabs, uint32_t *__restrict__ crc_out)
 {
-    // NIB: lane-bank-replicated nibble tables (64 KiB, v_perm addressed, no
-    // bank conflicts); the reduction tables stay in global memory (24 lookups
-    // per segment).  !NIB: 8-bit slice-by-16 tables.
-    constexpr int kD = NIB ? kNibPDwords : 16 * 256;
-    constexpr int kR = NIB ? 0 : 6 * 4 * 256;
+    // TM 1/2 (64 KiB conflict-free tables): the reduction tables stay in
+    // global memory (24 lookups per segment).  TM 0: everything in LDS.
+    constexpr int kD = TM == 1 ? kNibPDwords : (TM == 2 ? kRep8Dwords : 16 * 256);
+    constexpr int kR = TM ? 0 : 6 * 4 * 256;
     __shared__ uint32_t smem[kD + 256 + 2 * 4 * 256 + kR];
     uint32_t *sD = smem, *sT = smem + kD, *sA = sT + 256, *sS = sA + 1024;
-    const uint32_t *sR = NIB ? &tabs->t.ADVRED[0][0][0] : sS + 1024;
+    const uint32_t *sR = TM ? &tabs->t.ADVRED[0][0][0] : sS + 1024;
     lds_fill(sS, &tabs->t.ADVSEG[0][0], 4 * 256);
-    if constexpr (NIB)
+    if constexpr (TM == 1)
         lds_fill_nibp(sD, SAR ? &tabs->Nc[0][0] : &tabs->N[0][0]);
+    else if constexpr (TM == 2)
+        lds_fill_rep8(sD, SAR ? &tabs->Dc[0][0] : &tabs->t.D[0][0]);
     else
         lds_fill(sD, SAR ? &tabs->Dc[0][0] : &tabs->t.D[0][0], 16 * 256);
     lds_fill(sT, tabs->t.T, 256);
     lds_fill(sA, &tabs->t.ADV4032[0][0], 4 * 256);
-    if constexpr (!NIB)
+    if constexpr (!TM)
         lds_fill(sS + 1024, &tabs->t.ADVRED[0][0][0], 6 * 4 * 256);
     __syncthreads();
 
-    const uint32_t K16 = tabs->t.K16;
+    const uint32_t K16 = TM == 2 ? tabs->t.K8 : tabs->t.K16;
+    const Rep8Lane R8 = rep8_lane(threadIdx.x & 63);
     const int lane = threadIdx.x & 63;
     const uint64_t wpb = blockDim.x >> 6;
     const uint64_t w = (uint64_t)blockIdx.x * wpb + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -638,7 +802,7 @@ __global__ __launch_bounds__(512) void crc_seg_kernel(
         const uint8_t *fp = base + offs[f];
         const uint64_t lo_b = k * kSegBytes;
         const uint64_t hi_b = (L < lo_b + kSegBytes) ? L : lo_b + kSegBytes;
-        const uint32_t v = crc_segment<SAR, NIB>(sD, sT, sA, sR, K16, fp + lo_b, hi_b - lo_b, k == 0, lane);
+        const uint32_t v = crc_segment<SAR, TM>(sD, sT, sA, sR, R8, K16, fp + lo_b, hi_b - lo_b, k == 0, lane);
         if (run_f == f) {
             const uint64_t len = hi_b - lo_b;
             const uint32_t adv = (len == kSegBytes) ? apply4(sS, run_state)
@@ -857,30 +1021,44 @@ hipError_t launch_sig_lane(bool sar, int method, const uint8_t *base, const uint
     const unsigned g = (n + 255) / 256, g4 = (n + 1023) / 1024;
     if (ev0)
         (void)hipEventRecord(ev0, st);
+    const unsigned g7 = (n + kLaneBlock7 - 1) / kLaneBlock7;
 #define LANE_LAUNCH(S, M, V) \
-    sig_lane_kernel<S, M, V><<<(V == 4) ? g4 : g, (V == 4) ? 1024 : 256, 0, st>>>( \
+    sig_lane_kernel<S, M, V><<<(V == 4) ? g4 : ((V == 7) ? g7 : g), (V == 4) ? 1024 : ((V == 7) ? kLaneBlock7 : 256), 0, st>>>( \
         base, offs, sizes, order, n, tabs, crc_out, sig_out, codes_out)
     static int var = -1;
     if (var < 0) {  // FDFS_GPU_LANE_VARIANT: A/B of the hash-path load schedule
         const char *ev = getenv("FDFS_GPU_LANE_VARIANT");
         var = ev ? (ev[0] - '0') : 5;
-        if (var != 2 && var != 6)
+        if (var != 2 && var != 6 && var != 7)
             var = 5;
     }
-    if (method == 2) {
+    static int md5v = -1;
+    if (md5v < 0) {  // FDFS_GPU_MD5_LANE=1: the lane-per-file load path (A/B only)
+        const char *ev = getenv("FDFS_GPU_MD5_LANE");
+        md5v = (ev && ev[0] == '1') ? 1 : 0;
+    }
+    if (method == 2 && md5v == 0) {
+        md5_stage_kernel<kMd5Chunk><<<(n + 63) / 64, 64, 0, st>>>(
+            base, offs, sizes, order, n, reinterpret_cast<const uint8_t *>(tabs), sig_out,
+            codes_out);
+    } else if (method == 2) {
         if (sar)
             LANE_LAUNCH(true, 2, 0);
         else
             LANE_LAUNCH(false, 2, 0);
     } else if (sar) {
-        if (var == 5)
+        if (var == 7)
+            LANE_LAUNCH(true, 1, 7);
+        else if (var == 5)
             LANE_LAUNCH(true, 1, 5);
         else if (var == 6)
             LANE_LAUNCH(true, 1, 6);
         else
             LANE_LAUNCH(true, 1, 2);
     } else {
-        if (var == 5)
+        if (var == 7)
+            LANE_LAUNCH(false, 1, 7);
+        else if (var == 5)
             LANE_LAUNCH(false, 1, 5);
         else if (var == 6)
             LANE_LAUNCH(false, 1, 6);
@@ -904,38 +1082,49 @@ hipError_t launch_crc_seg(bool sar, const uint8_t *base, const uint64_t *offs, c
         return e;
     if (ev0)
         (void)hipEventRecord(ev0, st);
-    const bool nib = crc_tables_nibble();
-    if (sar && nib)
-        crc_seg_kernel<true, true><<<grid, 512, 0, st>>>(base, offs, sizes, seg_first, n, tabs, crc_out);
-    else if (sar)
-        crc_seg_kernel<true, false><<<grid, 512, 0, st>>>(base, offs, sizes, seg_first, n, tabs, crc_out);
-    else if (nib)
-        crc_seg_kernel<false, true><<<grid, 512, 0, st>>>(base, offs, sizes, seg_first, n, tabs, crc_out);
-    else
-        crc_seg_kernel<false, false><<<grid, 512, 0, st>>>(base, offs, sizes, seg_first, n, tabs, crc_out);
+    const int tm = crc_table_mode();
+#define SEG_LAUNCH(S, T) \
+    crc_seg_kernel<S, T><<<grid, kSegBlock, 0, st>>>(base, offs, sizes, seg_first, n, tabs, crc_out)
+    if (sar) {
+        if (tm == 2)
+            SEG_LAUNCH(true, 2);
+        else if (tm == 1)
+            SEG_LAUNCH(true, 1);
+        else
+            SEG_LAUNCH(true, 0);
+    } else {
+        if (tm == 2)
+            SEG_LAUNCH(false, 2);
+        else if (tm == 1)
+            SEG_LAUNCH(false, 1);
+        else
+            SEG_LAUNCH(false, 0);
+    }
+#undef SEG_LAUNCH
     if (ev1)
         (void)hipEventRecord(ev1, st);
     return hipGetLastError();
 }
 
-// Table form of the segmented CRC kernel: 8-bit (default) or nibble.
-// FDFS_GPU_CRC_TABLES=nib selects the nibble tables (A/B measurement only).
-bool crc_tables_nibble()
+// Table form of the segmented CRC kernel: FDFS_GPU_CRC_TABLES = rep8
+// (default, conflict-free), nib, or byte (A/B measurement only).
+int crc_table_mode()
 {
     static int v = -1;
     if (v < 0) {
         const char *e = getenv("FDFS_GPU_CRC_TABLES");
-        v = (e && e[0] == 'n') ? 1 : 0;
+        v = (e && e[0] == 'n') ? 1 : ((e && e[0] == 'b') ? 0 : 2);
     }
-    return v == 1;
+    return v;
 }
 
 int crc_seg_blocks_per_cu()
 {
     int nb = 0;
-    hipError_t e = crc_tables_nibble()
-                       ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, crc_seg_kernel<true, true>, 512, 0)
-                       : hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, crc_seg_kernel<true, false>, 512, 0);
+    const int tm = crc_table_mode();
+    hipError_t e = tm == 2   ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, crc_seg_kernel<true, 2>, kSegBlock, 0)
+                   : tm == 1 ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, crc_seg_kernel<true, 1>, kSegBlock, 0)
+                             : hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, crc_seg_kernel<true, 0>, kSegBlock, 0);
     if (e != hipSuccess)
         return 1;
     return nb > 0 ? nb : 1;

@@ -86,6 +86,17 @@ bool build_crc_tables(CrcTables &t, bool arithmetic_shift)
     }
     if (!t.sar && t.K16 != 0)
         return false;
+    // The same for 8-byte chunks: slice-by-8 uses D[8..15].
+    for (int i = 0; i < 32; i++) {
+        uint32_t e = 1u << i;
+        uint32_t r = adv_bytes(t, e, 8) ^ t.D[8 + i / 8][(e >> (8 * (i / 8))) & 0xFFu];
+        if (i < 31 && r != 0)
+            return false;
+        if (i == 31)
+            t.K8 = r;
+    }
+    if (!t.sar && t.K8 != 0)
+        return false;
 
     byte_tables_of(t, t.ADV4032, 4032);
     for (int l = 0; l < 6; l++)

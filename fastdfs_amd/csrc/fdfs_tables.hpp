@@ -17,6 +17,7 @@ struct CrcTables {
     uint32_t T[256];          // byte step table (reflected 0xEDB88320)
     uint32_t D[16][256];      // slice-by-16: byte x at chunk position p -> state at chunk end
     uint32_t K16;             // chain16 sign fix: M^16(c) = sum_j D[j][byte_j(c)] ^ (c<0 ? K16 : 0)
+    uint32_t K8;              // chain8 sign fix: M^8(c) = sum_j D[8+j][byte_j(c)] ^ (c<0 ? K8 : 0)
     uint32_t ADV4032[4][256]; // advance by 4032 zero bytes (wave stride - lane piece)
     uint32_t ADVRED[6][4][256]; // advance by 64<<t bytes, t = 0..5 (wave reduction tree)
     uint32_t ADVSEG[4][256];  // advance by one 64 KiB segment (kSegBytes)

@@ -157,3 +157,41 @@ def test_crc_paths_agree_at_scale(oracle, ctxs):
         assert c == crc_np[i] and s == sig1_np[i].tobytes(), i
     del data
     torch.cuda.empty_cache()
+
+
+def test_md5_staged_multiwave(oracle, ctxs):
+    """MD5 method over several waves of the staged kernel: files of 0 B to
+    1.2 MiB in one aligned batch (lanes finish at different rounds, partial
+    last rounds, a ragged last wave), plus one byte-misaligned file that
+    sends its wave down the lane-serial load path."""
+    rng = np.random.default_rng(31)
+    sizes = np.concatenate([rng.integers(0, 300, 70), rng.integers(300, 70000, 150),
+                            rng.integers(1 << 18, 1_200_000, 113)])
+    rng.shuffle(sizes)
+    buf, offs, sz = _packed(sizes, 16, rng, slack=64)
+    _check(oracle, ctxs[0], 0, buf, offs, sz, methods=(2,))
+    offs2 = offs.copy()
+    offs2[len(offs2) // 2] += 3
+    _check(oracle, ctxs[0], 0, buf, offs2, sz, methods=(2,))
+
+
+def test_md5_at_scale(oracle, ctxs):
+    """Config 3 shape (24K photos of 1-4 MiB, ~63 GB in HBM): a random sample
+    of files matches the oracle's CRC and MD5 signature bit for bit, and the
+    MD5 digests of the sample equal hashlib's."""
+    import hashlib
+    from fastdfs_amd import corpus as C
+    n = 24000
+    sizes = C.photo_sizes(n)
+    data, offs_t, sizes_t = C.device_batch(sizes, seed=4, device="cuda:0")
+    crc, sig, _ = ctxs[0].sig_batch(data, offs_t, sizes_t, method=2)
+    torch.cuda.synchronize()
+    sig_np, crc_np = sig.cpu().numpy(), crc.cpu().numpy().view(np.uint32)
+    offs = offs_t.cpu().numpy()
+    for i in np.random.default_rng(6).choice(n, size=120, replace=False):
+        d = data[int(offs[i]): int(offs[i] + sizes[i])].cpu().numpy()
+        c, s, _ = oracle.dio_file(d, 2, 0)
+        assert c == crc_np[i] and s == sig_np[i].tobytes(), i
+        assert sig_np[i, 8:].tobytes() == hashlib.md5(d.tobytes()).digest(), i
+    del data
+    torch.cuda.empty_cache()
