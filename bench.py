@@ -179,18 +179,18 @@ def main():
         if args.config == "c2":
             n = args.files or 1_000_000
             sizes = C.small_files_sizes(n, seed=1 + 1000 * rank)
-            method, kernel, kname = F.SIG_HASH, _lib.KERNEL_SIG_LANE, "sig_lane_kernel<SAR,1>"
+            method, kernel, kname = F.SIG_HASH, _lib.KERNEL_SIG_LANE, "sig_hash_kernel<SAR>"
             workload = ("config 2: 1M files/GPU of U[4,64] KiB, CRC32 + HASH_CODES4 signature "
                         "+ bulk dedup per step")
         elif args.config == "c3":
             n = args.files or 100_000  # the full config (~262 GB resident in HBM)
             sizes = C.photo_sizes(n, seed=3 + 1000 * rank)
-            method, kernel, kname = F.SIG_MD5, _lib.KERNEL_SIG_LANE, "sig_lane_kernel<SAR,2>"
+            method, kernel, kname = F.SIG_MD5, _lib.KERNEL_SIG_LANE, "md5_stage_kernel<256>"
             workload = f"config 3: {n} files/GPU of U[1,4] MiB, CRC32 + MD5 signature + dedup"
         else:
             n = args.files or 8
             sizes = np.full(n, 1 << 30, dtype=np.int64)
-            method, kernel, kname = F.SIG_CRC_ONLY, _lib.KERNEL_CRC_SEG, "crc_seg_kernel<SAR>"
+            method, kernel, kname = F.SIG_CRC_ONLY, _lib.KERNEL_CRC_SEG, "crc_seg_kernel<SAR,2>"
             workload = f"config 4: {n} x 1 GiB files/GPU, segmented CRC32 (64 KiB) + GF(2) combine"
         data, offs_t, sizes_t = C.device_batch(sizes, seed=2 + 1000 * rank, device=dev)
         nbytes = int(sizes.sum())

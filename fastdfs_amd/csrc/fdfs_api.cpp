@@ -79,7 +79,7 @@ struct Carve {
 
 size_t sig_ws_bytes(uint64_t n)
 {
-    size_t lane = align_up(sizeof(uint32_t) * 2 * fdfs::kSizeBins) + align_up(sizeof(uint32_t) * n);
+    size_t lane = align_up(sizeof(uint32_t) * fdfs::kLaneWsDwords) + align_up(sizeof(uint32_t) * n);
     size_t seg = align_up(sizeof(uint64_t) * n) + align_up(sizeof(uint64_t) * (n + 1)) +
                  align_up(sizeof(uint64_t) * fdfs::scan_workspace_elems(n));
     return lane + seg;  // the MD5 method runs both paths at once
@@ -183,13 +183,7 @@ int fdfs_gpu_open(int device, unsigned flags, fdfs_gpu_ctx **out)
     for (int p = 0; p < 16; p++)
         for (int x = 0; x < 256; x++)
             h->Dc[p][x] = h->t.D[p][x ^ 0xFF];
-    for (int p = 0; p < 16; p++)
-        for (int x = 0; x < 16; x++) {
-            h->N[2 * p][x] = h->t.D[p][x];
-            h->N[2 * p + 1][x] = h->t.D[p][x << 4];
-            h->Nc[2 * p][x] = h->Dc[p][x];
-            h->Nc[2 * p + 1][x] = h->Dc[p][x << 4] ^ h->Dc[p][0];
-        }
+    fdfs::build_poly_mfma_tables(h->pm);
     hipError_t e = hipMalloc(&ctx->d_tabs, sizeof(fdfs::DevTables));
     if (e == hipSuccess)
         e = hipMemcpy(ctx->d_tabs, h, sizeof(fdfs::DevTables), hipMemcpyHostToDevice);
@@ -318,7 +312,7 @@ int fdfs_gpu_sig_batch(fdfs_gpu_ctx *ctx, const fdfs_gpu_batch *batch, int metho
         e = fdfs::launch_crc_seg(ctx->sar, base, batch->offset, batch->size, n, nseg, first, bsum,
                                  ctx->d_tabs, crc_out, ctx->seg_grid, st, a, b);
     } else {
-        uint32_t *hist = cv.take<uint32_t>(2 * fdfs::kSizeBins);
+        uint32_t *hist = cv.take<uint32_t>(fdfs::kLaneWsDwords);
         uint32_t *order = cv.take<uint32_t>(n);
         if (method == FDFS_SIG_MD5) {
             // The MD5 lane kernel is latency-bound on a few waves per SIMD;

@@ -7,65 +7,14 @@
 
 namespace fdfs {
 
-// Device copy of the tables: CrcTables plus the complemented slice tables
-// used by the segmented kernel for the signed variant (see crc_seg_kernel).
+// Device copy of the tables: CrcTables, the complemented slice tables used by
+// the segmented kernel for the signed variant (see crc_seg_kernel), and the
+// matrix-core polynomial operands of sig_hash_kernel.
 struct DevTables {
     CrcTables t;
     uint32_t Dc[16][256];   // Dc[p][x] = D[p][x ^ 0xFF]
-    // nibble form of D / Dc: N[2p+h][x] = D[p][x << 4h]; replicated 32x per
-    // lane bank in LDS by the kernels (conflict-free lookups)
-    uint32_t N[32][16];
-    uint32_t Nc[32][16];
+    PolyMfmaTables pm;
 };
-
-constexpr int kNibTables = 32;
-constexpr int kNibDwords = kNibTables * 16 * 32;  // 64 KiB of LDS
-
-// Fill the lane-bank-replicated nibble tables: dword t*512 + x*32 + r = src[t][x].
-__device__ __forceinline__ void lds_fill_nib(uint32_t *dst, const uint32_t *__restrict__ src)
-{
-    for (int i = threadIdx.x; i < kNibDwords; i += blockDim.x)
-        dst[i] = src[(i >> 9) * 16 + ((i >> 5) & 15)];
-}
-
-// chain16 through the replicated nibble tables: lane l reads only bank l%32.
-// lb = (lane & 31) * 4.  32 lookups per 16 bytes, no bank conflicts.
-template <bool SAR>
-__device__ __forceinline__ uint32_t chain16n(const uint32_t *sN, uint32_t lb, uint32_t c, uint4 w,
-                                             uint32_t K16)
-{
-    const char *base = reinterpret_cast<const char *>(sN);
-    const uint32_t x = c ^ w.x;
-    const uint32_t words[4] = {x, w.y, w.z, w.w};
-    uint32_t r[4] = {0, 0, 0, 0};
-#pragma unroll
-    for (int wi = 0; wi < 4; wi++) {
-#pragma unroll
-        for (int k = 0; k < 8; k++) {
-            const uint32_t a = (((words[wi] >> (4 * k)) & 0xFu) << 7) | lb;
-            r[k & 3] ^= *reinterpret_cast<const uint32_t *>(base + a + (wi * 8 + k) * 2048);
-        }
-    }
-    uint32_t v = (r[0] ^ r[1]) ^ (r[2] ^ r[3]);
-    if (SAR)
-        v ^= (uint32_t)((int32_t)c >> 31) & K16;
-    return v;
-}
-
-// ---- nibble tables addressed with one v_perm_b32 per lookup ------------
-// Layout (64 KiB): table pair q = t/2 occupies 4 KiB; entry x of table t,
-// replica r (= lane % 32) sits at byte q*4096 + x*256 + (t&1)*128 + r*4.
-// Every lane reads only its own bank, and the address lb + (nibble << 8) is a
-// single byte permute of {nibble byte, lb byte}: v_perm_b32(v, lb, sel).
-constexpr int kNibPDwords = 16 * 1024;
-
-__device__ __forceinline__ void lds_fill_nibp(uint32_t *dst, const uint32_t *__restrict__ src)
-{
-    for (int i = threadIdx.x; i < kNibPDwords; i += blockDim.x) {
-        const int q = i >> 10, x = (i >> 6) & 15, h = (i >> 5) & 1;
-        dst[i] = src[(2 * q + h) * 16 + x];
-    }
-}
 
 // a ^ b ^ c in one VALU op (gfx950 v_bitop3_b32, truth table 0x96).
 __device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c)
@@ -73,37 +22,6 @@ __device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c)
     uint32_t r;
     asm("v_bitop3_b32 %0, %1, %2, %3 bitop3:0x96" : "=v"(r) : "v"(a), "v"(b), "v"(c));
     return r;
-}
-
-template <bool SAR>
-__device__ __forceinline__ uint32_t chain16p(const uint32_t *sN, uint32_t lb, uint32_t c, uint4 w,
-                                             uint32_t K16)
-{
-    const char *base = reinterpret_cast<const char *>(sN);
-    const uint32_t words[4] = {c ^ w.x, w.y, w.z, w.w};
-    uint32_t r0 = 0, r1 = 0;
-#pragma unroll
-    for (int wi = 0; wi < 4; wi++) {
-        const uint32_t lo = words[wi] & 0x0F0F0F0Fu;
-        const uint32_t hi = (words[wi] >> 4) & 0x0F0F0F0Fu;
-#pragma unroll
-        for (int j = 0; j < 4; j++) {
-            const int p = 4 * wi + j;  // byte position in the 16-byte chunk
-            const uint32_t sel = 0x0C0C0000u | ((4u + j) << 8);
-            const uint32_t alo = __builtin_amdgcn_perm(lo, lb, sel);
-            const uint32_t ahi = __builtin_amdgcn_perm(hi, lb, sel);
-            const uint32_t vlo = *reinterpret_cast<const uint32_t *>(base + alo + p * 4096);
-            const uint32_t vhi = *reinterpret_cast<const uint32_t *>(base + ahi + p * 4096 + 128);
-            if (j & 1)
-                r1 = xor3(r1, vlo, vhi);
-            else
-                r0 = xor3(r0, vlo, vhi);
-        }
-    }
-    uint32_t v = r0 ^ r1;
-    if (SAR)
-        v ^= (uint32_t)((int32_t)c >> 31) & K16;
-    return v;
 }
 
 // ---- conflict-free slice-by-8: rotated, replicated byte tables ----------
@@ -309,6 +227,74 @@ __device__ __forceinline__ void elf_word(uint32_t w, uint32_t &e)
     elf_byte<SAR>((w >> 8) & 0xFFu, e);
     elf_byte<SAR>((w >> 16) & 0xFFu, e);
     elf_byte<SAR>(w >> 24, e);
+}
+
+// ---- ELFHash_ex, byte k of word w ------------------------------------------
+// t = (e << 4) + b; e = t ^ ((t >> 24) & ~0xF) (the top nibble is left
+// "dirty": the next step shifts it out).  The exact step also clears the
+// bits of the top nibble that were set in t, as ELFHash_ex's `h &= ~x` does;
+// it is applied to the last byte of every 16-byte vector.
+// One word (4 bytes) of ELF steps as a single asm block: the byte select is
+// an SDWA operand of the add (v_lshl_add + v_bfe would be two half-rate
+// instructions), and hipcc pads an inline-asm result with an s_nop before
+// its first use, so the whole word is one statement.
+#define ELF_STEP(SH, BYTE)                                                        \
+    "v_lshlrev_b32 %1, 4, %0\n\t"                                                  \
+    "v_add_u32_sdwa %1, %1, %3 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:" BYTE "\n\t" \
+    SH " %2, 24, %1\n\t"                                                           \
+    "v_bitop3_b32 %0, %2, %1, %4 bitop3:0x6c\n\t"
+#define ELF_LAST(SH)                                                              \
+    "v_lshlrev_b32 %1, 4, %0\n\t"                                                  \
+    "v_add_u32_sdwa %1, %1, %3 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:BYTE_3\n\t" \
+    "v_and_b32 %0, 0xf0000000, %1\n\t"                                             \
+    SH " %2, 24, %0\n\t"                                                           \
+    "v_bitop3_b32 %0, %2, %0, %1 bitop3:0x12\n\t"
+
+// bitop3:0x6c = b ^ (a & c): e = t ^ ((t >> 24) & 0xFFFFFFF0), top nibble left
+// dirty (the next step shifts it out).  bitop3:0x12 = (c ^ a) & ~b: the exact
+// ELFHash_ex step, x = t & 0xF0000000, e = (t ^ (x >> 24)) & ~x.
+template <bool SAR, bool LAST>
+__device__ __forceinline__ void elf_word4(uint32_t w, uint32_t &e)
+{
+    uint32_t t, y;
+    const uint32_t M = 0xFFFFFFF0u;
+    if constexpr (SAR && LAST)
+        asm(ELF_STEP("v_ashrrev_i32", "BYTE_0") ELF_STEP("v_ashrrev_i32", "BYTE_1")
+                ELF_STEP("v_ashrrev_i32", "BYTE_2") ELF_LAST("v_ashrrev_i32")
+            : "+v"(e), "=&v"(t), "=&v"(y) : "v"(w), "s"(M));
+    else if constexpr (SAR)
+        asm(ELF_STEP("v_ashrrev_i32", "BYTE_0") ELF_STEP("v_ashrrev_i32", "BYTE_1")
+                ELF_STEP("v_ashrrev_i32", "BYTE_2") ELF_STEP("v_ashrrev_i32", "BYTE_3")
+            : "+v"(e), "=&v"(t), "=&v"(y) : "v"(w), "s"(M));
+    else if constexpr (LAST)
+        asm(ELF_STEP("v_lshrrev_b32", "BYTE_0") ELF_STEP("v_lshrrev_b32", "BYTE_1")
+                ELF_STEP("v_lshrrev_b32", "BYTE_2") ELF_LAST("v_lshrrev_b32")
+            : "+v"(e), "=&v"(t), "=&v"(y) : "v"(w), "s"(M));
+    else
+        asm(ELF_STEP("v_lshrrev_b32", "BYTE_0") ELF_STEP("v_lshrrev_b32", "BYTE_1")
+                ELF_STEP("v_lshrrev_b32", "BYTE_2") ELF_STEP("v_lshrrev_b32", "BYTE_3")
+            : "+v"(e), "=&v"(t), "=&v"(y) : "v"(w), "s"(M));
+}
+#undef ELF_STEP
+#undef ELF_LAST
+
+// ---- simple_hash_ex (M = 31) / Time33Hash_ex (M = 33), one word -----------
+// h4 = M^4 h + M^3 b0 + M^2 b1 + M b2 + b3 (mod 2^32).  M^3 < 2^16, so the
+// word polynomial is two v_dot4 byte planes.
+template <uint32_t M>
+struct Poly4 {
+    static constexpr uint32_t c3 = M * M * M, c2 = M * M, c1 = M;
+    static constexpr uint32_t lo = (c3 & 0xFFu) | ((c2 & 0xFFu) << 8) | ((c1 & 0xFFu) << 16) | (1u << 24);
+    static constexpr uint32_t hi = ((c3 >> 8) & 0xFFu) | (((c2 >> 8) & 0xFFu) << 8);
+    static constexpr uint32_t m4 = M * M * M * M;
+    static_assert(c3 < 65536 && c1 < 256, "two planes");
+};
+
+template <uint32_t M>
+__device__ __forceinline__ uint32_t poly_word(uint32_t h, uint32_t w)
+{
+    const uint32_t hi = __builtin_amdgcn_udot4(w, Poly4<M>::hi, 0u, false);
+    return __builtin_amdgcn_udot4(w, Poly4<M>::lo, h * Poly4<M>::m4 + (hi << 8), false);
 }
 
 __device__ __forceinline__ uint32_t bswap32(uint32_t v) { return __builtin_bswap32(v); }

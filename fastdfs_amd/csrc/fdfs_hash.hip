@@ -1,0 +1,291 @@
+// sig_hash_kernel: CRC32 + CALC_HASH_CODES4 (FDFS_SIG_HASH, config 2).
+//
+// One LANE per file (ELFHash is a byte-serial recurrence), 64 files of
+// near-equal size per wave (size-binned order), each lane streaming its own
+// file in whole 128-byte lines (8 x 16-byte loads per step, line-aligned
+// window: one L1/L2 line per lane per step).
+//
+// The kernel is VALU-issue bound.  On gfx950 v_lshl_add / v_bfe / v_perm /
+// v_dot4 / v_mul_lo / SDWA issue at half rate (profiles/r01/
+// ubench_valu_rate2.txt), so the per-byte cost is counted in full-rate slots
+// and each hash is placed where it is cheapest:
+//
+//  * CRC32_ex: slice-by-16 byte tables in LDS (1 lookup per byte).
+//  * ELFHash_ex: 4 VALU per byte (shift, SDWA byte add, shift, bitop3),
+//    one asm statement per word (fdfs_device.hpp elf_word4).
+//  * simple_hash_ex / Time33Hash_ex: over a 128-byte step each hash is
+//    h' = M^128 h + sum_pos M^(127-pos) b_pos (mod 2^32), i.e. a dot product
+//    of the bytes with fixed coefficients -- a contraction, so it runs on the
+//    i8 matrix cores.  The coefficients are split into 4 balanced int8 digit
+//    planes; per 16-byte vector one v_mfma_i32_16x16x64_i8 per hash takes
+//    the 64 lanes' vectors as A (lane l's 16 bytes are row l & 15 of k-block
+//    l >> 4) and a block-diagonal B (fdfs_tables.cpp), giving the 4 planes
+//    of every file's dot.  The running hash lives in the accumulator layout
+//    as 4 planes per file: once per step the planes are multiplied by M^128
+//    (and the 128 * sum(digits) bias of the b ^ 0x80 = b - 128 encoding is
+//    added), which is Horner's rule on each plane (multiplying by M is
+//    linear mod 2^32).  At the end the planes are summed (sum P_j << 8j),
+//    moved back to the file's lane, and the zero-padded steps of files
+//    shorter than the wave's longest are undone with M^-128 powers.
+//
+// Reference loops replaced: storage/storage_dio.c:465-515 (CRC32_ex and
+// CALC_HASH_CODES4 per chunk, FINISH_HASH_CODES4), storage/storage_service.c:
+// 106-120 (STORAGE_GEN_FILE_SIGNATURE).
+#include "fdfs_device.hpp"
+#include "fdfs_kernels.hpp"
+
+#include <cstdlib>
+
+namespace fdfs {
+
+constexpr int kHashBlock = 512;
+
+typedef int i32x4 __attribute__((ext_vector_type(4)));
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ uint32_t pow_dev(uint32_t m, uint32_t e)
+{
+    uint32_t r = 1;
+    for (; e; e >>= 1, m *= m)
+        if (e & 1)
+            r *= m;
+    return r;
+}
+
+// All four CALC_HASH_CODES4 hashes of one 16-byte vector on the lane.
+template <bool SAR, int TM>
+__device__ __forceinline__ uint32_t crc16(const uint32_t *sD, const Rep8Lane &R8, uint32_t K,
+                                          uint32_t c, uint4 q)
+{
+    if constexpr (TM == 2)
+        return chain16r<SAR>(sD, R8, c, q, K);
+    else
+        return chain16<SAR>(sD, c, q, K);
+}
+
+template <bool SAR, int TM>
+__device__ __forceinline__ void h4_lane(const uint32_t *sD, const Rep8Lane &R8, uint32_t K16,
+                                        uint4 q, uint32_t &c, uint32_t &e, uint32_t &s, uint32_t &t)
+{
+    c = crc16<SAR, TM>(sD, R8, K16, c, q);
+    elf_word4<SAR, false>(q.x, e);
+    elf_word4<SAR, false>(q.y, e);
+    elf_word4<SAR, false>(q.z, e);
+    elf_word4<SAR, true>(q.w, e);
+    s = poly_word<31>(s, q.x);
+    t = poly_word<33>(t, q.x);
+    s = poly_word<31>(s, q.y);
+    t = poly_word<33>(t, q.y);
+    s = poly_word<31>(s, q.z);
+    t = poly_word<33>(t, q.z);
+    s = poly_word<31>(s, q.w);
+    t = poly_word<33>(t, q.w);
+}
+
+template <bool SAR, int TM, int MODE>
+__global__ __launch_bounds__(TM == 2 ? 1024 : kHashBlock) void sig_hash_kernel(
+    const uint8_t *__restrict__ base, const uint64_t *__restrict__ offs,
+    const uint64_t *__restrict__ sizes, const uint32_t *__restrict__ order, uint32_t n,
+    const DevTables *__restrict__ tabs, uint32_t *__restrict__ crc_out,
+    uint8_t *__restrict__ sig_out, int32_t *__restrict__ codes_out)
+{
+    __shared__ uint32_t sD[TM == 2 ? kRep8Dwords : 16 * 256];
+    __shared__ uint32_t sT[256];
+    __shared__ uint4 sB[2 * 8 * 64];
+    if constexpr (TM == 2)
+        lds_fill_rep8(sD, &tabs->t.D[0][0]);
+    else
+        lds_fill(sD, &tabs->t.D[0][0], 16 * 256);
+    lds_fill(sT, tabs->t.T, 256);
+    lds_fill(reinterpret_cast<uint32_t *>(sB), reinterpret_cast<const uint32_t *>(&tabs->pm.B[0][0][0][0]),
+             2 * 8 * 64 * 4);
+    __syncthreads();
+
+    const int lane = threadIdx.x & 63;
+    const uint32_t wave0 = blockIdx.x * blockDim.x + (threadIdx.x & ~63u);
+    if (wave0 >= n)  // whole wave past the batch (wave-uniform: MFMAs below need every lane)
+        return;
+    const uint32_t i = wave0 + lane;
+    const bool valid = i < n;
+    const uint32_t K16 = TM == 2 ? tabs->t.K8 : tabs->t.K16;
+    const Rep8Lane R8 = rep8_lane(lane);
+    const uint8_t *safe = reinterpret_cast<const uint8_t *>(tabs);  // >= 128 readable bytes
+    const uint32_t f = valid ? order[i] : 0;
+    const uint64_t L = valid ? sizes[f] : 0;
+    const uint8_t *p = valid ? base + offs[f] : safe;
+    uint32_t c = 0xFFFFFFFFu;  // CRC32_XINIT (storage/storage_service.c:7149)
+    uint32_t e = 0, s = 0, t = 0;  // INIT_HASH_CODES4 (storage/storage_service.c:7156)
+
+    // bytes to 16-byte alignment, then vectors to 128-byte alignment (lane-serial)
+    uint64_t head = (16u - ((uintptr_t)p & 15u)) & 15u;
+    if (head > L)
+        head = L;
+    for (uint64_t k = 0; k < head; k++) {
+        const uint32_t b = p[k];
+        c = crc_byte<SAR>(sT, c, b);
+        h3_byte<SAR>(b, e, s, t);
+    }
+    const uint4 *v = reinterpret_cast<const uint4 *>(p + head);
+    const uint64_t nvec = (L - head) >> 4;
+    uint64_t lead = ((128u - ((uintptr_t)v & 127u)) & 127u) >> 4;
+    if (lead > nvec)
+        lead = nvec;
+    for (uint64_t j = 0; j < lead; j++)
+        h4_lane<SAR, TM>(sD, R8, K16, v[j], c, e, s, t);
+
+    // whole 128-byte lines: the wave steps in lockstep to its longest file
+    const uint32_t nsteps = (uint32_t)((nvec - lead) >> 3);
+    uint32_t nmax = nsteps;
+#pragma unroll
+    for (int o = 32; o; o >>= 1) {
+        const uint32_t y = __shfl_xor(nmax, o);
+        nmax = y > nmax ? y : nmax;
+    }
+    if (nmax) {
+        const uint32_t m31 = tabs->pm.m128[0], m33 = tabs->pm.m128[1];
+        const int col = lane & 15, j = col & 3, g = col >> 2;
+        const i32x4 k31 = {tabs->pm.K[0][j], tabs->pm.K[0][j], tabs->pm.K[0][j], tabs->pm.K[0][j]};
+        const i32x4 k33 = {tabs->pm.K[1][j], tabs->pm.K[1][j], tabs->pm.K[1][j], tabs->pm.K[1][j]};
+        // accumulator element r of this lane: plane j of the file in lane
+        // 16 g + 4 (lane >> 4) + r; plane 0 starts from the lane-serial state
+        i32x4 C31, C33;
+#pragma unroll
+        for (int r = 0; r < 4; r++) {
+            const int src = 16 * g + 4 * (lane >> 4) + r;
+            const uint32_t s0 = __shfl(s, src), t0 = __shfl(t, src);
+            C31[r] = j == 0 ? (int)s0 : 0;
+            C33[r] = j == 0 ? (int)t0 : 0;
+        }
+        const uint4 *w = v + lead;
+        // One 128-byte step: lane hashes for files not yet ended, then the
+        // two polynomial MFMAs per vector for every lane.
+        auto step = [&](const u32x4 (&a)[8], bool ok) {
+#pragma unroll
+            for (int r = 0; r < 4; r++) {
+                C31[r] = (int)((uint32_t)C31[r] * m31) + k31[r];
+                C33[r] = (int)((uint32_t)C33[r] * m33) + k33[r];
+            }
+#pragma unroll
+            for (int q = 0; q < 8; q++) {
+                const uint4 aq = make_uint4(a[q][0], a[q][1], a[q][2], a[q][3]);
+                if constexpr (MODE == 1) {  // PROBE: loads only
+                    if (ok)
+                        c ^= aq.x ^ aq.y ^ aq.z ^ aq.w;
+                    continue;
+                }
+                if (ok) {
+                    c = crc16<SAR, TM>(sD, R8, K16, c, aq);
+                    elf_word4<SAR, false>(aq.x, e);
+                    elf_word4<SAR, false>(aq.y, e);
+                    elf_word4<SAR, false>(aq.z, e);
+                    elf_word4<SAR, true>(aq.w, e);
+                }
+                // b - 128 as int8 (b ^ 0x80); a padded step is all-zero data
+                const uint32_t msk = ok ? 0xFFFFFFFFu : 0u;
+                const i32x4 A = {(int)((aq.x & msk) ^ 0x80808080u), (int)((aq.y & msk) ^ 0x80808080u),
+                                 (int)((aq.z & msk) ^ 0x80808080u), (int)((aq.w & msk) ^ 0x80808080u)};
+                const uint4 b31 = sB[(0 * 8 + q) * 64 + lane], b33 = sB[(1 * 8 + q) * 64 + lane];
+                const i32x4 B31 = {(int)b31.x, (int)b31.y, (int)b31.z, (int)b31.w};
+                const i32x4 B33 = {(int)b33.x, (int)b33.y, (int)b33.z, (int)b33.w};
+                C31 = __builtin_amdgcn_mfma_i32_16x16x64_i8(A, B31, C31, 0, 0, 0);
+                C33 = __builtin_amdgcn_mfma_i32_16x16x64_i8(A, B33, C33, 0, 0, 0);
+            }
+        };
+        // The next step's line is loaded while this one is hashed: two
+        // register sets, asm loads (hipcc would sink plain loads to their
+        // use), issued unconditionally (past-the-end steps read `safe`) so no
+        // register an asm load is still writing is ever copied.
+        u32x4 RA[8], RB[8];
+        auto issue = [&](u32x4 (&R)[8], uint32_t stp) {
+            const uint8_t *ln = (MODE != 2 && stp < nsteps) ? reinterpret_cast<const uint8_t *>(w + 8 * (uint64_t)stp) : safe;
+#pragma unroll
+            for (int q = 0; q < 8; q++)
+                asm volatile("global_load_dwordx4 %0, %1, off offset:%2" : "=v"(R[q]) : "v"(ln), "i"(16 * q) : "memory");
+        };
+        auto wait_older = [&](u32x4 (&R)[8]) {  // R is the older of the two sets in flight
+            asm volatile("s_waitcnt vmcnt(8)" : "+v"(R[0]), "+v"(R[1]), "+v"(R[2]), "+v"(R[3]) :: "memory");
+            asm volatile("" : "+v"(R[4]), "+v"(R[5]), "+v"(R[6]), "+v"(R[7]));
+        };
+        issue(RA, 0);
+        for (uint32_t st = 0; st < nmax; st += 2) {
+            issue(RB, st + 1);
+            wait_older(RA);
+            step(RA, st < nsteps);
+            issue(RA, st + 2);
+            wait_older(RB);
+            if (st + 1 < nmax)
+                step(RB, st + 1 < nsteps);
+        }
+        asm volatile("s_waitcnt vmcnt(0)"
+                     : "+v"(RA[0]), "+v"(RA[1]), "+v"(RA[2]), "+v"(RA[3]), "+v"(RA[4]), "+v"(RA[5]),
+                       "+v"(RA[6]), "+v"(RA[7]) :: "memory");
+        // planes -> value: sum_j P_j << 8j over the lane quad (j = lane & 3),
+        // then back to the file's lane; undo the padded steps (M^-128 each)
+        uint32_t s31 = 0, s33 = 0;
+#pragma unroll
+        for (int r = 0; r < 4; r++) {
+            uint32_t x = (uint32_t)C31[r] << (8 * j), y = (uint32_t)C33[r] << (8 * j);
+            x += __shfl_xor(x, 1);
+            y += __shfl_xor(y, 1);
+            x += __shfl_xor(x, 2);
+            y += __shfl_xor(y, 2);
+            // file lane F = 16 g' + 4 h + r has its sum in lane 4 g' + 16 h (g' = F >> 4, h = (F & 15) >> 2)
+            const int src = 4 * (lane >> 4) + 16 * ((lane & 15) >> 2);
+            const uint32_t xs = __shfl(x, src), ys = __shfl(y, src);
+            if ((lane & 3) == r) {
+                s31 = xs;
+                s33 = ys;
+            }
+        }
+        const uint32_t pad = nmax - nsteps;
+        s = s31 * pow_dev(tabs->pm.inv128[0], pad);
+        t = s33 * pow_dev(tabs->pm.inv128[1], pad);
+    }
+
+    for (uint64_t jv = lead + 8 * (uint64_t)nsteps; jv < nvec; jv++)
+        h4_lane<SAR, TM>(sD, R8, K16, v[jv], c, e, s, t);
+    for (uint64_t k = head + (nvec << 4); k < L; k++) {  // the last (L - head) & 15 bytes
+        const uint32_t b = p[k];
+        c = crc_byte<SAR>(sT, c, b);
+        h3_byte<SAR>(b, e, s, t);
+    }
+    if (!valid)
+        return;
+    c ^= 0xFFFFFFFFu;  // CRC32_FINAL / FINISH_HASH_CODES4 (storage/storage_dio.c:500,508)
+    crc_out[f] = c;
+    if (sig_out) {  // STORAGE_GEN_FILE_SIGNATURE (storage/storage_service.c:106-120)
+        uint2 *sp = reinterpret_cast<uint2 *>(sig_out + 24ull * f);
+        sp[0] = make_uint2(bswap32((uint32_t)(L >> 32)), bswap32((uint32_t)L));
+        sp[1] = make_uint2(bswap32(c), bswap32(e));
+        sp[2] = make_uint2(bswap32(s), bswap32(t));
+    }
+    if (codes_out)
+        reinterpret_cast<int4 *>(codes_out)[f] = make_int4((int)c, (int)e, (int)s, (int)t);
+}
+
+hipError_t launch_sig_hash(bool sar, const uint8_t *base, const uint64_t *offs,
+                           const uint64_t *sizes, uint32_t n, const uint32_t *order,
+                           const DevTables *tabs, uint32_t *crc_out, uint8_t *sig_out,
+                           int32_t *codes_out, hipStream_t st)
+{
+    static int mode = -1;
+    if (mode < 0) {  // FDFS_GPU_HASH_MODE (measurement probes): 1 = loads only, 2 = compute only
+        const char *ev = getenv("FDFS_GPU_HASH_MODE");
+        mode = ev ? atoi(ev) : 0;
+    }
+    const unsigned grid = (n + kHashBlock - 1) / kHashBlock;
+#define HASH_LAUNCH(S, M) \
+    sig_hash_kernel<S, 0, M><<<grid, kHashBlock, 0, st>>>(base, offs, sizes, order, n, tabs, crc_out, sig_out, codes_out)
+    if (mode == 1)
+        HASH_LAUNCH(true, 1);
+    else if (mode == 2)
+        HASH_LAUNCH(true, 2);
+    else if (sar)
+        HASH_LAUNCH(true, 0);
+    else
+        HASH_LAUNCH(false, 0);
+#undef HASH_LAUNCH
+    return hipGetLastError();
+}
+
+}  // namespace fdfs

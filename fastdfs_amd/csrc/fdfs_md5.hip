@@ -1,0 +1,292 @@
+// MD5 signature path (FDFS_SIG_MD5, file_signature_method=md5; config 3).
+//
+// Reference: my_md5_init / my_md5_update / my_md5_final (libfastcommon md5.c,
+// RSA RFC 1321 code) driven by storage/storage_dio.c:480,512 and initialised
+// at storage/storage_service.c:7160; the digest is the signature tail
+// (storage/storage_service.c:106-120).
+#include "fdfs_device.hpp"
+#include "fdfs_kernels.hpp"
+
+namespace fdfs {
+
+// ----------------------------------------------------------------- MD5 core
+
+__device__ __forceinline__ uint32_t rotl(uint32_t x, int s)
+{
+    return __builtin_amdgcn_alignbit(x, x, 32 - s);
+}
+
+#define MD5_F(b, c, d) ((d) ^ ((b) & ((c) ^ (d))))
+#define MD5_G(b, c, d) ((c) ^ ((d) & ((b) ^ (c))))
+#define MD5_H(b, c, d) ((b) ^ (c) ^ (d))
+#define MD5_I(b, c, d) ((c) ^ ((b) | ~(d)))
+#define MD5_STEP(FN, a, b, c, d, m, k, s) a = (b) + rotl((a) + FN(b, c, d) + (m) + (k), s)
+
+__device__ __forceinline__ void md5_compress(uint32_t st[4], const uint32_t m[16])
+{
+    uint32_t a = st[0], b = st[1], c = st[2], d = st[3];
+    MD5_STEP(MD5_F, a, b, c, d, m[0], 0xd76aa478u, 7);
+    MD5_STEP(MD5_F, d, a, b, c, m[1], 0xe8c7b756u, 12);
+    MD5_STEP(MD5_F, c, d, a, b, m[2], 0x242070dbu, 17);
+    MD5_STEP(MD5_F, b, c, d, a, m[3], 0xc1bdceeeu, 22);
+    MD5_STEP(MD5_F, a, b, c, d, m[4], 0xf57c0fafu, 7);
+    MD5_STEP(MD5_F, d, a, b, c, m[5], 0x4787c62au, 12);
+    MD5_STEP(MD5_F, c, d, a, b, m[6], 0xa8304613u, 17);
+    MD5_STEP(MD5_F, b, c, d, a, m[7], 0xfd469501u, 22);
+    MD5_STEP(MD5_F, a, b, c, d, m[8], 0x698098d8u, 7);
+    MD5_STEP(MD5_F, d, a, b, c, m[9], 0x8b44f7afu, 12);
+    MD5_STEP(MD5_F, c, d, a, b, m[10], 0xffff5bb1u, 17);
+    MD5_STEP(MD5_F, b, c, d, a, m[11], 0x895cd7beu, 22);
+    MD5_STEP(MD5_F, a, b, c, d, m[12], 0x6b901122u, 7);
+    MD5_STEP(MD5_F, d, a, b, c, m[13], 0xfd987193u, 12);
+    MD5_STEP(MD5_F, c, d, a, b, m[14], 0xa679438eu, 17);
+    MD5_STEP(MD5_F, b, c, d, a, m[15], 0x49b40821u, 22);
+
+    MD5_STEP(MD5_G, a, b, c, d, m[1], 0xf61e2562u, 5);
+    MD5_STEP(MD5_G, d, a, b, c, m[6], 0xc040b340u, 9);
+    MD5_STEP(MD5_G, c, d, a, b, m[11], 0x265e5a51u, 14);
+    MD5_STEP(MD5_G, b, c, d, a, m[0], 0xe9b6c7aau, 20);
+    MD5_STEP(MD5_G, a, b, c, d, m[5], 0xd62f105du, 5);
+    MD5_STEP(MD5_G, d, a, b, c, m[10], 0x02441453u, 9);
+    MD5_STEP(MD5_G, c, d, a, b, m[15], 0xd8a1e681u, 14);
+    MD5_STEP(MD5_G, b, c, d, a, m[4], 0xe7d3fbc8u, 20);
+    MD5_STEP(MD5_G, a, b, c, d, m[9], 0x21e1cde6u, 5);
+    MD5_STEP(MD5_G, d, a, b, c, m[14], 0xc33707d6u, 9);
+    MD5_STEP(MD5_G, c, d, a, b, m[3], 0xf4d50d87u, 14);
+    MD5_STEP(MD5_G, b, c, d, a, m[8], 0x455a14edu, 20);
+    MD5_STEP(MD5_G, a, b, c, d, m[13], 0xa9e3e905u, 5);
+    MD5_STEP(MD5_G, d, a, b, c, m[2], 0xfcefa3f8u, 9);
+    MD5_STEP(MD5_G, c, d, a, b, m[7], 0x676f02d9u, 14);
+    MD5_STEP(MD5_G, b, c, d, a, m[12], 0x8d2a4c8au, 20);
+
+    MD5_STEP(MD5_H, a, b, c, d, m[5], 0xfffa3942u, 4);
+    MD5_STEP(MD5_H, d, a, b, c, m[8], 0x8771f681u, 11);
+    MD5_STEP(MD5_H, c, d, a, b, m[11], 0x6d9d6122u, 16);
+    MD5_STEP(MD5_H, b, c, d, a, m[14], 0xfde5380cu, 23);
+    MD5_STEP(MD5_H, a, b, c, d, m[1], 0xa4beea44u, 4);
+    MD5_STEP(MD5_H, d, a, b, c, m[4], 0x4bdecfa9u, 11);
+    MD5_STEP(MD5_H, c, d, a, b, m[7], 0xf6bb4b60u, 16);
+    MD5_STEP(MD5_H, b, c, d, a, m[10], 0xbebfbc70u, 23);
+    MD5_STEP(MD5_H, a, b, c, d, m[13], 0x289b7ec6u, 4);
+    MD5_STEP(MD5_H, d, a, b, c, m[0], 0xeaa127fau, 11);
+    MD5_STEP(MD5_H, c, d, a, b, m[3], 0xd4ef3085u, 16);
+    MD5_STEP(MD5_H, b, c, d, a, m[6], 0x04881d05u, 23);
+    MD5_STEP(MD5_H, a, b, c, d, m[9], 0xd9d4d039u, 4);
+    MD5_STEP(MD5_H, d, a, b, c, m[12], 0xe6db99e5u, 11);
+    MD5_STEP(MD5_H, c, d, a, b, m[15], 0x1fa27cf8u, 16);
+    MD5_STEP(MD5_H, b, c, d, a, m[2], 0xc4ac5665u, 23);
+
+    MD5_STEP(MD5_I, a, b, c, d, m[0], 0xf4292244u, 6);
+    MD5_STEP(MD5_I, d, a, b, c, m[7], 0x432aff97u, 10);
+    MD5_STEP(MD5_I, c, d, a, b, m[14], 0xab9423a7u, 15);
+    MD5_STEP(MD5_I, b, c, d, a, m[5], 0xfc93a039u, 21);
+    MD5_STEP(MD5_I, a, b, c, d, m[12], 0x655b59c3u, 6);
+    MD5_STEP(MD5_I, d, a, b, c, m[3], 0x8f0ccc92u, 10);
+    MD5_STEP(MD5_I, c, d, a, b, m[10], 0xffeff47du, 15);
+    MD5_STEP(MD5_I, b, c, d, a, m[1], 0x85845dd1u, 21);
+    MD5_STEP(MD5_I, a, b, c, d, m[8], 0x6fa87e4fu, 6);
+    MD5_STEP(MD5_I, d, a, b, c, m[15], 0xfe2ce6e0u, 10);
+    MD5_STEP(MD5_I, c, d, a, b, m[6], 0xa3014314u, 15);
+    MD5_STEP(MD5_I, b, c, d, a, m[13], 0x4e0811a1u, 21);
+    MD5_STEP(MD5_I, a, b, c, d, m[4], 0xf7537e82u, 6);
+    MD5_STEP(MD5_I, d, a, b, c, m[11], 0xbd3af235u, 10);
+    MD5_STEP(MD5_I, c, d, a, b, m[2], 0x2ad7d2bbu, 15);
+    MD5_STEP(MD5_I, b, c, d, a, m[9], 0xeb86d391u, 21);
+    st[0] += a;
+    st[1] += b;
+    st[2] += c;
+    st[3] += d;
+}
+
+// 16 bytes at p; aligned -> one dwordx4, otherwise byte loads.
+__device__ __forceinline__ uint4 load16(const uint8_t *p, bool aligned)
+{
+    if (aligned)
+        return *reinterpret_cast<const uint4 *>(p);
+    uint32_t w[4];
+#pragma unroll
+    for (int d = 0; d < 4; d++)
+        w[d] = (uint32_t)p[4 * d] | ((uint32_t)p[4 * d + 1] << 8) |
+               ((uint32_t)p[4 * d + 2] << 16) | ((uint32_t)p[4 * d + 3] << 24);
+    return make_uint4(w[0], w[1], w[2], w[3]);
+}
+
+__device__ __forceinline__ void store_sig(uint8_t *sig, uint64_t L, uint32_t w2, uint32_t w3,
+                                          uint32_t w4, uint32_t w5)
+{
+    uint2 *sp = reinterpret_cast<uint2 *>(sig);
+    sp[0] = make_uint2(bswap32((uint32_t)(L >> 32)), bswap32((uint32_t)L));
+    sp[1] = make_uint2(w2, w3);
+    sp[2] = make_uint2(w4, w5);
+}
+
+// Final block(s) of a file whose first nblk full 64-byte blocks are already
+// folded into st: the L & 63 tail bytes, 0x80, zero pad and the 64-bit bit
+// length (RFC 1321 3.1-3.2; my_md5_final at storage/storage_dio.c:512).
+__device__ __forceinline__ void md5_finish(uint32_t st[4], const uint8_t *p, uint64_t nblk,
+                                           uint64_t L)
+{
+    const uint8_t *tp = p + (nblk << 6);
+    const uint32_t r = (uint32_t)(L & 63u);
+    uint32_t m[16];
+#pragma unroll
+    for (int wd = 0; wd < 16; wd++) {
+        uint32_t word = 0;
+#pragma unroll
+        for (int q = 0; q < 4; q++) {
+            const uint32_t k = 4 * wd + q;
+            uint32_t b = 0;
+            if (k < r) {
+                b = tp[k];
+            } else if (k == r) {
+                b = 0x80u;
+            }
+            word |= b << (8 * q);
+        }
+        m[wd] = word;
+    }
+    const uint64_t bits = L << 3;
+    if (r < 56) {
+        m[14] = (uint32_t)bits;
+        m[15] = (uint32_t)(bits >> 32);
+        md5_compress(st, m);
+    } else {
+        md5_compress(st, m);
+#pragma unroll
+        for (int wd = 0; wd < 14; wd++)
+            m[wd] = 0;
+        m[14] = (uint32_t)bits;
+        m[15] = (uint32_t)(bits >> 32);
+        md5_compress(st, m);
+    }
+}
+
+// ------------------------------------------------ MD5 path, staged loads
+//
+// MD5 is serial per file, so it stays one LANE per file, but the bytes do not
+// travel lane-per-file.  A lane-per-file load touches 64 files (64 pages) per
+// wave-instruction; over a batch of 100K 1-4 MiB files that is ~100K
+// concurrently open pages and the address translation, not the MD5 chain or
+// HBM, set the time.  Here each round the wave loads
+// CH bytes of each of its 64 files cooperatively: every load instruction
+// reads whole 256-byte runs of 4 files (16 lanes x 16 B each), the data is
+// written to LDS as one padded row per file, and each lane then hashes its
+// own row.  The next round's loads are in flight (asm, so hipcc cannot sink
+// them to their use) while this round is hashed.
+//
+// LDS row stride CH+16: ds_write_b128 groups (8 lanes = 128 contiguous bytes
+// of one row) and ds_read_b128 groups (16 lanes, rows l..l+15 at quad
+// (l + const) mod 16) are both conflict-free.
+constexpr int kMd5Chunk = 256;
+
+template <int CH>
+__global__ __launch_bounds__(64) void md5_stage_kernel(
+    const uint8_t *__restrict__ base, const uint64_t *__restrict__ offs,
+    const uint64_t *__restrict__ sizes, const uint32_t *__restrict__ order, uint32_t n,
+    const uint8_t *__restrict__ safe, uint8_t *__restrict__ sig_out, int32_t *__restrict__ codes_out)
+{
+    constexpr int PIECES = CH / 16;   // 16-byte pieces of one file's chunk
+    constexpr int FPI = 64 / PIECES;  // files per load instruction
+    constexpr int NLD = 64 / FPI;     // load instructions per round
+    constexpr int STRIDE = CH + 16;   // padded LDS row per file
+    constexpr int BPR = CH / 64;      // MD5 blocks per round
+    static_assert(CH == 256 && NLD == 16, "the asm wait below names 16 registers");
+    __shared__ __attribute__((aligned(16))) uint8_t sbuf[64 * STRIDE];
+    typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+
+    const int lane = threadIdx.x;
+    const uint32_t i = blockIdx.x * 64 + lane;
+    const bool valid = i < n;
+    const uint32_t f = valid ? order[i] : 0;
+    const uint64_t L = valid ? sizes[f] : 0;
+    const uint8_t *p = valid ? base + offs[f] : safe;
+    const uint64_t nblk = L >> 6;
+    uint32_t st[4] = {0x67452301u, 0xefcdab89u, 0x98badcfeu, 0x10325476u};  // my_md5_init
+
+    if (__all((((uintptr_t)p) & 15u) == 0)) {
+        uint64_t mx = nblk;
+#pragma unroll
+        for (int o = 32; o; o >>= 1) {
+            const uint64_t y = __shfl_xor(mx, o);
+            mx = y > mx ? y : mx;
+        }
+        const uint64_t rounds = (mx + BPR - 1) / BPR;
+        const int piece = lane % PIECES, fsub = lane / PIECES;
+        const uint8_t *lp[NLD];
+        uint32_t lim[NLD];  // valid 16-byte pieces (full blocks) of the loaded file
+#pragma unroll
+        for (int k = 0; k < NLD; k++) {
+            const int src = k * FPI + fsub;
+            lp[k] = reinterpret_cast<const uint8_t *>(__shfl((uintptr_t)p, src)) + piece * 16;
+            const uint64_t nb = __shfl(nblk, src);
+            lim[k] = nb >= (1ull << 30) ? 0xFFFFFFFFu : (uint32_t)(nb * 4);
+        }
+        u32x4 R[NLD];
+        auto issue = [&](uint64_t r) {
+            const uint32_t rp = (uint32_t)r * PIECES + piece;
+            const uint64_t roff = r * CH;
+#pragma unroll
+            for (int k = 0; k < NLD; k++) {
+                const uint8_t *a = (rp < lim[k]) ? lp[k] + roff : safe;
+                asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(R[k]) : "v"(a) : "memory");
+            }
+        };
+        if (rounds)
+            issue(0);
+        const uint8_t *mine = sbuf + lane * STRIDE;
+        for (uint64_t r = 0; r < rounds; r++) {
+            __syncthreads();  // the previous round's row reads precede these writes
+            asm volatile("s_waitcnt vmcnt(0)"
+                         : "+v"(R[0]), "+v"(R[1]), "+v"(R[2]), "+v"(R[3]), "+v"(R[4]), "+v"(R[5]),
+                           "+v"(R[6]), "+v"(R[7]), "+v"(R[8]), "+v"(R[9]), "+v"(R[10]),
+                           "+v"(R[11]), "+v"(R[12]), "+v"(R[13]), "+v"(R[14]), "+v"(R[15])
+                         :: "memory");
+#pragma unroll
+            for (int k = 0; k < NLD; k++)
+                *reinterpret_cast<u32x4 *>(sbuf + (k * FPI + fsub) * STRIDE + piece * 16) = R[k];
+            __syncthreads();
+            if (r + 1 < rounds)
+                issue(r + 1);
+#pragma unroll
+            for (int b = 0; b < BPR; b++) {
+                if (r * BPR + b < nblk) {
+                    const uint4 *q = reinterpret_cast<const uint4 *>(mine + b * 64);
+                    const uint4 a0 = q[0], a1 = q[1], a2 = q[2], a3 = q[3];
+                    const uint32_t m[16] = {a0.x, a0.y, a0.z, a0.w, a1.x, a1.y, a1.z, a1.w,
+                                            a2.x, a2.y, a2.z, a2.w, a3.x, a3.y, a3.z, a3.w};
+                    md5_compress(st, m);
+                }
+            }
+        }
+    } else {
+        // some file of this wave starts off a 16-byte boundary: lane-serial
+        // byte-assembled loads (rare; bulk-ingest batches are aligned)
+        for (uint64_t j = 0; j < nblk; j++) {
+            const uint8_t *q = p + j * 64;
+            const uint4 a0 = load16(q, false), a1 = load16(q + 16, false),
+                        a2 = load16(q + 32, false), a3 = load16(q + 48, false);
+            const uint32_t m[16] = {a0.x, a0.y, a0.z, a0.w, a1.x, a1.y, a1.z, a1.w,
+                                    a2.x, a2.y, a2.z, a2.w, a3.x, a3.y, a3.z, a3.w};
+            md5_compress(st, m);
+        }
+    }
+    if (!valid)
+        return;
+    md5_finish(st, p, nblk, L);
+    if (sig_out)  // memcpy(sig + 8, md5 digest, 16) (storage/storage_service.c:119)
+        store_sig(sig_out + 24ull * f, L, st[0], st[1], st[2], st[3]);
+    if (codes_out)
+        reinterpret_cast<int4 *>(codes_out)[f] =
+            make_int4((int)st[0], (int)st[1], (int)st[2], (int)st[3]);
+}
+
+hipError_t launch_md5_stage(const uint8_t *base, const uint64_t *offs, const uint64_t *sizes,
+                            uint32_t n, const uint32_t *order, const DevTables *tabs,
+                            uint8_t *sig_out, int32_t *codes_out, hipStream_t st)
+{
+    md5_stage_kernel<kMd5Chunk><<<(n + 63) / 64, 64, 0, st>>>(
+        base, offs, sizes, order, n, reinterpret_cast<const uint8_t *>(tabs), sig_out, codes_out);
+    return hipGetLastError();
+}
+
+}  // namespace fdfs

@@ -117,4 +117,59 @@ bool build_crc_tables(CrcTables &t, bool arithmetic_shift)
     return true;
 }
 
+static uint32_t pow_u32(uint32_t m, uint64_t e)
+{
+    uint32_t r = 1;
+    for (; e; e >>= 1, m *= m)
+        if (e & 1)
+            r *= m;
+    return r;
+}
+
+static uint32_t inv_u32(uint32_t m)  // m odd: Newton's iteration for m^-1 mod 2^32
+{
+    uint32_t x = m;  // correct to 3 bits
+    for (int i = 0; i < 5; i++)
+        x *= 2 - m * x;
+    return x;
+}
+
+// Balanced base-256 digits d0..d3 (each in [-128, 127]) with
+// sum d_i 256^i == c (mod 2^32).
+static void digits4(uint32_t c, int d[4])
+{
+    int64_t x = c;
+    for (int i = 0; i < 4; i++) {
+        int v = (int)(x & 0xFF);
+        if (v >= 128)
+            v -= 256;
+        d[i] = v;
+        x = (x - v) >> 8;
+    }
+}
+
+void build_poly_mfma_tables(PolyMfmaTables &t)
+{
+    std::memset(&t, 0, sizeof(t));
+    const uint32_t M[2] = {31u, 33u};
+    for (int h = 0; h < 2; h++) {
+        int64_t ksum[4] = {0, 0, 0, 0};
+        for (int pos = 0; pos < 128; pos++) {
+            int d[4];
+            digits4(pow_u32(M[h], 127 - pos), d);
+            for (int j = 0; j < 4; j++)
+                ksum[j] += d[j];
+            const int q = pos >> 4, e = pos & 15;
+            for (int lane = 0; lane < 64; lane++) {
+                const int col = lane & 15, kb = col >> 2, j = col & 3, g = lane >> 4;
+                t.B[h][q][lane][e] = (g == kb) ? (int8_t)d[j] : (int8_t)0;
+            }
+        }
+        for (int j = 0; j < 4; j++)
+            t.K[h][j] = (int32_t)(uint32_t)(128 * ksum[j]);
+        t.m128[h] = pow_u32(M[h], 128);
+        t.inv128[h] = inv_u32(t.m128[h]);
+    }
+}
+
 }  // namespace fdfs

@@ -25,6 +25,24 @@ struct CrcTables {
     int sar;                  // 1 = arithmetic shift (signed state)
 };
 
+// simple_hash_ex (M = 31) and Time33Hash_ex (M = 33) on the i8 matrix cores
+// (see sig_hash_kernel): over one 128-byte step the hash advances as
+//   h' = M^128 h + sum_pos M^(127 - pos) b_pos   (mod 2^32),
+// a dot product with fixed coefficients.  Each coefficient is split into
+// four balanced base-256 digits (int8), one per output "plane"; byte data
+// enters the i8 MFMA as b ^ 0x80 = b - 128 and the 128 * sum(digits) term is
+// added back per step (K).  B[h][q][lane] is the lane's 16-byte B operand for
+// vector q of the step: block-diagonal over the 4 lane groups, so one
+// v_mfma_i32_16x16x64_i8 yields the 4 planes of 64 files' 16-byte dots.
+struct PolyMfmaTables {
+    int8_t B[2][8][64][16];  // [hash 0 = M 31, 1 = M 33][vector q][lane][k element]
+    int32_t K[2][4];         // per plane: 128 * sum over the step of the digits
+    uint32_t m128[2];        // M^128 mod 2^32
+    uint32_t inv128[2];      // M^-128 mod 2^32
+};
+
+void build_poly_mfma_tables(PolyMfmaTables &t);
+
 // Returns false if an internal identity check fails (never expected).
 bool build_crc_tables(CrcTables &t, bool arithmetic_shift);
 
