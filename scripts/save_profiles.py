@@ -1,0 +1,78 @@
+"""Copy a gpu_round.sh run's evidence into profiles/<round>/ (short kernel
+names, fdfs kernels only) and refresh profiles/pmc_<config>.json, the HBM
+traffic per launch that bench.py reports as roofline.traffic.
+
+python scripts/save_profiles.py gpurun_out/round_r01b profiles/r01
+"""
+import csv
+import glob
+import json
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+from pmc_summary import load  # noqa: E402
+
+BENCH_KERNEL = {"c2": ("sig_hash_kernel<true, 0, 0>", "sig_hash_kernel<SAR>"),
+                "c3": ("md5_stage_kernel<256>", "md5_stage_kernel<256>"),
+                "c4": ("crc_seg_kernel<true, 2>", "crc_seg_kernel<SAR,2>")}
+
+
+def short(name):
+    return name.split("(")[0].replace("void ", "").replace("fdfs::", "")
+
+
+def main(src, dst):
+    os.makedirs(dst, exist_ok=True)
+    for c in ("c2", "c3", "c4", "c5"):
+        log = os.path.join(src, f"bench_{c}.log")
+        if os.path.exists(log):
+            line = open(log).read().strip().split("\n")[-1]
+            json.loads(line)
+            open(os.path.join(dst, f"bench_{c}.json"), "w").write(line + "\n")
+    for c in ("c2", "c3", "c4"):
+        for f in glob.glob(os.path.join(src, f"stats_{c}", "**", "*kernel_stats.csv"), recursive=True):
+            rows = list(csv.DictReader(open(f)))
+            with open(os.path.join(dst, f"kernel_stats_{c}.csv"), "w", newline="") as out:
+                w = csv.DictWriter(out, fieldnames=list(rows[0].keys()))
+                w.writeheader()
+                for r in rows:
+                    if "fdfs::" in r["Name"] or "rocclr" in r["Name"]:
+                        r["Name"] = short(r["Name"])
+                        w.writerow(r)
+        pm = {}
+        for kind in ("fetch", "write"):
+            d = load(os.path.join(src, f"{kind}_{c}"))
+            with open(os.path.join(dst, f"pmc_{kind}_{c}.txt"), "w") as out:
+                for k, v in d.items():
+                    if "fdfs::" in k:
+                        out.write(f"{short(k)} {json.dumps(v)}\n")
+            for k, v in d.items():
+                if BENCH_KERNEL[c][0] in k:
+                    pm.update(v)
+        if "FETCH_SIZE" in pm and "WRITE_SIZE" in pm:
+            rd, wr = 2 * pm["FETCH_SIZE"] * 1024, pm["WRITE_SIZE"] * 1024
+            rel = os.path.relpath(dst, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+            json.dump({"kernel": BENCH_KERNEL[c][1], "hbm_bytes_per_launch": round(rd + wr),
+                       "read_bytes": round(rd), "write_bytes": round(wr),
+                       "source": "rocprofv3 --pmc FETCH_SIZE and --pmc WRITE_SIZE (separate passes); "
+                                 "read = 2 x FETCH_SIZE x 1024 (gfx950 correction, MI355X_MICROARCH.md "
+                                 "HBM section), write = WRITE_SIZE x 1024",
+                       "files": [f"{rel}/pmc_fetch_{c}.txt", f"{rel}/pmc_write_{c}.txt"]},
+                      open(os.path.join(os.path.dirname(dst), f"pmc_{c}.json"), "w"), indent=1)
+    sq = load(os.path.join(src, "sq_c2"))
+    with open(os.path.join(dst, "pmc_sq_c2.txt"), "w") as out:
+        for k, v in sq.items():
+            if "fdfs::" in k:
+                out.write(f"{short(k)} {json.dumps(v)}\n")
+    with open(os.path.join(dst, "probes_c2.txt"), "w") as out:
+        for m in (1, 2):
+            log = os.path.join(src, f"probe_c2_mode{m}.log")
+            if os.path.exists(log):
+                d = json.loads(open(log).read().strip().split("\n")[-1])
+                out.write(f"FDFS_GPU_HASH_MODE={m} ({'loads only' if m == 1 else 'compute only'}): "
+                          f"kernel {d['roofline']['kernel_ms_avg']} ms\n")
+
+
+if __name__ == "__main__":
+    main(sys.argv[1], sys.argv[2])
