@@ -19,8 +19,6 @@ struct fdfs_gpu_ctx {
     bool sar = true;
     fdfs::DevTables *d_tabs = nullptr;
     unsigned seg_grid = 0;
-    hipStream_t aux = nullptr;  // second stream: CRC beside the MD5 lane kernel
-    hipEvent_t ev_fork = nullptr, ev_join = nullptr;
     void *ws = nullptr;
     size_t ws_bytes = 0;
     char err[256] = {0};
@@ -82,7 +80,7 @@ size_t sig_ws_bytes(uint64_t n)
     size_t lane = align_up(sizeof(uint32_t) * fdfs::kLaneWsDwords) + align_up(sizeof(uint32_t) * n);
     size_t seg = align_up(sizeof(uint64_t) * n) + align_up(sizeof(uint64_t) * (n + 1)) +
                  align_up(sizeof(uint64_t) * fdfs::scan_workspace_elems(n));
-    return lane + seg;  // the MD5 method runs both paths at once
+    return lane > seg ? lane : seg;  // one path per call
 }
 
 size_t dedup_ws_bytes(uint64_t n)
@@ -199,12 +197,6 @@ int fdfs_gpu_open(int device, unsigned flags, fdfs_gpu_ctx **out)
     if (hipGetDeviceProperties(&prop, device) == hipSuccess && prop.multiProcessorCount > 0)
         ncu = prop.multiProcessorCount;
     ctx->seg_grid = (unsigned)(ncu * fdfs::crc_seg_blocks_per_cu());
-    if (hipStreamCreateWithFlags(&ctx->aux, hipStreamNonBlocking) != hipSuccess ||
-        hipEventCreateWithFlags(&ctx->ev_fork, hipEventDisableTiming) != hipSuccess ||
-        hipEventCreateWithFlags(&ctx->ev_join, hipEventDisableTiming) != hipSuccess) {
-        fdfs_gpu_close(ctx);
-        return EIO;
-    }
     *out = ctx;
     return 0;
 }
@@ -223,12 +215,6 @@ int fdfs_gpu_close(fdfs_gpu_ctx *ctx)
     }
     for (auto e : ctx->pool)
         (void)hipEventDestroy(e);
-    if (ctx->ev_fork)
-        (void)hipEventDestroy(ctx->ev_fork);
-    if (ctx->ev_join)
-        (void)hipEventDestroy(ctx->ev_join);
-    if (ctx->aux)
-        (void)hipStreamDestroy(ctx->aux);
     if (ctx->d_tabs)
         (void)hipFree(ctx->d_tabs);
     delete ctx;
@@ -314,32 +300,10 @@ int fdfs_gpu_sig_batch(fdfs_gpu_ctx *ctx, const fdfs_gpu_batch *batch, int metho
     } else {
         uint32_t *hist = cv.take<uint32_t>(fdfs::kLaneWsDwords);
         uint32_t *order = cv.take<uint32_t>(n);
-        if (method == FDFS_SIG_MD5) {
-            // The MD5 lane kernel is latency-bound on a few waves per SIMD;
-            // the file CRCs run beside it on the context's second stream
-            // (the wave-parallel segmented kernel), joined back into `st`.
-            uint64_t *nseg = cv.take<uint64_t>(n);
-            uint64_t *first = cv.take<uint64_t>((size_t)n + 1);
-            uint64_t *bsum = cv.take<uint64_t>(fdfs::scan_workspace_elems(n));
-            e = hipEventRecord(ctx->ev_fork, st);
-            if (e == hipSuccess)
-                e = hipStreamWaitEvent(ctx->aux, ctx->ev_fork, 0);
-            if (e == hipSuccess)
-                e = fdfs::launch_crc_seg(ctx->sar, base, batch->offset, batch->size, n, nseg, first,
-                                         bsum, ctx->d_tabs, crc_out, ctx->seg_grid, ctx->aux,
-                                         nullptr, nullptr);
-            if (e != hipSuccess)
-                return fail(ctx, e, "sig_batch crc fork");
-        }
         hipEvent_t a, b;
         timing_pair(ctx, FDFS_KERNEL_SIG_LANE, a, b);
         e = fdfs::launch_sig_lane(ctx->sar, method, base, batch->offset, batch->size, n, hist,
                                   order, ctx->d_tabs, crc_out, sig_out, codes_out, st, a, b);
-        if (e == hipSuccess && method == FDFS_SIG_MD5) {
-            e = hipEventRecord(ctx->ev_join, ctx->aux);
-            if (e == hipSuccess)
-                e = hipStreamWaitEvent(st, ctx->ev_join, 0);
-        }
     }
     return e == hipSuccess ? 0 : fail(ctx, e, "sig_batch launch");
 }

@@ -24,9 +24,10 @@ hipError_t launch_crc_seg(bool sar, const uint8_t *base, const uint64_t *offs, c
                           uint32_t n, uint64_t *nseg, uint64_t *seg_first, uint64_t *bsum,
                           const DevTables *tabs, uint32_t *crc_out, unsigned grid, hipStream_t st,
                           hipEvent_t ev0, hipEvent_t ev1);
-hipError_t launch_md5_stage(const uint8_t *base, const uint64_t *offs, const uint64_t *sizes,
-                            uint32_t n, const uint32_t *order, const DevTables *tabs,
-                            uint8_t *sig_out, int32_t *codes_out, hipStream_t st);
+hipError_t launch_md5_stage(bool sar, const uint8_t *base, const uint64_t *offs,
+                            const uint64_t *sizes, uint32_t n, const uint32_t *order,
+                            const DevTables *tabs, uint32_t *crc_out, uint8_t *sig_out,
+                            int32_t *codes_out, hipStream_t st);
 hipError_t launch_sig_hash(bool sar, const uint8_t *base, const uint64_t *offs,
                            const uint64_t *sizes, uint32_t n, const uint32_t *order,
                            const DevTables *tabs, uint32_t *crc_out, uint8_t *sig_out,

@@ -169,39 +169,79 @@ __device__ __forceinline__ void md5_finish(uint32_t st[4], const uint8_t *p, uin
 // concurrently open pages and the address translation, not the MD5 chain or
 // HBM, set the time.  Here each round the wave loads
 // CH bytes of each of its 64 files cooperatively: every load instruction
-// reads whole 256-byte runs of 4 files (16 lanes x 16 B each), the data is
+// reads whole 128-byte lines of 8 files (8 lanes x 16 B each), the data is
 // written to LDS as one padded row per file, and each lane then hashes its
-// own row.  The next round's loads are in flight (asm, so hipcc cannot sink
-// them to their use) while this round is hashed.
+// own row.  The next round's loads are in flight while this round is hashed
+// (two register sets, asm loads so hipcc cannot sink them to their use).
 //
-// LDS row stride CH+16: ds_write_b128 groups (8 lanes = 128 contiguous bytes
-// of one row) and ds_read_b128 groups (16 lanes, rows l..l+15 at quad
-// (l + const) mod 16) are both conflict-free.
-constexpr int kMd5Chunk = 256;
+// The file's CRC32 (CRC32_ex over the same bytes, storage/storage_dio.c:467)
+// is computed by the same lane from the same LDS row: one pass over HBM for
+// CRC + MD5.  Its table lookups are independent of the MD5 chain, so they
+// fill the issue slots a latency-bound MD5 wave leaves empty.  The slice-by-16
+// tables are shared by the workgroup's waves (waves are otherwise
+// independent: no barrier after the table fill).
+//
+// LDS row stride CH+16 = 144 B: ds_write_b128 groups (8 lanes = one 128-byte
+// row) and ds_read_b128 groups (16 lanes, rows f at quad 9f + const mod 16)
+// are both conflict-free.
+constexpr int kMd5Chunk = 128;
+constexpr int kMd5Waves = 4;
 
-template <int CH>
-__global__ __launch_bounds__(64) void md5_stage_kernel(
+template <bool SAR>
+__global__ __launch_bounds__(64 * kMd5Waves) void md5_stage_kernel(
     const uint8_t *__restrict__ base, const uint64_t *__restrict__ offs,
     const uint64_t *__restrict__ sizes, const uint32_t *__restrict__ order, uint32_t n,
-    const uint8_t *__restrict__ safe, uint8_t *__restrict__ sig_out, int32_t *__restrict__ codes_out)
+    const DevTables *__restrict__ tabs, uint32_t w1, uint32_t *__restrict__ crc_out,
+    uint8_t *__restrict__ sig_out, int32_t *__restrict__ codes_out)
 {
+    constexpr int CH = kMd5Chunk;
     constexpr int PIECES = CH / 16;   // 16-byte pieces of one file's chunk
     constexpr int FPI = 64 / PIECES;  // files per load instruction
     constexpr int NLD = 64 / FPI;     // load instructions per round
     constexpr int STRIDE = CH + 16;   // padded LDS row per file
     constexpr int BPR = CH / 64;      // MD5 blocks per round
-    static_assert(CH == 256 && NLD == 16, "the asm wait below names 16 registers");
-    __shared__ __attribute__((aligned(16))) uint8_t sbuf[64 * STRIDE];
+    static_assert(NLD == 8, "the asm waits below name 8 registers");
+    __shared__ uint32_t sD[16 * 256];
+    __shared__ uint32_t sT[256];
+    __shared__ __attribute__((aligned(16))) uint8_t sbuf[kMd5Waves][64 * STRIDE];
+    lds_fill(sD, &tabs->t.D[0][0], 16 * 256);
+    lds_fill(sT, tabs->t.T, 256);
+    __syncthreads();
     typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 
-    const int lane = threadIdx.x;
-    const uint32_t i = blockIdx.x * 64 + lane;
+    const int lane = threadIdx.x & 63;
+    // Waves take 64-file chunks of the size-descending order.  Every wave is
+    // resident at once (a few per SIMD), so the kernel ends with the SIMD
+    // that holds the most bytes: the first `w1` waves (one workgroup per
+    // CU) take the largest chunks and the rest take the remaining chunks
+    // smallest first, so a CU's second workgroup is a light one.
+    const uint32_t nw = (n + 63) / 64;
+    const uint32_t w = blockIdx.x * kMd5Waves + (threadIdx.x >> 6);
+    if (w >= nw)
+        return;
+    const uint32_t chunk = (w < w1) ? w : nw - 1 - (w - w1);
+    const uint32_t wave0 = chunk * 64;
+    uint8_t *tile = sbuf[threadIdx.x >> 6];
+    const uint8_t *safe = reinterpret_cast<const uint8_t *>(tabs);  // >= 16 readable bytes
+    const uint32_t K16 = tabs->t.K16;
+    const uint32_t i = wave0 + lane;
     const bool valid = i < n;
     const uint32_t f = valid ? order[i] : 0;
     const uint64_t L = valid ? sizes[f] : 0;
     const uint8_t *p = valid ? base + offs[f] : safe;
     const uint64_t nblk = L >> 6;
     uint32_t st[4] = {0x67452301u, 0xefcdab89u, 0x98badcfeu, 0x10325476u};  // my_md5_init
+    uint32_t c = 0xFFFFFFFFu;  // CRC32_XINIT (storage/storage_service.c:7149)
+
+    auto block = [&](uint4 a0, uint4 a1, uint4 a2, uint4 a3) {
+        const uint32_t m[16] = {a0.x, a0.y, a0.z, a0.w, a1.x, a1.y, a1.z, a1.w,
+                                a2.x, a2.y, a2.z, a2.w, a3.x, a3.y, a3.z, a3.w};
+        md5_compress(st, m);
+        c = chain16<SAR>(sD, c, a0, K16);
+        c = chain16<SAR>(sD, c, a1, K16);
+        c = chain16<SAR>(sD, c, a2, K16);
+        c = chain16<SAR>(sD, c, a3, K16);
+    };
 
     if (__all((((uintptr_t)p) & 15u) == 0)) {
         uint64_t mx = nblk;
@@ -213,66 +253,69 @@ __global__ __launch_bounds__(64) void md5_stage_kernel(
         const uint64_t rounds = (mx + BPR - 1) / BPR;
         const int piece = lane % PIECES, fsub = lane / PIECES;
         const uint8_t *lp[NLD];
-        uint32_t lim[NLD];  // valid 16-byte pieces (full blocks) of the loaded file
+        uint64_t lim[NLD];  // 16-byte pieces in the loaded file's full blocks
 #pragma unroll
         for (int k = 0; k < NLD; k++) {
             const int src = k * FPI + fsub;
             lp[k] = reinterpret_cast<const uint8_t *>(__shfl((uintptr_t)p, src)) + piece * 16;
-            const uint64_t nb = __shfl(nblk, src);
-            lim[k] = nb >= (1ull << 30) ? 0xFFFFFFFFu : (uint32_t)(nb * 4);
+            lim[k] = __shfl(nblk, src) * 4;
         }
-        u32x4 R[NLD];
-        auto issue = [&](uint64_t r) {
-            const uint32_t rp = (uint32_t)r * PIECES + piece;
-            const uint64_t roff = r * CH;
+        u32x4 RA[NLD], RB[NLD];
+        auto issue = [&](u32x4 (&R)[NLD], uint64_t r) {  // unconditional: past the end reads `safe`
+            const uint64_t rp = r * PIECES + piece;
 #pragma unroll
             for (int k = 0; k < NLD; k++) {
-                const uint8_t *a = (rp < lim[k]) ? lp[k] + roff : safe;
+                const uint8_t *a = (rp < lim[k]) ? lp[k] + r * CH : safe;
                 asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(R[k]) : "v"(a) : "memory");
             }
         };
-        if (rounds)
-            issue(0);
-        const uint8_t *mine = sbuf + lane * STRIDE;
-        for (uint64_t r = 0; r < rounds; r++) {
-            __syncthreads();  // the previous round's row reads precede these writes
-            asm volatile("s_waitcnt vmcnt(0)"
-                         : "+v"(R[0]), "+v"(R[1]), "+v"(R[2]), "+v"(R[3]), "+v"(R[4]), "+v"(R[5]),
-                           "+v"(R[6]), "+v"(R[7]), "+v"(R[8]), "+v"(R[9]), "+v"(R[10]),
-                           "+v"(R[11]), "+v"(R[12]), "+v"(R[13]), "+v"(R[14]), "+v"(R[15])
-                         :: "memory");
+        auto stage = [&](u32x4 (&R)[NLD]) {  // R = the older of two sets in flight
+            asm volatile("s_waitcnt vmcnt(8)" : "+v"(R[0]), "+v"(R[1]), "+v"(R[2]), "+v"(R[3]) :: "memory");
+            asm volatile("" : "+v"(R[4]), "+v"(R[5]), "+v"(R[6]), "+v"(R[7]));
+            __builtin_amdgcn_wave_barrier();
 #pragma unroll
             for (int k = 0; k < NLD; k++)
-                *reinterpret_cast<u32x4 *>(sbuf + (k * FPI + fsub) * STRIDE + piece * 16) = R[k];
-            __syncthreads();
-            if (r + 1 < rounds)
-                issue(r + 1);
+                *reinterpret_cast<u32x4 *>(tile + (k * FPI + fsub) * STRIDE + piece * 16) = R[k];
+            __builtin_amdgcn_wave_barrier();
+        };
+        const uint8_t *mine = tile + lane * STRIDE;
+        auto hash_round = [&](uint64_t r) {
 #pragma unroll
             for (int b = 0; b < BPR; b++) {
                 if (r * BPR + b < nblk) {
                     const uint4 *q = reinterpret_cast<const uint4 *>(mine + b * 64);
-                    const uint4 a0 = q[0], a1 = q[1], a2 = q[2], a3 = q[3];
-                    const uint32_t m[16] = {a0.x, a0.y, a0.z, a0.w, a1.x, a1.y, a1.z, a1.w,
-                                            a2.x, a2.y, a2.z, a2.w, a3.x, a3.y, a3.z, a3.w};
-                    md5_compress(st, m);
+                    block(q[0], q[1], q[2], q[3]);
                 }
             }
+            __builtin_amdgcn_wave_barrier();
+        };
+        issue(RA, 0);
+        for (uint64_t r = 0; r < rounds; r += 2) {
+            issue(RB, r + 1);
+            stage(RA);
+            hash_round(r);
+            issue(RA, r + 2);
+            stage(RB);
+            if (r + 1 < rounds)
+                hash_round(r + 1);
         }
+        asm volatile("s_waitcnt vmcnt(0)"
+                     : "+v"(RA[0]), "+v"(RA[1]), "+v"(RA[2]), "+v"(RA[3]), "+v"(RA[4]), "+v"(RA[5]),
+                       "+v"(RA[6]), "+v"(RA[7]) :: "memory");
     } else {
         // some file of this wave starts off a 16-byte boundary: lane-serial
         // byte-assembled loads (rare; bulk-ingest batches are aligned)
         for (uint64_t j = 0; j < nblk; j++) {
             const uint8_t *q = p + j * 64;
-            const uint4 a0 = load16(q, false), a1 = load16(q + 16, false),
-                        a2 = load16(q + 32, false), a3 = load16(q + 48, false);
-            const uint32_t m[16] = {a0.x, a0.y, a0.z, a0.w, a1.x, a1.y, a1.z, a1.w,
-                                    a2.x, a2.y, a2.z, a2.w, a3.x, a3.y, a3.z, a3.w};
-            md5_compress(st, m);
+            block(load16(q, false), load16(q + 16, false), load16(q + 32, false), load16(q + 48, false));
         }
     }
     if (!valid)
         return;
+    for (uint64_t k = nblk << 6; k < L; k++)  // CRC of the L & 63 tail bytes
+        c = crc_byte<SAR>(sT, c, p[k]);
     md5_finish(st, p, nblk, L);
+    crc_out[f] = c ^ 0xFFFFFFFFu;  // CRC32_FINAL (storage/storage_dio.c:500)
     if (sig_out)  // memcpy(sig + 8, md5 digest, 16) (storage/storage_service.c:119)
         store_sig(sig_out + 24ull * f, L, st[0], st[1], st[2], st[3]);
     if (codes_out)
@@ -280,12 +323,30 @@ __global__ __launch_bounds__(64) void md5_stage_kernel(
             make_int4((int)st[0], (int)st[1], (int)st[2], (int)st[3]);
 }
 
-hipError_t launch_md5_stage(const uint8_t *base, const uint64_t *offs, const uint64_t *sizes,
-                            uint32_t n, const uint32_t *order, const DevTables *tabs,
-                            uint8_t *sig_out, int32_t *codes_out, hipStream_t st)
+hipError_t launch_md5_stage(bool sar, const uint8_t *base, const uint64_t *offs,
+                            const uint64_t *sizes, uint32_t n, const uint32_t *order,
+                            const DevTables *tabs, uint32_t *crc_out, uint8_t *sig_out,
+                            int32_t *codes_out, hipStream_t st)
 {
-    md5_stage_kernel<kMd5Chunk><<<(n + 63) / 64, 64, 0, st>>>(
-        base, offs, sizes, order, n, reinterpret_cast<const uint8_t *>(tabs), sig_out, codes_out);
+    static int ncu[64];
+    int dev = 0;
+    hipError_t e = hipGetDevice(&dev);
+    if (e != hipSuccess)
+        return e;
+    if (dev < 0 || dev >= 64)
+        return hipErrorInvalidDevice;
+    if (ncu[dev] == 0 &&
+        (e = hipDeviceGetAttribute(&ncu[dev], hipDeviceAttributeMultiprocessorCount, dev)) != hipSuccess)
+        return e;
+    constexpr unsigned kBlk = 64 * kMd5Waves;
+    const unsigned grid = (n + kBlk - 1) / kBlk;
+    const uint32_t w1 = (uint32_t)ncu[dev] * kMd5Waves;
+    if (sar)
+        md5_stage_kernel<true><<<grid, kBlk, 0, st>>>(base, offs, sizes, order, n, tabs, w1, crc_out,
+                                                      sig_out, codes_out);
+    else
+        md5_stage_kernel<false><<<grid, kBlk, 0, st>>>(base, offs, sizes, order, n, tabs, w1, crc_out,
+                                                       sig_out, codes_out);
     return hipGetLastError();
 }
 

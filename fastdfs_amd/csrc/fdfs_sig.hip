@@ -480,7 +480,8 @@ hipError_t launch_sig_lane(bool sar, int method, const uint8_t *base, const uint
     bin_scatter_kernel<<<hb, 1024, 0, st>>>(sizes, n, cursor, order);
     if (ev0)
         (void)hipEventRecord(ev0, st);
-    e = (method == 2) ? launch_md5_stage(base, offs, sizes, n, order, tabs, sig_out, codes_out, st)
+    e = (method == 2) ? launch_md5_stage(sar, base, offs, sizes, n, order, tabs, crc_out, sig_out,
+                                         codes_out, st)
                       : launch_sig_hash(sar, base, offs, sizes, n, order, tabs, crc_out, sig_out,
                                         codes_out, st);
     if (e != hipSuccess)
