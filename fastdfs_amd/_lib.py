@@ -30,6 +30,12 @@ EXPORTS = (
     "fdfs_gpu_dedup_group",
     "fdfs_gpu_set_timing",
     "fdfs_gpu_read_timing",
+    "fdfs_gpu_file_ids",
+    "fdfs_gpu_parse_file_ids",
+    "fdfs_gpu_trunk_pack",
+    "fdfs_gpu_trunk_unpack",
+    "fdfs_gpu_fdht_route",
+    "fdfs_gpu_scrub",
     "fdfs_gpu_last_error",
 )
 KERNEL_SIG_LANE = 0
@@ -82,6 +88,19 @@ def load() -> ctypes.CDLL:
     L.fdfs_gpu_read_timing.restype = i32
     L.fdfs_gpu_read_timing.argtypes = [vp, i32, ctypes.POINTER(ctypes.c_double),
                                        ctypes.POINTER(ctypes.c_uint64)]
+    L.fdfs_gpu_file_ids.restype = i32
+    L.fdfs_gpu_file_ids.argtypes = [vp, u32, vp, vp, vp, vp, u32, u32, vp, vp, vp]
+    L.fdfs_gpu_parse_file_ids.restype = i32
+    L.fdfs_gpu_parse_file_ids.argtypes = [vp, vp, u32, vp, vp, vp, vp, vp]
+    L.fdfs_gpu_trunk_pack.restype = i32
+    L.fdfs_gpu_trunk_pack.argtypes = [vp, vp, vp, vp, vp, vp, vp, u32, vp, vp]
+    L.fdfs_gpu_trunk_unpack.restype = i32
+    L.fdfs_gpu_trunk_unpack.argtypes = [vp, vp, u32, vp, vp, vp, vp, vp, vp, vp]
+    L.fdfs_gpu_fdht_route.restype = i32
+    L.fdfs_gpu_fdht_route.argtypes = [vp, vp, u64, ctypes.c_char_p, i32, u32, vp, vp, vp, vp, vp,
+                                      vp, vp]
+    L.fdfs_gpu_scrub.restype = i32
+    L.fdfs_gpu_scrub.argtypes = [vp, ctypes.POINTER(FdfsGpuBatch), vp, vp, vp, vp, vp]
     L.fdfs_gpu_last_error.restype = ctypes.c_char_p
     L.fdfs_gpu_last_error.argtypes = [vp]
     _lib = L

@@ -164,3 +164,104 @@ class Context:
                                               ref.data_ptr(), _stream_handle(stream)),
                  "fdfs_gpu_dedup_group")
         return rep, ref
+
+    # ------------------------------------------- formats, routing, scrub
+    def file_ids(self, server_id: int, crc32: torch.Tensor, file_size: torch.Tensor,
+                 timestamp: torch.Tensor, rnd: torch.Tensor, subdir_count: int = 256,
+                 stream=None):
+        """storage_gen_filename for a batch: (names uint8[n,27], sub_path uint8[n,2]).
+
+        crc32 int32[n] (uint32 bit pattern), file_size int64[n], timestamp
+        int32[n], rnd int32[n] (the rand() draws of COMBINE_RAND_FILE_SIZE)."""
+        for t, nm, dt in ((crc32, "crc32", torch.int32), (file_size, "file_size", torch.int64),
+                          (timestamp, "timestamp", torch.int32), (rnd, "rnd", torch.int32)):
+            _check_dev(t, nm, dt)
+        n = crc32.numel()
+        names = torch.empty((n, 27), dtype=torch.uint8, device=crc32.device)
+        sub = torch.empty((n, 2), dtype=torch.uint8, device=crc32.device)
+        self._rc(self._L.fdfs_gpu_file_ids(self._h, server_id & 0xFFFFFFFF, crc32.data_ptr(),
+                                           file_size.data_ptr(), timestamp.data_ptr(),
+                                           rnd.data_ptr(), n, subdir_count, names.data_ptr(),
+                                           sub.data_ptr(), _stream_handle(stream)),
+                 "fdfs_gpu_file_ids")
+        return names, sub
+
+    def parse_file_ids(self, names: torch.Tensor, stream=None):
+        """Decode 27-char names: (server_id int32, timestamp int32, file_size int64, crc32 int32)."""
+        _check_dev(names, "names", torch.uint8)
+        n = names.numel() // 27
+        dev = names.device
+        sid = torch.empty(n, dtype=torch.int32, device=dev)
+        ts = torch.empty(n, dtype=torch.int32, device=dev)
+        sz = torch.empty(n, dtype=torch.int64, device=dev)
+        crc = torch.empty(n, dtype=torch.int32, device=dev)
+        self._rc(self._L.fdfs_gpu_parse_file_ids(self._h, names.data_ptr(), n, sid.data_ptr(),
+                                                 ts.data_ptr(), sz.data_ptr(), crc.data_ptr(),
+                                                 _stream_handle(stream)),
+                 "fdfs_gpu_parse_file_ids")
+        return sid, ts, sz, crc
+
+    def trunk_pack(self, file_type, alloc_size, file_size, crc32, mtime, ext, stream=None):
+        """24-byte trunk headers uint8[n,24] (ext: uint8[n,7])."""
+        for t, nm, dt in ((file_type, "file_type", torch.uint8), (alloc_size, "alloc_size", torch.int32),
+                          (file_size, "file_size", torch.int32), (crc32, "crc32", torch.int32),
+                          (mtime, "mtime", torch.int32), (ext, "ext", torch.uint8)):
+            _check_dev(t, nm, dt)
+        n = crc32.numel()
+        hdr = torch.empty((n, 24), dtype=torch.uint8, device=crc32.device)
+        self._rc(self._L.fdfs_gpu_trunk_pack(self._h, file_type.data_ptr(), alloc_size.data_ptr(),
+                                             file_size.data_ptr(), crc32.data_ptr(), mtime.data_ptr(),
+                                             ext.data_ptr(), n, hdr.data_ptr(),
+                                             _stream_handle(stream)), "fdfs_gpu_trunk_pack")
+        return hdr
+
+    def trunk_unpack(self, hdr: torch.Tensor, stream=None):
+        """(file_type u8, alloc_size i32, file_size i32, crc32 i32, mtime i32, ext u8[n,7])."""
+        _check_dev(hdr, "hdr", torch.uint8)
+        n = hdr.numel() // 24
+        dev = hdr.device
+        out = (torch.empty(n, dtype=torch.uint8, device=dev), torch.empty(n, dtype=torch.int32, device=dev),
+               torch.empty(n, dtype=torch.int32, device=dev), torch.empty(n, dtype=torch.int32, device=dev),
+               torch.empty(n, dtype=torch.int32, device=dev), torch.empty((n, 7), dtype=torch.uint8, device=dev))
+        self._rc(self._L.fdfs_gpu_trunk_unpack(self._h, hdr.data_ptr(), n, *[t.data_ptr() for t in out],
+                                               _stream_handle(stream)), "fdfs_gpu_trunk_unpack")
+        return out
+
+    def fdht_route(self, sig: torch.Tensor, namespace: bytes, group_count: int,
+                   servers_per_group: torch.Tensor | None = None, stream=None):
+        """FastDHT routing of (namespace, sig, "fid") keys:
+        (key_hash int32[n], group int32[n], server int32[n], order int64[n], group_start int64[G+1])."""
+        _check_dev(sig, "sig", torch.uint8)
+        if servers_per_group is not None:
+            _check_dev(servers_per_group, "servers_per_group", torch.int32)
+        n = sig.numel() // 24
+        dev = sig.device
+        kh = torch.empty(n, dtype=torch.int32, device=dev)
+        grp = torch.empty(n, dtype=torch.int32, device=dev)
+        srv = torch.empty(n, dtype=torch.int32, device=dev)
+        order = torch.empty(n, dtype=torch.int64, device=dev)
+        start = torch.empty(group_count + 1, dtype=torch.int64, device=dev)
+        self._rc(self._L.fdfs_gpu_fdht_route(self._h, sig.data_ptr(), n, namespace, len(namespace),
+                                             group_count, _ptr(servers_per_group), kh.data_ptr(),
+                                             grp.data_ptr(), srv.data_ptr(), order.data_ptr(),
+                                             start.data_ptr(), _stream_handle(stream)),
+                 "fdfs_gpu_fdht_route")
+        return kh, grp, srv, order, start
+
+    def scrub(self, data: torch.Tensor, offsets: torch.Tensor, sizes: torch.Tensor,
+              expected_crc: torch.Tensor, stream=None):
+        """Recompute every file's CRC32 and compare: (crc int32[n], bad uint8[n], nbad int32[1])."""
+        _check_dev(data, "data", torch.uint8)
+        _check_dev(offsets, "offsets", torch.int64)
+        _check_dev(sizes, "sizes", torch.int64)
+        _check_dev(expected_crc, "expected_crc", torch.int32)
+        n = offsets.numel()
+        dev = data.device
+        crc = torch.empty(n, dtype=torch.int32, device=dev)
+        bad = torch.empty(n, dtype=torch.uint8, device=dev)
+        nbad = torch.zeros(1, dtype=torch.int32, device=dev)
+        b = _lib.FdfsGpuBatch(data.data_ptr(), offsets.data_ptr(), sizes.data_ptr(), n)
+        self._rc(self._L.fdfs_gpu_scrub(self._h, ctypes.byref(b), expected_crc.data_ptr(),
+                                        crc.data_ptr(), bad.data_ptr(), nbad.data_ptr(),
+                                        _stream_handle(stream)), "fdfs_gpu_scrub")
+        return crc, bad, nbad

@@ -375,4 +375,129 @@ int fdfs_gpu_dedup_bucket(fdfs_gpu_ctx *ctx, const uint8_t *sig, const uint64_t 
     return e == hipSuccess ? 0 : fail(ctx, e, "dedup_bucket launch");
 }
 
+// ---- formats that consume the CRC, FastDHT routing, scrub ----
+
+int fdfs_gpu_file_ids(fdfs_gpu_ctx *ctx, uint32_t server_id, const uint32_t *crc32,
+                      const int64_t *file_size, const int32_t *timestamp, const uint32_t *rnd,
+                      uint32_t n, uint32_t subdir_count, char *name_out, uint8_t *sub_path_out,
+                      void *stream)
+{
+    if (!ctx || subdir_count == 0 || subdir_count > 256)
+        return EINVAL;
+    if (n == 0)
+        return 0;
+    if (!crc32 || !file_size || !timestamp || !rnd || !name_out || !sub_path_out)
+        return EINVAL;
+    DeviceGuard g(ctx->device);
+    if (!g.ok)
+        return ENODEV;
+    hipError_t e = fdfs::launch_file_ids(ctx->sar, server_id, crc32, file_size, timestamp, rnd, n,
+                                         subdir_count, name_out, sub_path_out,
+                                         reinterpret_cast<hipStream_t>(stream));
+    return e == hipSuccess ? 0 : fail(ctx, e, "file_ids launch");
+}
+
+int fdfs_gpu_parse_file_ids(fdfs_gpu_ctx *ctx, const char *names, uint32_t n,
+                            uint32_t *server_id_out, int32_t *timestamp_out,
+                            int64_t *file_size_out, uint32_t *crc32_out, void *stream)
+{
+    if (!ctx)
+        return EINVAL;
+    if (n == 0)
+        return 0;
+    if (!names || !server_id_out || !timestamp_out || !file_size_out || !crc32_out)
+        return EINVAL;
+    DeviceGuard g(ctx->device);
+    if (!g.ok)
+        return ENODEV;
+    hipError_t e = fdfs::launch_parse_file_ids(reinterpret_cast<const uint8_t *>(names), n,
+                                               server_id_out, timestamp_out, file_size_out,
+                                               crc32_out, reinterpret_cast<hipStream_t>(stream));
+    return e == hipSuccess ? 0 : fail(ctx, e, "parse_file_ids launch");
+}
+
+int fdfs_gpu_trunk_pack(fdfs_gpu_ctx *ctx, const uint8_t *file_type, const int32_t *alloc_size,
+                        const int32_t *file_size, const uint32_t *crc32, const int32_t *mtime,
+                        const char *ext, uint32_t n, uint8_t *hdr_out, void *stream)
+{
+    if (!ctx)
+        return EINVAL;
+    if (n == 0)
+        return 0;
+    if (!file_type || !alloc_size || !file_size || !crc32 || !mtime || !ext || !hdr_out)
+        return EINVAL;
+    DeviceGuard g(ctx->device);
+    if (!g.ok)
+        return ENODEV;
+    hipError_t e = fdfs::launch_trunk_pack(file_type, alloc_size, file_size, crc32, mtime,
+                                           reinterpret_cast<const uint8_t *>(ext), n, hdr_out,
+                                           reinterpret_cast<hipStream_t>(stream));
+    return e == hipSuccess ? 0 : fail(ctx, e, "trunk_pack launch");
+}
+
+int fdfs_gpu_trunk_unpack(fdfs_gpu_ctx *ctx, const uint8_t *hdr, uint32_t n, uint8_t *file_type,
+                          int32_t *alloc_size, int32_t *file_size, uint32_t *crc32,
+                          int32_t *mtime, char *ext, void *stream)
+{
+    if (!ctx)
+        return EINVAL;
+    if (n == 0)
+        return 0;
+    if (!hdr || !file_type || !alloc_size || !file_size || !crc32 || !mtime || !ext)
+        return EINVAL;
+    DeviceGuard g(ctx->device);
+    if (!g.ok)
+        return ENODEV;
+    hipError_t e = fdfs::launch_trunk_unpack(hdr, n, file_type, alloc_size, file_size, crc32, mtime,
+                                             reinterpret_cast<uint8_t *>(ext),
+                                             reinterpret_cast<hipStream_t>(stream));
+    return e == hipSuccess ? 0 : fail(ctx, e, "trunk_unpack launch");
+}
+
+int fdfs_gpu_fdht_route(fdfs_gpu_ctx *ctx, const uint8_t *sig, uint64_t n, const char *ns,
+                        int ns_len, uint32_t group_count, const uint32_t *servers_per_group,
+                        int32_t *key_hash_out, uint32_t *group_out, uint32_t *server_out,
+                        uint64_t *order_out, uint64_t *group_start_out, void *stream)
+{
+    // FDHT_MAX_NAMESPACE_LEN (storage/fdht_client/fdht_types.h:23); an empty
+    // namespace is rejected like CALC_KEY_HASH_CODE does with an object id
+    if (!ctx || !ns || ns_len <= 0 || ns_len > 64 || group_count == 0 || !group_start_out)
+        return EINVAL;
+    if (n && (!sig || !key_hash_out || !group_out || !server_out))
+        return EINVAL;
+    if (reinterpret_cast<uintptr_t>(sig) & 7)  // the kernel reads each record as 3 x u64
+        return EINVAL;
+    DeviceGuard g(ctx->device);
+    if (!g.ok)
+        return ENODEV;
+    hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+    int rc = ensure_ws(ctx, align_up(4ull * group_count) + align_up(8ull * group_count), st);
+    if (rc)
+        return rc;
+    Carve cv{static_cast<char *>(ctx->ws)};
+    uint32_t *gcount = cv.take<uint32_t>(group_count);
+    uint64_t *cursor = cv.take<uint64_t>(group_count);
+    const uint32_t h0 = fdfs::pjw_prefix(ctx->sar, ns, ns_len);
+    hipError_t e = fdfs::launch_fdht_route(ctx->sar, sig, n, h0, group_count, servers_per_group,
+                                           key_hash_out, group_out, server_out, gcount,
+                                           group_start_out, cursor, order_out, st);
+    return e == hipSuccess ? 0 : fail(ctx, e, "fdht_route launch");
+}
+
+int fdfs_gpu_scrub(fdfs_gpu_ctx *ctx, const fdfs_gpu_batch *batch, const uint32_t *expected_crc,
+                   uint32_t *crc_out, uint8_t *bad_out, uint32_t *nbad_out, void *stream)
+{
+    if (!ctx || !batch || !expected_crc || !crc_out || !bad_out || !nbad_out)
+        return EINVAL;
+    int rc = fdfs_gpu_sig_batch(ctx, batch, FDFS_SIG_CRC_ONLY, crc_out, nullptr, nullptr, stream);
+    if (rc || batch->n == 0)
+        return rc;
+    DeviceGuard g(ctx->device);
+    if (!g.ok)
+        return ENODEV;
+    hipError_t e = fdfs::launch_scrub(crc_out, expected_crc, batch->n, bad_out, nbad_out,
+                                      reinterpret_cast<hipStream_t>(stream));
+    return e == hipSuccess ? 0 : fail(ctx, e, "scrub launch");
+}
+
 }  // extern "C"

@@ -35,6 +35,26 @@ hipError_t launch_sig_hash(bool sar, const uint8_t *base, const uint64_t *offs,
 int crc_seg_blocks_per_cu();
 int crc_table_mode();
 
+// formats, FastDHT routing, scrub (fdfs_format.hip)
+hipError_t launch_file_ids(bool sar, uint32_t server_id, const uint32_t *crc32, const int64_t *size,
+                           const int32_t *ts, const uint32_t *rnd, uint32_t n, uint32_t subdirs,
+                           char *name_out, uint8_t *sub_out, hipStream_t st);
+hipError_t launch_parse_file_ids(const uint8_t *names, uint32_t n, uint32_t *sid, int32_t *ts,
+                                 int64_t *size, uint32_t *crc, hipStream_t st);
+hipError_t launch_trunk_pack(const uint8_t *type, const int32_t *alloc, const int32_t *size,
+                             const uint32_t *crc, const int32_t *mtime, const uint8_t *ext,
+                             uint32_t n, uint8_t *hdr, hipStream_t st);
+hipError_t launch_trunk_unpack(const uint8_t *hdr, uint32_t n, uint8_t *type, int32_t *alloc,
+                               int32_t *size, uint32_t *crc, int32_t *mtime, uint8_t *ext,
+                               hipStream_t st);
+uint32_t pjw_prefix(bool sar, const char *ns, int len);
+hipError_t launch_fdht_route(bool sar, const uint8_t *sig, uint64_t n, uint32_t h0,
+                             uint32_t group_count, const uint32_t *servers, int32_t *hash_out,
+                             uint32_t *group_out, uint32_t *server_out, uint32_t *gcount,
+                             uint64_t *start, uint64_t *cursor, uint64_t *order, hipStream_t st);
+hipError_t launch_scrub(const uint32_t *crc, const uint32_t *expect, uint32_t n, uint8_t *bad,
+                        uint32_t *nbad, hipStream_t st);
+
 // dedup path (fdfs_dedup.hip)
 uint64_t dedup_table_slots(uint64_t n);
 hipError_t launch_dedup_group(const uint8_t *sig, uint32_t sig_stride, const uint64_t *gidx,

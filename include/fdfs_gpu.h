@@ -22,6 +22,15 @@
  *   fdht_get_ex1 "fid" / fdht_set_ex / fdht_inc_ex "ref" dedup decision
  *       storage/storage_service.c:2652,2714,2734,2984 -> fdfs_gpu_dedup (1 GPU)
  *       or fdfs_gpu_dedup_bucket + exchange + fdfs_gpu_dedup_group (N GPUs)
+ *   storage_gen_filename + storage_get_store_path (random mode)
+ *       storage/storage_service.c:2080-2202      -> fdfs_gpu_file_ids
+ *   fdfs_get_file_info_ex's name decode
+ *       client/storage_client.c:2133-2214        -> fdfs_gpu_parse_file_ids
+ *   trunk_pack_header / trunk_unpack_header
+ *       storage/trunk_mgr/trunk_shared.c:340-370 -> fdfs_gpu_trunk_pack / _unpack
+ *   CALC_KEY_HASH_CODE + group / server pick of the dedup keys
+ *       storage/fdht_client/fdht_client.c:207-212,256-305,375-376 -> fdfs_gpu_fdht_route
+ *   (new) CRC scrub of stored files against their file-id CRCs -> fdfs_gpu_scrub
  */
 #ifndef FDFS_GPU_H
 #define FDFS_GPU_H
@@ -116,7 +125,7 @@ int fdfs_gpu_dedup_group(fdfs_gpu_ctx *ctx, const uint8_t *records, uint64_t n,
 
 /* Kernel timing (for benchmarks and profiling).  When enabled, every call
  * records a HIP event pair on its stream around its main kernel:
- *   FDFS_KERNEL_SIG_LANE  sig_lane_kernel   (FDFS_SIG_HASH / FDFS_SIG_MD5)
+ *   FDFS_KERNEL_SIG_LANE  sig_hash_kernel / md5_stage_kernel (FDFS_SIG_HASH / FDFS_SIG_MD5)
  *   FDFS_KERNEL_CRC_SEG   crc_seg_kernel    (FDFS_SIG_CRC_ONLY)
  *   FDFS_KERNEL_DEDUP     insert + emit     (fdfs_gpu_dedup / _group)
  *   FDFS_KERNEL_BUCKET    count + scatter   (fdfs_gpu_dedup_bucket)
@@ -129,6 +138,69 @@ int fdfs_gpu_dedup_group(fdfs_gpu_ctx *ctx, const uint8_t *records, uint64_t n,
 #define FDFS_KERNEL_BUCKET   3
 int fdfs_gpu_set_timing(fdfs_gpu_ctx *ctx, int enable);
 int fdfs_gpu_read_timing(fdfs_gpu_ctx *ctx, int kernel, double *ms_out, uint64_t *launches_out);
+
+/* ---- Formats that consume the file CRC, FastDHT routing, scrub ---------- */
+
+#define FDFS_FILENAME_BASE64_LENGTH 27  /* tracker/tracker_types.h:35 */
+#define FDFS_TRUNK_HEADER_SIZE      24  /* storage/trunk_mgr/trunk_shared.h:40 */
+#define FDFS_EXT_NAME_FIELD         7   /* FDFS_FILE_EXT_NAME_MAX_LEN + 1 */
+
+/* storage_gen_filename for a batch (storage/storage_service.c:2145-2202): the
+ * 20-byte id le32(server_id) || be32(timestamp) || be64(masked size) ||
+ * be32(crc32) in FastDFS base64 (A-Z a-z 0-9 - _, no padding) -> 27 chars per
+ * file in name_out (no NUL).  masked size = COMBINE_RAND_FILE_SIZE (:2136)
+ * with the caller's rand() draw rnd[i] when the size is below 2^32, else the
+ * size (callers set the trunk / appender marks in file_size).  sub_path_out
+ * [2i], [2i+1] = sub_path_high / low of storage_get_store_path's random mode
+ * (:2128-2132): n = PJWHash(name) % 65536, (n >> 8) % subdir_count,
+ * (n & 0xFF) % subdir_count; subdir_count in [1, 256].  The logical name is
+ * "M%02d/%02X/%02X/" + name + ext, assembled by the caller.
+ * Device arrays: crc32, file_size, timestamp, rnd [n]; name_out [n*27];
+ * sub_path_out [n*2]. */
+int fdfs_gpu_file_ids(fdfs_gpu_ctx *ctx, uint32_t server_id, const uint32_t *crc32,
+                      const int64_t *file_size, const int32_t *timestamp, const uint32_t *rnd,
+                      uint32_t n, uint32_t subdir_count, char *name_out, uint8_t *sub_path_out,
+                      void *stream);
+
+/* Decode of the 27-char name core as fdfs_get_file_info_ex does
+ * (client/storage_client.c:2133-2214): server id, create timestamp, crc32 and
+ * the file size under the master-file rule (low 32 bits when the size was
+ * masked or carries the trunk mark, -1 for an appender file).  Slave names
+ * (detected there by the full name length) are the caller's to flag. */
+int fdfs_gpu_parse_file_ids(fdfs_gpu_ctx *ctx, const char *names, uint32_t n,
+                            uint32_t *server_id_out, int32_t *timestamp_out,
+                            int64_t *file_size_out, uint32_t *crc32_out, void *stream);
+
+/* trunk_pack_header / trunk_unpack_header (storage/trunk_mgr/trunk_shared.c:
+ * 340-370), 24 bytes per file: type, be32 alloc_size, be32 file_size,
+ * be32 crc32, be32 mtime, 7-byte formatted ext name (ext: n*7 bytes). */
+int fdfs_gpu_trunk_pack(fdfs_gpu_ctx *ctx, const uint8_t *file_type, const int32_t *alloc_size,
+                        const int32_t *file_size, const uint32_t *crc32, const int32_t *mtime,
+                        const char *ext, uint32_t n, uint8_t *hdr_out, void *stream);
+int fdfs_gpu_trunk_unpack(fdfs_gpu_ctx *ctx, const uint8_t *hdr, uint32_t n, uint8_t *file_type,
+                          int32_t *alloc_size, int32_t *file_size, uint32_t *crc32,
+                          int32_t *mtime, char *ext, void *stream);
+
+/* FastDHT routing of the dedup keys (ns, sig, "fid") for a batch: key_hash =
+ * PJWHash(ns || 0x01 || sig) (CALC_KEY_HASH_CODE, storage/fdht_client/
+ * fdht_client.c:256-305), group = key_hash % group_count (:375-376), server =
+ * index inside the group from get_connection's rotate-16 (:207-212;
+ * servers_per_group: device uint32[group_count], or NULL for 1 each).
+ * order_out (device uint64[n], optional) lists the records group by group
+ * (order inside a group unspecified) and group_start_out (device
+ * uint64[group_count+1]) the group boundaries: one fdht_batch_set_ex (:512)
+ * per group instead of one RPC per file.  ns: host string, 1..64 bytes. */
+int fdfs_gpu_fdht_route(fdfs_gpu_ctx *ctx, const uint8_t *sig, uint64_t n, const char *ns,
+                        int ns_len, uint32_t group_count, const uint32_t *servers_per_group,
+                        int32_t *key_hash_out, uint32_t *group_out, uint32_t *server_out,
+                        uint64_t *order_out, uint64_t *group_start_out, void *stream);
+
+/* Scrub: recompute the CRC32 of every file of the batch (as
+ * FDFS_SIG_CRC_ONLY) and compare with expected_crc (e.g. from
+ * fdfs_gpu_parse_file_ids): crc_out[n], bad_out[n] (1 = mismatch), nbad_out
+ * (device uint32, mismatch count). */
+int fdfs_gpu_scrub(fdfs_gpu_ctx *ctx, const fdfs_gpu_batch *batch, const uint32_t *expected_crc,
+                   uint32_t *crc_out, uint8_t *bad_out, uint32_t *nbad_out, void *stream);
 
 /* Last HIP error string of this context (for logging), never NULL. */
 const char *fdfs_gpu_last_error(fdfs_gpu_ctx *ctx);

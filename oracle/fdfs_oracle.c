@@ -447,3 +447,157 @@ int orc_dedup(const uint8_t *sig, uint64_t n, uint64_t *rep_out,
     free(ord);
     return 0;
 }
+
+/* ---- formats that consume the CRC, FastDHT routing -------------------- */
+
+int32_t orc_pjw_hash(const void *buf, size_t len, int variant)
+{
+    const uint8_t *p = (const uint8_t *)buf;
+    uint32_t h = 0;
+    for (size_t i = 0; i < len; i++) {
+        h = (h << 4) + p[i];
+        const uint32_t x = h & 0xF0000000u;
+        if (x) {
+            const uint32_t s = variant == ORC_VARIANT_SIGNED ? sar32(x, 24) : (x >> 24);
+            h = (h ^ s) & 0x0FFFFFFFu;
+        }
+    }
+    return (int32_t)h;
+}
+
+static const char B64[] = "ABCDEFGHIJKLMNOPQRSTUVWXYZabcdefghijklmnopqrstuvwxyz0123456789-_";
+
+int orc_base64_encode(const uint8_t *src, int len, char *dst)
+{
+    int o = 0, i = 0;
+    for (; i + 3 <= len; i += 3) {
+        const uint32_t v = ((uint32_t)src[i] << 16) | ((uint32_t)src[i + 1] << 8) | src[i + 2];
+        dst[o++] = B64[v >> 18];
+        dst[o++] = B64[(v >> 12) & 63];
+        dst[o++] = B64[(v >> 6) & 63];
+        dst[o++] = B64[v & 63];
+    }
+    if (len - i == 1) {
+        const uint32_t v = (uint32_t)src[i] << 16;
+        dst[o++] = B64[v >> 18];
+        dst[o++] = B64[(v >> 12) & 63];
+    } else if (len - i == 2) {
+        const uint32_t v = ((uint32_t)src[i] << 16) | ((uint32_t)src[i + 1] << 8);
+        dst[o++] = B64[v >> 18];
+        dst[o++] = B64[(v >> 12) & 63];
+        dst[o++] = B64[(v >> 6) & 63];
+    }
+    return o;
+}
+
+static int b64_val(char c)
+{
+    if (c >= 'A' && c <= 'Z') return c - 'A';
+    if (c >= 'a' && c <= 'z') return c - 'a' + 26;
+    if (c >= '0' && c <= '9') return c - '0' + 52;
+    if (c == '-') return 62;
+    if (c == '_') return 63;
+    return -1;
+}
+
+int orc_base64_decode(const char *src, int len, uint8_t *dst)
+{
+    uint32_t acc = 0;
+    int bits = 0, o = 0;
+    for (int i = 0; i < len; i++) {
+        const int v = b64_val(src[i]);
+        if (v < 0)
+            break;  /* pad '.' or end */
+        acc = (acc << 6) | (uint32_t)v;
+        bits += 6;
+        if (bits >= 8) {
+            bits -= 8;
+            dst[o++] = (uint8_t)(acc >> bits);
+        }
+    }
+    return o;
+}
+
+static void put_be32(uint8_t *p, uint32_t v)
+{
+    p[0] = (uint8_t)(v >> 24); p[1] = (uint8_t)(v >> 16); p[2] = (uint8_t)(v >> 8); p[3] = (uint8_t)v;
+}
+
+static uint32_t get_be32(const uint8_t *p)
+{
+    return ((uint32_t)p[0] << 24) | ((uint32_t)p[1] << 16) | ((uint32_t)p[2] << 8) | p[3];
+}
+
+void orc_file_id(uint32_t server_id, int32_t timestamp, int64_t file_size,
+                 uint32_t crc32, uint32_t rnd, int subdir_count, int variant,
+                 char name[27], uint8_t sub_path[2])
+{
+    uint8_t buff[20];
+    /* int2buff(htonl(id)) on a little-endian host: the id's LE bytes */
+    buff[0] = (uint8_t)server_id; buff[1] = (uint8_t)(server_id >> 8);
+    buff[2] = (uint8_t)(server_id >> 16); buff[3] = (uint8_t)(server_id >> 24);
+    put_be32(buff + 4, (uint32_t)timestamp);
+    uint64_t masked = (uint64_t)file_size;
+    if ((file_size >> 32) == 0) {  /* COMBINE_RAND_FILE_SIZE */
+        const uint32_t r = (rnd & 0x007FFFFFu) | 0x80000000u;
+        masked = ((uint64_t)r << 32) | (uint64_t)file_size;
+    }
+    put_be32(buff + 8, (uint32_t)(masked >> 32));
+    put_be32(buff + 12, (uint32_t)masked);
+    put_be32(buff + 16, crc32);
+    orc_base64_encode(buff, 20, name);
+    const uint32_t h = (uint32_t)orc_pjw_hash(name, 27, variant) % (1u << 16);
+    sub_path[0] = (uint8_t)(((h >> 8) & 0xFF) % (uint32_t)subdir_count);
+    sub_path[1] = (uint8_t)((h & 0xFF) % (uint32_t)subdir_count);
+}
+
+void orc_parse_file_id(const char name[27], uint32_t *server_id, int32_t *timestamp,
+                       int64_t *file_size, uint32_t *crc32)
+{
+    uint8_t buff[21];
+    orc_base64_decode(name, 27, buff);
+    *server_id = (uint32_t)buff[0] | ((uint32_t)buff[1] << 8) | ((uint32_t)buff[2] << 16) |
+                 ((uint32_t)buff[3] << 24);
+    *timestamp = (int32_t)get_be32(buff + 4);
+    int64_t sz = (int64_t)(((uint64_t)get_be32(buff + 8) << 32) | get_be32(buff + 12));
+    const int64_t kAppender = 1LL << 58, kTrunk = 1LL << 59;  /* INFINITE_FILE_SIZE, FDFS_TRUNK_FILE_MARK_SIZE */
+    *crc32 = get_be32(buff + 16);
+    if (sz & kAppender) {          /* IS_APPENDER_FILE: size -1, crc32 left 0 (:2181-2201) */
+        sz = -1;
+        *crc32 = 0;
+    } else if ((uint64_t)sz >> 63) /* master file (:2203-2213) */
+        sz &= 0xFFFFFFFFLL;
+    else if (sz & kTrunk)
+        sz &= 0xFFFFFFFFLL;        /* FDFS_TRUNK_FILE_TRUE_SIZE */
+    *file_size = sz;
+}
+
+void orc_trunk_pack(uint8_t file_type, int32_t alloc_size, int32_t file_size,
+                    uint32_t crc32, int32_t mtime, const char ext[7], uint8_t hdr[24])
+{
+    hdr[0] = file_type;
+    put_be32(hdr + 1, (uint32_t)alloc_size);
+    put_be32(hdr + 5, (uint32_t)file_size);
+    put_be32(hdr + 9, crc32);
+    put_be32(hdr + 13, (uint32_t)mtime);
+    memcpy(hdr + 17, ext, 7);
+}
+
+void orc_fdht_route(const char *ns, int ns_len, const uint8_t sig[24], uint32_t group_count,
+                    uint32_t servers, int variant, int32_t *key_hash, uint32_t *group,
+                    uint32_t *server)
+{
+    uint8_t key[64 + 1 + 24];
+    memcpy(key, ns, (size_t)ns_len);
+    key[ns_len] = 0x01;  /* FDHT_FULL_KEY_SEPERATOR */
+    memcpy(key + ns_len + 1, sig, 24);
+    int32_t h = orc_pjw_hash(key, (size_t)ns_len + 25, variant);
+    if (h < 0)
+        h &= 0x7FFFFFFF;
+    *key_hash = h;
+    *group = (uint32_t)h % group_count;
+    int32_t nh = (int32_t)(((uint32_t)h << 16) | ((uint32_t)h >> 16));
+    if (nh < 0)
+        nh &= 0x7FFFFFFF;
+    *server = (uint32_t)nh % servers;
+}

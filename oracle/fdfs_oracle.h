@@ -89,6 +89,50 @@ void orc_gen_files(uint8_t *out);
 int orc_dedup(const uint8_t *sig, uint64_t n, uint64_t *rep_out,
               uint32_t *ref_out);
 
+
+/* ---- formats that consume the CRC, FastDHT routing ------- */
+
+/* PJWHash (libfastcommon hash.c, called at storage/storage_service.c:2130 and
+ * storage/fdht_client/fdht_client.c:301): h = (h << 4) + b; if the top nibble
+ * x is set, h = (h ^ (x >> 24)) & 0x0FFFFFFF; `x >> 24` arithmetic for the
+ * signed-int state (variant 0).  PARITY UNPINNED (libfastcommon absent). */
+int32_t orc_pjw_hash(const void *buf, size_t len, int variant);
+
+/* FastDFS base64 (base64_init_ex(ctx, 0, '-', '_', '.'),
+ * storage/trunk_mgr/trunk_shared.c:32): alphabet A-Z a-z 0-9 - _, no
+ * padding (bPad = false at storage/storage_service.c:2176).  Returns the
+ * encoded / decoded length. */
+int orc_base64_encode(const uint8_t *src, int len, char *dst);
+int orc_base64_decode(const char *src, int len, uint8_t *dst);
+
+/* storage_gen_filename core (storage/storage_service.c:2145-2202):
+ * buff = le32 server_id || be32 timestamp || be64 masked size || be32 crc32
+ * (masked size = COMBINE_RAND_FILE_SIZE, :2136-2142, with rand() draw rnd,
+ * when size < 2^32); name = 27-char base64 of buff; sub_path = the random
+ * distribution of storage_get_store_path (:2128-2132). */
+void orc_file_id(uint32_t server_id, int32_t timestamp, int64_t file_size,
+                 uint32_t crc32, uint32_t rnd, int subdir_count, int variant,
+                 char name[27], uint8_t sub_path[2]);
+/* fdfs_get_file_info_ex's decode (client/storage_client.c:2133-2214) of a
+ * 27-char name: server id, timestamp, the file size under the master-file
+ * rule (low 32 bits for masked or trunk sizes, -1 for an appender), crc32. */
+void orc_parse_file_id(const char name[27], uint32_t *server_id, int32_t *timestamp,
+                       int64_t *file_size, uint32_t *crc32);
+
+/* trunk_pack_header / trunk_unpack_header (storage/trunk_mgr/trunk_shared.c:
+ * 340-370): 24 bytes = type, be32 alloc_size, be32 file_size, be32 crc32,
+ * be32 mtime, 7 bytes formatted ext name. */
+void orc_trunk_pack(uint8_t file_type, int32_t alloc_size, int32_t file_size,
+                    uint32_t crc32, int32_t mtime, const char ext[7], uint8_t hdr[24]);
+
+/* FastDHT routing of the dedup key (ns, sig24, "fid"):
+ * CALC_KEY_HASH_CODE (storage/fdht_client/fdht_client.c:256-305) over
+ * ns || 0x01 || sig, group = (unsigned)hash % group_count (:375-376), server
+ * index in the group = get_connection's rotate-16 % count (:207-212). */
+void orc_fdht_route(const char *ns, int ns_len, const uint8_t sig[24], uint32_t group_count,
+                    uint32_t servers, int variant, int32_t *key_hash, uint32_t *group,
+                    uint32_t *server);
+
 #ifdef __cplusplus
 }
 #endif

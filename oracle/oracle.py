@@ -167,3 +167,102 @@ def dedup(sig: np.ndarray) -> tuple[np.ndarray, np.ndarray]:
     ref = np.zeros(n, np.uint32)
     assert lib().orc_dedup(_ptr(sig), n, _ptr(rep), _ptr(ref)) == 0
     return rep, ref
+
+
+# ---- formats that consume the CRC, FastDHT routing ----------
+
+def _fmt_lib():
+    L = lib()
+    if not getattr(L, "_fmt_ready", False):
+        vp, i32, u32 = ctypes.c_void_p, ctypes.c_int32, ctypes.c_uint32
+        L.orc_pjw_hash.restype = i32
+        L.orc_pjw_hash.argtypes = [vp, ctypes.c_size_t, ctypes.c_int]
+        L.orc_base64_encode.restype = ctypes.c_int
+        L.orc_base64_encode.argtypes = [vp, ctypes.c_int, vp]
+        L.orc_base64_decode.restype = ctypes.c_int
+        L.orc_base64_decode.argtypes = [vp, ctypes.c_int, vp]
+        L.orc_file_id.restype = None
+        L.orc_file_id.argtypes = [u32, i32, ctypes.c_int64, u32, u32, ctypes.c_int, ctypes.c_int,
+                                  vp, vp]
+        L.orc_parse_file_id.restype = None
+        L.orc_parse_file_id.argtypes = [vp, vp, vp, vp, vp]
+        L.orc_trunk_pack.restype = None
+        L.orc_trunk_pack.argtypes = [ctypes.c_uint8, i32, i32, u32, i32, vp, vp]
+        L.orc_fdht_route.restype = None
+        L.orc_fdht_route.argtypes = [ctypes.c_char_p, ctypes.c_int, vp, u32, u32, ctypes.c_int,
+                                     vp, vp, vp]
+        L._fmt_ready = True
+    return L
+
+
+def pjw_hash(data: bytes, variant: int = VARIANT_SIGNED) -> int:
+    return _fmt_lib().orc_pjw_hash(data, len(data), variant)
+
+
+def base64_encode(data: bytes) -> bytes:
+    out = ctypes.create_string_buffer(4 * len(data) // 3 + 4)
+    n = _fmt_lib().orc_base64_encode(data, len(data), out)
+    return out.raw[:n]
+
+
+def base64_decode(text: bytes) -> bytes:
+    out = ctypes.create_string_buffer(len(text))
+    n = _fmt_lib().orc_base64_decode(text, len(text), out)
+    return out.raw[:n]
+
+
+def file_ids(server_id: int, crc32, file_size, timestamp, rnd, subdir_count: int = 256,
+             variant: int = VARIANT_SIGNED):
+    """(names uint8[n,27], sub_path uint8[n,2]) for a batch."""
+    n = len(crc32)
+    names = np.zeros((n, 27), np.uint8)
+    sub = np.zeros((n, 2), np.uint8)
+    L = _fmt_lib()
+    for i in range(n):
+        L.orc_file_id(server_id, int(timestamp[i]), int(file_size[i]), int(crc32[i]),
+                      int(rnd[i]), subdir_count, variant, names[i].ctypes.data,
+                      sub[i].ctypes.data)
+    return names, sub
+
+
+def parse_file_ids(names):
+    """(server_id u32, timestamp i32, file_size i64, crc32 u32) arrays."""
+    names = np.ascontiguousarray(names, np.uint8).reshape(-1, 27)
+    n = names.shape[0]
+    sid, ts = np.zeros(n, np.uint32), np.zeros(n, np.int32)
+    sz, crc = np.zeros(n, np.int64), np.zeros(n, np.uint32)
+    L = _fmt_lib()
+    for i in range(n):
+        L.orc_parse_file_id(names[i].ctypes.data, sid[i:].ctypes.data, ts[i:].ctypes.data,
+                            sz[i:].ctypes.data, crc[i:].ctypes.data)
+    return sid, ts, sz, crc
+
+
+def trunk_pack(file_type, alloc_size, file_size, crc32, mtime, ext):
+    """uint8[n,24] trunk headers."""
+    n = len(crc32)
+    ext = np.ascontiguousarray(ext, np.uint8).reshape(n, 7)
+    out = np.zeros((n, 24), np.uint8)
+    L = _fmt_lib()
+    for i in range(n):
+        L.orc_trunk_pack(int(file_type[i]), int(alloc_size[i]), int(file_size[i]),
+                         int(crc32[i]), int(mtime[i]), ext[i].ctypes.data, out[i].ctypes.data)
+    return out
+
+
+def fdht_route(ns: bytes, sig, group_count: int, servers_per_group,
+               variant: int = VARIANT_SIGNED):
+    """(key_hash i32, group u32, server u32) per signature."""
+    sig = np.ascontiguousarray(sig, np.uint8).reshape(-1, 24)
+    n = sig.shape[0]
+    kh, grp, srv = np.zeros(n, np.int32), np.zeros(n, np.uint32), np.zeros(n, np.uint32)
+    L = _fmt_lib()
+    for i in range(n):
+        g = ctypes.c_uint32()
+        L.orc_fdht_route(ns, len(ns), sig[i].ctypes.data, group_count, 1, variant,
+                         kh[i:].ctypes.data, ctypes.byref(g), srv[i:].ctypes.data)
+        grp[i] = g.value
+        L.orc_fdht_route(ns, len(ns), sig[i].ctypes.data, group_count,
+                         int(servers_per_group[g.value]), variant, kh[i:].ctypes.data,
+                         grp[i:].ctypes.data, srv[i:].ctypes.data)
+    return kh, grp, srv

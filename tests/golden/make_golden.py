@@ -15,6 +15,7 @@ so the signed-variant values are pinned only by the survey's record
 
 Run:  python tests/golden/make_golden.py
 """
+import base64
 import hashlib
 import json
 import os
@@ -52,6 +53,34 @@ CORPUS = {
 
 CHECK = {"input": "123456789", "crc_signed": "206AF85B", "crc_unsigned": "CBF43926"}
 
+# Real FastDFS file ids held by the reference's own PHP client tests
+# (php_client/fastdfs_test.php:3,9, php_client/fastdfs_test1.php:6).  Their
+# 27-char core is the storage_gen_filename encoding (storage/storage_service.c:
+# 2145-2202) of an older daemon (no COMBINE_RAND_FILE_SIZE mask); the second
+# one is a trunk file (size field carries FDFS_TRUNK_FILE_MARK_SIZE).
+FILE_IDS = [
+    ("php_client/fastdfs_test.php:9", "M00/00/02/wKjRbExc_qIAAAAAAABtNw6hsnM56585.part2.c"),
+    ("php_client/fastdfs_test1.php:6", "M00/01/14/wKgAxU5n9gUIAAAAAAAD8uiojuUAAAAEgP_8YAAAAQK66492"),
+    ("php_client/fastdfs_test.php:3", "M00/28/E3/U6Q-CkrMFUgAAAAAAAAIEBucRWc5452.h"),
+]
+
+
+def decode_file_id(core: str) -> dict:
+    """Independent restatement of fdfs_get_file_info_ex's decode
+    (client/storage_client.c:2133-2214) with Python's urlsafe base64 (the
+    FastDFS alphabet: A-Z a-z 0-9 - _)."""
+    b = base64.urlsafe_b64decode(core + "=")
+    sid = int.from_bytes(b[0:4], "little")          # ntohl(buff2int(buff))
+    ts = int.from_bytes(b[4:8], "big", signed=True)
+    size = int.from_bytes(b[8:16], "big", signed=True)
+    crc = int.from_bytes(b[16:20], "big")
+    if size & (1 << 58):                            # IS_APPENDER_FILE
+        size, crc = -1, 0
+    elif (size >> 63) != 0 or size & (1 << 59):     # masked / trunk: low 32 bits
+        size &= 0xFFFFFFFF
+    return {"server_id": sid, "ip": ".".join(str(x) for x in b[0:4]), "timestamp": ts,
+            "file_size": size, "crc32": "%08X" % crc, "raw_hex": b.hex()}
+
 
 def main():
     rng = np.random.default_rng(20261015)
@@ -65,7 +94,17 @@ def main():
             "crc_unsigned": "%08X" % zlib.crc32(buf),
             "md5": hashlib.md5(buf).hexdigest(),
         })
+    file_ids = []
+    for src, fid in FILE_IDS:
+        core = fid[10:10 + 27]  # FDFS_LOGIC_FILE_PATH_LEN, FDFS_FILENAME_BASE64_LENGTH
+        file_ids.append({"source": src, "file_id": fid, "core": core, **decode_file_id(core)})
+    b64 = []
+    for n in [0, 1, 2, 3, 4, 5, 19, 20, 21, 64]:
+        raw = rng.integers(0, 256, size=n, dtype=np.uint8).tobytes()
+        b64.append({"hex": raw.hex(),
+                    "enc": base64.urlsafe_b64encode(raw).decode().rstrip("=")})
     out = {"rfc1321": RFC1321, "check": CHECK, "corpus": CORPUS, "random": rand_vectors,
+           "file_ids": file_ids, "base64": b64,
            "random_note": "buffers with len > 1000 are regenerated from numpy "
                           "default_rng(20261015) in list order"}
     with open(os.path.join(HERE, "kat.json"), "w") as f:
