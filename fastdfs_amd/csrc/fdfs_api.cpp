@@ -83,11 +83,7 @@ size_t sig_ws_bytes(uint64_t n)
     return lane > seg ? lane : seg;  // one path per call
 }
 
-size_t dedup_ws_bytes(uint64_t n)
-{
-    const uint64_t c = fdfs::dedup_table_slots(n);
-    return align_up(4 * c) + align_up(8 * c) + align_up(4 * c) + align_up(4 * n) + align_up(8 * 64);
-}
+size_t dedup_ws_bytes(uint64_t n) { return fdfs::dedup_ws_bytes(n) + align_up(8 * 64); }
 
 int ensure_ws(fdfs_gpu_ctx *ctx, size_t bytes, hipStream_t st)
 {
@@ -325,16 +321,10 @@ static int dedup_common(fdfs_gpu_ctx *ctx, const uint8_t *sig, uint32_t stride,
     int rc = ensure_ws(ctx, dedup_ws_bytes(n), st);
     if (rc)
         return rc;
-    const uint64_t c = fdfs::dedup_table_slots(n);
-    Carve cv{static_cast<char *>(ctx->ws)};
-    uint32_t *slots = cv.take<uint32_t>(c);
-    uint64_t *minidx = cv.take<uint64_t>(c);
-    uint32_t *count = cv.take<uint32_t>(c);
-    uint32_t *slot_of = cv.take<uint32_t>(n);
     hipEvent_t a, b;
     timing_pair(ctx, FDFS_KERNEL_DEDUP, a, b);
-    hipError_t e = fdfs::launch_dedup_group(sig, stride, gidx, gstride, n, slots, minidx, count,
-                                            slot_of, c, rep_out, ref_out, st, a, b);
+    hipError_t e = fdfs::launch_dedup_group(sig, stride, gidx, gstride, n, ctx->ws, rep_out, ref_out,
+                                            st, a, b);
     return e == hipSuccess ? 0 : fail(ctx, e, "dedup launch");
 }
 

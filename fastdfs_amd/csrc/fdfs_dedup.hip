@@ -11,16 +11,31 @@
 //    packed per owner for one all-to-all over RCCL (the FastDHT key
 //    partition, storage/fdht_client/fdht_client.c:301-305, re-expressed as a
 //    GPU bucket).
-//  * dedup_group: on the owner, a lock-free open-addressing table keyed by the
-//    full 24 bytes: a slot is claimed by CAS of a record index and never
-//    changes, so a probe compares the immutable signature bytes of the
-//    claiming record; class min(gidx) and size via 64/32-bit atomics.
+//  * dedup_group: partition, then group each partition in LDS.
+//      K1 dp_keys      key32 = low half of a 64-bit mix of the signature;
+//                      per-tile LDS histogram of its top D1 bits
+//      K2 scan         exclusive scan of the [digit][tile] counts
+//      K3 dp_scatter   (key32, record) pairs to their D1 bucket (LDS ranks)
+//      K4 dp_split     one workgroup per D1 bucket splits it by the next D2
+//                      bits (LDS histogram + scan + LDS cursors)
+//      K5 dp_group     one workgroup per partition (~1K records): an
+//                      open-addressing table in LDS keyed by key32, a slot
+//                      is claimed by 64-bit CAS of {key32, claimer} and never
+//                      changes, equal keys are confirmed on the full 24 bytes
+//                      against the claimer's row, class min(gidx) and size
+//                      by LDS atomics, then rep/ref written per record.
+//    Every random-access atomic stays in LDS: device-scope atomics to
+//    random addresses run at a few percent of the HBM rate on MI355X
+//    (MI355X_MICROARCH.md, global atomics), which is what bounded the
+//    single global hash table this replaces (20 ms for 100M records).
+//    A partition with more records than the LDS table holds (heavy
+//    duplication of one signature, or adversarial keys) is grouped by the
+//    same code on a table in HBM, in a region of the workspace that belongs
+//    to that partition alone; results do not depend on arrival order.
 #include "fdfs_device.hpp"
 #include "fdfs_kernels.hpp"
 
 namespace fdfs {
-
-constexpr uint32_t kEmpty = 0xFFFFFFFFu;
 
 __device__ __forceinline__ uint64_t fmix64(uint64_t k)
 {
@@ -45,56 +60,297 @@ __device__ __forceinline__ uint64_t sig_hash(uint64_t a, uint64_t b, uint64_t c)
     return fmix64(a ^ fmix64(b ^ fmix64(c + 0x9E3779B97F4A7C15ull)));
 }
 
-__global__ void dedup_insert_kernel(const uint8_t *__restrict__ sig, uint32_t sig_stride,
-                                    const uint64_t *__restrict__ gidx, uint32_t gidx_stride,
-                                    uint64_t n, uint32_t *__restrict__ slots,
-                                    uint64_t *__restrict__ minidx, uint32_t *__restrict__ count,
-                                    uint32_t *__restrict__ slot_of, uint64_t mask)
+__device__ __forceinline__ bool sig_equal(const uint8_t *sig, uint32_t stride, uint32_t x, uint32_t y)
 {
-    for (uint64_t r = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; r < n;
-         r += (uint64_t)gridDim.x * blockDim.x) {
-        uint64_t a, b, c;
-        load_sig(sig + r * sig_stride, a, b, c);
-        uint64_t pos = sig_hash(a, b, c) & mask;
-        for (;;) {
-            uint32_t cur = __hip_atomic_load(&slots[pos], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            if (cur == kEmpty) {
-                cur = atomicCAS(&slots[pos], kEmpty, (uint32_t)r);
-                if (cur == kEmpty)
-                    break;  // claimed
-            }
-            uint64_t a2, b2, c2;
-            load_sig(sig + (uint64_t)cur * sig_stride, a2, b2, c2);
-            if (a2 == a && b2 == b && c2 == c)
-                break;  // same signature class
-            pos = (pos + 1) & mask;
+    uint64_t a, b, c, a2, b2, c2;
+    load_sig(sig + (uint64_t)x * stride, a, b, c);
+    load_sig(sig + (uint64_t)y * stride, a2, b2, c2);
+    return a == a2 && b == b2 && c == c2;
+}
+
+constexpr int kDpTileThreads = 256;
+constexpr int kDpTileItems = 16;
+constexpr int kDpTile = kDpTileThreads * kDpTileItems;  // records per K1/K3 tile
+constexpr int kDpMaxD1 = 8;
+constexpr int kDpMaxD2 = 12;
+constexpr int kDpSlotsLog = 11;  // LDS table: 2048 slots
+constexpr int kDpSlots = 1 << kDpSlotsLog;
+constexpr uint32_t kDpCap = kDpSlots * 3 / 4;  // records per partition grouped in LDS
+constexpr uint64_t kDpEmpty = ~0ull;
+constexpr int kDpGroupThreads = 256;
+
+struct DpPlan {
+    int d1, d2;          // partition bits: top d1 of key32 (K3), next d2 (K4)
+    uint64_t tiles;      // K1/K3 tiles
+    uint64_t nparts() const { return 1ull << (d1 + d2); }
+};
+
+DpPlan dp_plan(uint64_t n)
+{
+    int p = 1;  // partitions of ~1K records: mean n / 2^p <= 1024
+    while (p < kDpMaxD1 + kDpMaxD2 && (n >> p) > 1024)
+        p++;
+    DpPlan pl;
+    pl.d1 = p < kDpMaxD1 ? p : kDpMaxD1;
+    pl.d2 = p - pl.d1;
+    pl.tiles = (n + kDpTile - 1) / kDpTile;
+    return pl;
+}
+
+// K1: key32 per record + the tile's histogram of the top d1 bits
+__global__ __launch_bounds__(kDpTileThreads) void dp_keys_kernel(
+    const uint8_t *__restrict__ sig, uint32_t stride, const uint64_t *__restrict__ gidx,
+    uint32_t gstride, uint64_t n, int d1, uint64_t tiles, uint32_t *__restrict__ keys,
+    uint64_t *__restrict__ gk, uint64_t *__restrict__ counts)
+{
+    __shared__ uint32_t h[1 << kDpMaxD1];
+    for (int k = threadIdx.x; k < (1 << d1); k += blockDim.x)
+        h[k] = 0;
+    __syncthreads();
+    const uint64_t t0 = (uint64_t)blockIdx.x * kDpTile;
+    for (int it = 0; it < kDpTileItems; it++) {
+        const uint64_t r = t0 + (uint64_t)it * kDpTileThreads + threadIdx.x;
+        if (r < n) {
+            uint64_t a, b, c;
+            load_sig(sig + r * stride, a, b, c);
+            const uint32_t key = (uint32_t)sig_hash(a, b, c);
+            keys[r] = key;
+            gk[r] = gstride ? gidx[r * gstride] : r;
+            atomicAdd(&h[key >> (32 - d1)], 1u);
         }
-        const uint64_t g = gidx_stride ? gidx[r * gidx_stride] : r;
-        atomicMin(reinterpret_cast<unsigned long long *>(&minidx[pos]), (unsigned long long)g);
-        atomicAdd(&count[pos], 1u);
-        slot_of[r] = (uint32_t)pos;
+    }
+    __syncthreads();
+    for (int k = threadIdx.x; k < (1 << d1); k += blockDim.x)
+        counts[(uint64_t)k * tiles + blockIdx.x] = h[k];
+}
+
+// K3: (key32 << 32 | record) to its d1 bucket; ranks inside the tile from LDS
+// counters (unstable: order inside a partition does not matter)
+__global__ __launch_bounds__(kDpTileThreads) void dp_scatter_kernel(
+    const uint32_t *__restrict__ keys, const uint64_t *__restrict__ gk, uint64_t n, int d1,
+    uint64_t tiles, const uint64_t *__restrict__ off, ulonglong2 *__restrict__ ent)
+{
+    __shared__ uint32_t cur[1 << kDpMaxD1];
+    __shared__ uint64_t bas[1 << kDpMaxD1];
+    for (int k = threadIdx.x; k < (1 << d1); k += blockDim.x) {
+        cur[k] = 0;
+        bas[k] = off[(uint64_t)k * tiles + blockIdx.x];
+    }
+    __syncthreads();
+    const uint64_t t0 = (uint64_t)blockIdx.x * kDpTile;
+    for (int it = 0; it < kDpTileItems; it++) {
+        const uint64_t r = t0 + (uint64_t)it * kDpTileThreads + threadIdx.x;
+        if (r < n) {
+            const uint32_t key = keys[r];
+            const uint32_t d = key >> (32 - d1);
+            const uint32_t rank = atomicAdd(&cur[d], 1u);
+            ent[bas[d] + rank] = make_ulonglong2(((uint64_t)key << 32) | (uint32_t)r, gk[r]);
+        }
     }
 }
 
-__global__ void dedup_emit_kernel(uint64_t n, const uint32_t *__restrict__ slot_of,
-                                  const uint64_t *__restrict__ minidx,
-                                  const uint32_t *__restrict__ count, uint64_t *__restrict__ rep_out,
-                                  uint32_t *__restrict__ ref_out)
+// K4: one workgroup per d1 bucket: split by the next d2 bits into ent2 and
+// write the partition starts (pstart[nparts] = n).
+constexpr int kDpSplitThreads = 1024;
+
+__global__ __launch_bounds__(kDpSplitThreads) void dp_split_kernel(
+    const ulonglong2 *__restrict__ ent, uint64_t n, int d1, int d2, uint64_t tiles,
+    const uint64_t *__restrict__ off, ulonglong2 *__restrict__ ent2, uint32_t *__restrict__ pstart)
+{
+    __shared__ uint32_t h[1 << kDpMaxD2];
+    __shared__ uint32_t wsum[kDpSplitThreads / 64];
+    const uint32_t nd2 = 1u << d2;
+    const uint64_t s = off[(uint64_t)blockIdx.x * tiles];
+    const uint64_t e = (blockIdx.x + 1 == (1u << d1)) ? n : off[(uint64_t)(blockIdx.x + 1) * tiles];
+    const int sh = 32 - d1 - d2;
+    for (uint32_t k = threadIdx.x; k < nd2; k += blockDim.x)
+        h[k] = 0;
+    __syncthreads();
+    for (uint64_t i = s + threadIdx.x; i < e; i += blockDim.x)
+        atomicAdd(&h[(uint32_t)(ent[i].x >> (32 + sh)) & (nd2 - 1)], 1u);
+    __syncthreads();
+    // exclusive scan of h (nd2 <= 4096 = 4 per thread), in place
+    constexpr int kPer = (1 << kDpMaxD2) / kDpSplitThreads;
+    uint32_t v[kPer], sum = 0;
+#pragma unroll
+    for (int q = 0; q < kPer; q++) {
+        const uint32_t k = threadIdx.x * kPer + q;
+        v[q] = k < nd2 ? h[k] : 0u;
+        sum += v[q];
+    }
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    uint32_t x = sum;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t y = __shfl_up(x, o);
+        if (lane >= o)
+            x += y;
+    }
+    if (lane == 63)
+        wsum[wid] = x;
+    __syncthreads();
+    uint32_t pre = 0;
+    for (int k = 0; k < wid; k++)
+        pre += wsum[k];
+    uint32_t run = pre + x - sum;
+#pragma unroll
+    for (int q = 0; q < kPer; q++) {
+        const uint32_t k = threadIdx.x * kPer + q;
+        if (k < nd2) {
+            h[k] = run;
+            pstart[((uint64_t)blockIdx.x << d2) + k] = (uint32_t)(s + run);
+        }
+        run += v[q];
+    }
+    if (blockIdx.x + 1 == (1u << d1) && threadIdx.x == 0)
+        pstart[(uint64_t)1 << (d1 + d2)] = (uint32_t)n;
+    __syncthreads();
+    for (uint64_t i = s + threadIdx.x; i < e; i += blockDim.x) {
+        const ulonglong2 en = ent[i];
+        const uint32_t pos = atomicAdd(&h[(uint32_t)(en.x >> (32 + sh)) & (nd2 - 1)], 1u);
+        ent2[s + pos] = en;
+    }
+}
+
+// d2 == 0: the d1 buckets are the partitions
+__global__ void dp_starts_kernel(const uint64_t *__restrict__ off, uint64_t n, int d1,
+                                 uint64_t tiles, uint32_t *__restrict__ pstart)
+{
+    const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
+    if (k < (1u << d1))
+        pstart[k] = (uint32_t)off[(uint64_t)k * tiles];
+    if (k == 0)
+        pstart[1u << d1] = (uint32_t)n;
+}
+
+// Insert entry i (record r, key) into an open-addressing table of `size`
+// slots (power of two when MASKED, else any size): claim by CAS of
+// {key, i - base}; an equal key is confirmed on the full signature against
+// the claimer's record.  Returns the slot.
+template <bool MASKED>
+__device__ __forceinline__ uint32_t dp_insert(uint64_t *word, uint32_t size, uint32_t key,
+                                              uint32_t local, uint32_t r, const ulonglong2 *ent,
+                                              uint64_t base, const uint8_t *sig, uint32_t stride)
+{
+    uint32_t slot = MASKED ? ((key * 0x9E3779B1u) >> (32 - kDpSlotsLog))
+                           : (uint32_t)(((uint64_t)(key * 0x9E3779B1u) * size) >> 32);
+    const uint64_t mine = ((uint64_t)key << 32) | local;
+    for (;;) {
+        uint64_t cur = word[slot];
+        if (cur == kDpEmpty) {
+            cur = atomicCAS(reinterpret_cast<unsigned long long *>(&word[slot]), kDpEmpty, mine);
+            if (cur == kDpEmpty)
+                return slot;  // claimed
+        }
+        if ((uint32_t)(cur >> 32) == key) {
+            const uint32_t owner = (uint32_t)ent[base + (uint32_t)cur].x;
+            if (sig_equal(sig, stride, r, owner))
+                return slot;
+        }
+        slot = MASKED ? ((slot + 1) & (kDpSlots - 1)) : (slot + 1 == size ? 0 : slot + 1);
+    }
+}
+
+// Results go to res[record] = {rep, ref} (one 16-byte random store per
+// record); dp_emit_kernel then splits them into rep_out / ref_out in order.
+constexpr int kDpEpt = (kDpCap + kDpGroupThreads - 1) / kDpGroupThreads;  // entries per thread
+
+__global__ __launch_bounds__(kDpGroupThreads) void dp_group_kernel(
+    const ulonglong2 *__restrict__ ent, const uint32_t *__restrict__ pstart,
+    const uint8_t *__restrict__ sig, uint32_t stride, uint64_t *__restrict__ gword,
+    uint64_t *__restrict__ gmin, uint32_t *__restrict__ gcnt, uint32_t *__restrict__ gslot,
+    ulonglong2 *__restrict__ res)
+{
+    __shared__ uint64_t word[kDpSlots];
+    __shared__ uint64_t mn[kDpSlots];
+    __shared__ uint32_t cn[kDpSlots];
+    const uint32_t s = pstart[blockIdx.x], e = pstart[blockIdx.x + 1];
+    const uint32_t cnt = e - s;
+    if (cnt == 0)
+        return;
+    if (cnt <= kDpCap) {
+        // all of this thread's entries in flight at once
+        ulonglong2 en[kDpEpt];
+#pragma unroll
+        for (int k = 0; k < kDpEpt; k++) {
+            const uint32_t l = threadIdx.x + k * kDpGroupThreads;
+            en[k] = l < cnt ? ent[s + l] : make_ulonglong2(0, 0);
+        }
+        for (int k = threadIdx.x; k < kDpSlots; k += blockDim.x) {
+            word[k] = kDpEmpty;
+            mn[k] = kDpEmpty;
+            cn[k] = 0;
+        }
+        __syncthreads();
+        uint32_t slot[kDpEpt];
+#pragma unroll
+        for (int k = 0; k < kDpEpt; k++) {
+            const uint32_t l = threadIdx.x + k * kDpGroupThreads;
+            if (l < cnt) {
+                slot[k] = dp_insert<true>(word, kDpSlots, (uint32_t)(en[k].x >> 32), l,
+                                          (uint32_t)en[k].x, ent, s, sig, stride);
+                atomicMin(reinterpret_cast<unsigned long long *>(&mn[slot[k]]),
+                          (unsigned long long)en[k].y);
+                atomicAdd(&cn[slot[k]], 1u);
+            }
+        }
+        __syncthreads();
+#pragma unroll
+        for (int k = 0; k < kDpEpt; k++) {
+            const uint32_t l = threadIdx.x + k * kDpGroupThreads;
+            if (l < cnt)
+                res[(uint32_t)en[k].x] = make_ulonglong2(mn[slot[k]], cn[slot[k]]);
+        }
+        return;
+    }
+    // oversized partition: the same grouping on this partition's own HBM
+    // region (2 * cnt slots at 2 * s)
+    const uint32_t size = 2 * cnt;
+    uint64_t *w = gword + 2ull * s;
+    uint64_t *m = gmin + 2ull * s;
+    uint32_t *c = gcnt + 2ull * s;
+    for (uint32_t k = threadIdx.x; k < size; k += blockDim.x) {
+        w[k] = kDpEmpty;
+        m[k] = kDpEmpty;
+        c[k] = 0;
+    }
+    __syncthreads();
+    for (uint32_t l = threadIdx.x; l < cnt; l += blockDim.x) {
+        const ulonglong2 en = ent[s + l];
+        const uint32_t slot = dp_insert<false>(w, size, (uint32_t)(en.x >> 32), l, (uint32_t)en.x, ent,
+                                               s, sig, stride);
+        atomicMin(reinterpret_cast<unsigned long long *>(&m[slot]), (unsigned long long)en.y);
+        atomicAdd(&c[slot], 1u);
+        gslot[s + l] = slot;
+    }
+    __syncthreads();
+    for (uint32_t l = threadIdx.x; l < cnt; l += blockDim.x) {
+        const uint32_t slot = gslot[s + l];
+        res[(uint32_t)ent[s + l].x] = make_ulonglong2(m[slot], c[slot]);
+    }
+}
+
+__global__ void dp_emit_kernel(const ulonglong2 *__restrict__ res, uint64_t n,
+                               uint64_t *__restrict__ rep_out, uint32_t *__restrict__ ref_out)
 {
     for (uint64_t r = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; r < n;
          r += (uint64_t)gridDim.x * blockDim.x) {
-        const uint32_t s = slot_of[r];
-        rep_out[r] = minidx[s];
-        ref_out[r] = count[s];
+        const ulonglong2 v = res[r];
+        rep_out[r] = v.x;
+        ref_out[r] = (uint32_t)v.y;
     }
 }
 
-uint64_t dedup_table_slots(uint64_t n)
+// Workspace layout of launch_dedup_group (bytes, 256-aligned pieces).
+static inline uint64_t al(uint64_t x) { return (x + 255) & ~255ull; }
+
+uint64_t dedup_ws_bytes(uint64_t n)
 {
-    uint64_t c = 1024;
-    while (c < 2 * n)
-        c <<= 1;
-    return c;
+    const DpPlan pl = dp_plan(n);
+    const uint64_t ncnt = (1ull << pl.d1) * pl.tiles;
+    return al(4 * n) + al(8 * n) + al(8 * (ncnt + 1)) + al(8 * (ncnt + 1)) +
+           al(8 * scan_workspace_elems(ncnt)) + al(16 * n) + al(16 * n) + al(4 * (pl.nparts() + 1)) +
+           al(16 * n) + al(16 * n);
 }
 
 static unsigned grid_for(uint64_t n, unsigned block)
@@ -106,25 +362,51 @@ static unsigned grid_for(uint64_t n, unsigned block)
 }
 
 hipError_t launch_dedup_group(const uint8_t *sig, uint32_t sig_stride, const uint64_t *gidx,
-                              uint32_t gidx_stride, uint64_t n, uint32_t *slots, uint64_t *minidx,
-                              uint32_t *count, uint32_t *slot_of, uint64_t nslots,
-                              uint64_t *rep_out, uint32_t *ref_out, hipStream_t st, hipEvent_t ev0,
-                              hipEvent_t ev1)
+                              uint32_t gidx_stride, uint64_t n, void *ws, uint64_t *rep_out,
+                              uint32_t *ref_out, hipStream_t st, hipEvent_t ev0, hipEvent_t ev1)
 {
     if (n == 0)
         return hipSuccess;
+    const DpPlan pl = dp_plan(n);
+    const uint64_t ncnt = (1ull << pl.d1) * pl.tiles;
+    char *p = static_cast<char *>(ws);
+    auto take = [&](uint64_t bytes) {
+        char *q = p;
+        p += al(bytes);
+        return q;
+    };
+    uint32_t *keys = reinterpret_cast<uint32_t *>(take(4 * n));
+    uint64_t *gk = reinterpret_cast<uint64_t *>(take(8 * n));
+    uint64_t *counts = reinterpret_cast<uint64_t *>(take(8 * (ncnt + 1)));
+    uint64_t *off = reinterpret_cast<uint64_t *>(take(8 * (ncnt + 1)));
+    uint64_t *bsum = reinterpret_cast<uint64_t *>(take(8 * scan_workspace_elems(ncnt)));
+    ulonglong2 *ent = reinterpret_cast<ulonglong2 *>(take(16 * n));
+    ulonglong2 *ent2 = reinterpret_cast<ulonglong2 *>(take(16 * n));
+    uint32_t *pstart = reinterpret_cast<uint32_t *>(take(4 * (pl.nparts() + 1)));
+    uint64_t *gword = reinterpret_cast<uint64_t *>(take(16 * n));  // oversized-partition tables
+    uint64_t *gmin = reinterpret_cast<uint64_t *>(take(16 * n));
+    uint32_t *gcnt = reinterpret_cast<uint32_t *>(gk);  // keys / gk are dead after K3
+    uint32_t *gslot = keys;
+    ulonglong2 *res = pl.d2 ? ent : ent2;  // whichever entry array K5 does not read
     hipError_t e;
-    if ((e = hipMemsetAsync(slots, 0xFF, nslots * sizeof(uint32_t), st)) != hipSuccess)
-        return e;
-    if ((e = hipMemsetAsync(minidx, 0xFF, nslots * sizeof(uint64_t), st)) != hipSuccess)
-        return e;
-    if ((e = hipMemsetAsync(count, 0, nslots * sizeof(uint32_t), st)) != hipSuccess)
-        return e;
     if (ev0)
         (void)hipEventRecord(ev0, st);
-    dedup_insert_kernel<<<grid_for(n, 256), 256, 0, st>>>(sig, sig_stride, gidx, gidx_stride, n,
-                                                          slots, minidx, count, slot_of, nslots - 1);
-    dedup_emit_kernel<<<grid_for(n, 256), 256, 0, st>>>(n, slot_of, minidx, count, rep_out, ref_out);
+    dp_keys_kernel<<<(unsigned)pl.tiles, kDpTileThreads, 0, st>>>(sig, sig_stride, gidx, gidx_stride, n,
+                                                                  pl.d1, pl.tiles, keys, gk, counts);
+    if ((e = launch_exclusive_scan(counts, ncnt, off, bsum, st)) != hipSuccess)
+        return e;
+    dp_scatter_kernel<<<(unsigned)pl.tiles, kDpTileThreads, 0, st>>>(keys, gk, n, pl.d1, pl.tiles, off, ent);
+    const ulonglong2 *parts = ent;
+    if (pl.d2) {
+        dp_split_kernel<<<1u << pl.d1, kDpSplitThreads, 0, st>>>(ent, n, pl.d1, pl.d2, pl.tiles, off,
+                                                                  ent2, pstart);
+        parts = ent2;
+    } else {
+        dp_starts_kernel<<<((1u << pl.d1) + 255) / 256, 256, 0, st>>>(off, n, pl.d1, pl.tiles, pstart);
+    }
+    dp_group_kernel<<<(unsigned)pl.nparts(), kDpGroupThreads, 0, st>>>(
+        parts, pstart, sig, sig_stride, gword, gmin, gcnt, gslot, res);
+    dp_emit_kernel<<<grid_for(n, 256), 256, 0, st>>>(res, n, rep_out, ref_out);
     if (ev1)
         (void)hipEventRecord(ev1, st);
     return hipGetLastError();

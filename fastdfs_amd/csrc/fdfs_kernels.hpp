@@ -56,12 +56,10 @@ hipError_t launch_scrub(const uint32_t *crc, const uint32_t *expect, uint32_t n,
                         uint32_t *nbad, hipStream_t st);
 
 // dedup path (fdfs_dedup.hip)
-uint64_t dedup_table_slots(uint64_t n);
+uint64_t dedup_ws_bytes(uint64_t n);
 hipError_t launch_dedup_group(const uint8_t *sig, uint32_t sig_stride, const uint64_t *gidx,
-                              uint32_t gidx_stride, uint64_t n, uint32_t *slots, uint64_t *minidx,
-                              uint32_t *count, uint32_t *slot_of, uint64_t nslots,
-                              uint64_t *rep_out, uint32_t *ref_out, hipStream_t st, hipEvent_t ev0,
-                              hipEvent_t ev1);
+                              uint32_t gidx_stride, uint64_t n, void *ws, uint64_t *rep_out,
+                              uint32_t *ref_out, hipStream_t st, hipEvent_t ev0, hipEvent_t ev1);
 hipError_t launch_dedup_bucket(const uint8_t *sig, const uint64_t *gidx, uint64_t n,
                                uint32_t nranks, uint8_t *records_out, uint64_t *counts_out,
                                uint64_t *cursor, uint64_t *row_of_out, hipStream_t st,

@@ -36,7 +36,7 @@ def test_library_exports_every_declared_symbol():
 def test_gfx950_code_object_embedded():
     data = open(_lib.LIB_PATH, "rb").read()
     assert b"amdgcn-amd-amdhsa--gfx950" in data
-    for k in (b"sig_hash_kernel", b"md5_stage_kernel", b"crc_seg_kernel", b"dedup_insert_kernel"):
+    for k in (b"sig_hash_kernel", b"md5_stage_kernel", b"crc_seg_kernel", b"dp_group_kernel"):
         assert k in data, k
 
 

@@ -99,3 +99,59 @@ def test_c5_one_gpu_share(oracle, ctx):
     orep, oref = oracle.dedup(sig.numpy())
     assert np.array_equal(rep.cpu().numpy(), orep.astype(np.int64))
     assert np.array_equal(ref.cpu().numpy(), oref.astype(np.int32))
+
+
+# ---- crafted hash collisions: distinct signatures with one 64-bit key ----
+
+M64 = (1 << 64) - 1
+
+
+def _fmix64(k):
+    k ^= k >> 33
+    k = (k * 0xff51afd7ed558ccd) & M64
+    k ^= k >> 33
+    k = (k * 0xc4ceb9fe1a85ec53) & M64
+    k ^= k >> 33
+    return k
+
+
+def _colliding(count, seed):
+    """`count` distinct signatures with identical 64-bit grouping hash
+    (fmix64(a ^ fmix64(b ^ fmix64(c + K)))): pick b freely, solve for a."""
+    rng = np.random.default_rng(seed)
+    c = int(rng.integers(0, 1 << 62))
+    inner = _fmix64((c + 0x9E3779B97F4A7C15) & M64)
+    a0, b0 = int(rng.integers(0, 1 << 62)), int(rng.integers(0, 1 << 62))
+    target = a0 ^ _fmix64(b0 ^ inner)
+    out = np.zeros((count, 24), np.uint8)
+    for i in range(count):
+        b = (b0 + i * 0x1234567) & M64
+        a = target ^ _fmix64(b ^ inner)
+        out[i] = np.frombuffer(a.to_bytes(8, "little") + b.to_bytes(8, "little")
+                               + c.to_bytes(8, "little"), np.uint8)
+    return out
+
+
+@pytest.mark.parametrize("ncoll,reps", [(40, 3), (700, 2), (2500, 1)])
+def test_dedup_full_hash_collisions(oracle, ctx, ncoll, reps):
+    """Distinct signatures sharing the whole 64-bit key (one partition, one
+    probe chain) stay distinct classes; with 2500 of them the partition is
+    over the LDS capacity and takes the HBM-table path."""
+    coll = _colliding(ncoll, ncoll)
+    bg = _sigs(30_000, 20_000, 77)
+    sig = np.concatenate([np.tile(coll, (reps, 1)), bg])
+    sig = sig[np.random.default_rng(ncoll).permutation(len(sig))]
+    rep, ref = ctx.dedup(torch.from_numpy(np.ascontiguousarray(sig)).cuda())
+    orep, oref = oracle.dedup(sig)
+    assert np.array_equal(rep.cpu().numpy(), orep.astype(np.int64))
+    assert np.array_equal(ref.cpu().numpy(), oref.astype(np.int32))
+
+
+@pytest.mark.parametrize("n", [2, 1023, 1025, 3000, 2_100_000])
+def test_dedup_partition_plans(oracle, ctx, n):
+    """Sizes around the partition-plan steps (one, two and three levels)."""
+    sig = _sigs(n, max(1, n * 9 // 10), n + 3)
+    rep, ref = ctx.dedup(torch.from_numpy(sig).cuda())
+    orep, oref = oracle.dedup(sig)
+    assert np.array_equal(rep.cpu().numpy(), orep.astype(np.int64))
+    assert np.array_equal(ref.cpu().numpy(), oref.astype(np.int32))
