@@ -97,11 +97,12 @@ DpPlan dp_plan(uint64_t n)
     return pl;
 }
 
-// K1: key32 per record + the tile's histogram of the top d1 bits
+// K1: key32 per record + the tile's histogram of the top d1 bits; the
+// singleton answer (rep = own gidx, ref = 1) for every record
 __global__ __launch_bounds__(kDpTileThreads) void dp_keys_kernel(
     const uint8_t *__restrict__ sig, uint32_t stride, const uint64_t *__restrict__ gidx,
     uint32_t gstride, uint64_t n, int d1, uint64_t tiles, uint32_t *__restrict__ keys,
-    uint64_t *__restrict__ gk, uint64_t *__restrict__ counts)
+    uint64_t *__restrict__ rep_out, uint32_t *__restrict__ ref_out, uint64_t *__restrict__ counts)
 {
     __shared__ uint32_t h[1 << kDpMaxD1];
     for (int k = threadIdx.x; k < (1 << d1); k += blockDim.x)
@@ -115,7 +116,10 @@ __global__ __launch_bounds__(kDpTileThreads) void dp_keys_kernel(
             load_sig(sig + r * stride, a, b, c);
             const uint32_t key = (uint32_t)sig_hash(a, b, c);
             keys[r] = key;
-            gk[r] = gstride ? gidx[r * gstride] : r;
+            // every record starts as its own class; dp_group overwrites the
+            // records of classes with more than one member
+            rep_out[r] = gstride ? gidx[r * gstride] : r;
+            ref_out[r] = 1;
             atomicAdd(&h[key >> (32 - d1)], 1u);
         }
     }
@@ -251,15 +255,15 @@ __device__ __forceinline__ uint32_t dp_insert(uint64_t *word, uint32_t size, uin
     }
 }
 
-// Results go to res[record] = {rep, ref} (one 16-byte random store per
-// record); dp_emit_kernel then splits them into rep_out / ref_out in order.
+// Only records of classes with more than one member are written (random
+// stores); K1 already wrote every record's singleton answer.
 constexpr int kDpEpt = (kDpCap + kDpGroupThreads - 1) / kDpGroupThreads;  // entries per thread
 
 __global__ __launch_bounds__(kDpGroupThreads) void dp_group_kernel(
     const ulonglong2 *__restrict__ ent, const uint32_t *__restrict__ pstart,
     const uint8_t *__restrict__ sig, uint32_t stride, uint64_t *__restrict__ gword,
     uint64_t *__restrict__ gmin, uint32_t *__restrict__ gcnt, uint32_t *__restrict__ gslot,
-    ulonglong2 *__restrict__ res)
+    uint64_t *__restrict__ rep_out, uint32_t *__restrict__ ref_out)
 {
     __shared__ uint64_t word[kDpSlots];
     __shared__ uint64_t mn[kDpSlots];
@@ -298,8 +302,14 @@ __global__ __launch_bounds__(kDpGroupThreads) void dp_group_kernel(
 #pragma unroll
         for (int k = 0; k < kDpEpt; k++) {
             const uint32_t l = threadIdx.x + k * kDpGroupThreads;
-            if (l < cnt)
-                res[(uint32_t)en[k].x] = make_ulonglong2(mn[slot[k]], cn[slot[k]]);
+            if (l < cnt) {
+                const uint32_t c = cn[slot[k]];
+                if (c > 1) {
+                    const uint32_t r = (uint32_t)en[k].x;
+                    rep_out[r] = mn[slot[k]];
+                    ref_out[r] = c;
+                }
+            }
         }
         return;
     }
@@ -326,18 +336,11 @@ __global__ __launch_bounds__(kDpGroupThreads) void dp_group_kernel(
     __syncthreads();
     for (uint32_t l = threadIdx.x; l < cnt; l += blockDim.x) {
         const uint32_t slot = gslot[s + l];
-        res[(uint32_t)ent[s + l].x] = make_ulonglong2(m[slot], c[slot]);
-    }
-}
-
-__global__ void dp_emit_kernel(const ulonglong2 *__restrict__ res, uint64_t n,
-                               uint64_t *__restrict__ rep_out, uint32_t *__restrict__ ref_out)
-{
-    for (uint64_t r = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; r < n;
-         r += (uint64_t)gridDim.x * blockDim.x) {
-        const ulonglong2 v = res[r];
-        rep_out[r] = v.x;
-        ref_out[r] = (uint32_t)v.y;
+        if (c[slot] > 1) {
+            const uint32_t r = (uint32_t)ent[s + l].x;
+            rep_out[r] = m[slot];
+            ref_out[r] = c[slot];
+        }
     }
 }
 
@@ -376,7 +379,6 @@ hipError_t launch_dedup_group(const uint8_t *sig, uint32_t sig_stride, const uin
         return q;
     };
     uint32_t *keys = reinterpret_cast<uint32_t *>(take(4 * n));
-    uint64_t *gk = reinterpret_cast<uint64_t *>(take(8 * n));
     uint64_t *counts = reinterpret_cast<uint64_t *>(take(8 * (ncnt + 1)));
     uint64_t *off = reinterpret_cast<uint64_t *>(take(8 * (ncnt + 1)));
     uint64_t *bsum = reinterpret_cast<uint64_t *>(take(8 * scan_workspace_elems(ncnt)));
@@ -385,17 +387,18 @@ hipError_t launch_dedup_group(const uint8_t *sig, uint32_t sig_stride, const uin
     uint32_t *pstart = reinterpret_cast<uint32_t *>(take(4 * (pl.nparts() + 1)));
     uint64_t *gword = reinterpret_cast<uint64_t *>(take(16 * n));  // oversized-partition tables
     uint64_t *gmin = reinterpret_cast<uint64_t *>(take(16 * n));
-    uint32_t *gcnt = reinterpret_cast<uint32_t *>(gk);  // keys / gk are dead after K3
-    uint32_t *gslot = keys;
-    ulonglong2 *res = pl.d2 ? ent : ent2;  // whichever entry array K5 does not read
+    uint32_t *gcnt = reinterpret_cast<uint32_t *>(take(8 * n));
+    uint32_t *gslot = keys;  // keys are dead after K3
     hipError_t e;
     if (ev0)
         (void)hipEventRecord(ev0, st);
     dp_keys_kernel<<<(unsigned)pl.tiles, kDpTileThreads, 0, st>>>(sig, sig_stride, gidx, gidx_stride, n,
-                                                                  pl.d1, pl.tiles, keys, gk, counts);
+                                                                  pl.d1, pl.tiles, keys, rep_out, ref_out,
+                                                                  counts);
     if ((e = launch_exclusive_scan(counts, ncnt, off, bsum, st)) != hipSuccess)
         return e;
-    dp_scatter_kernel<<<(unsigned)pl.tiles, kDpTileThreads, 0, st>>>(keys, gk, n, pl.d1, pl.tiles, off, ent);
+    dp_scatter_kernel<<<(unsigned)pl.tiles, kDpTileThreads, 0, st>>>(keys, rep_out, n, pl.d1, pl.tiles, off,
+                                                                     ent);
     const ulonglong2 *parts = ent;
     if (pl.d2) {
         dp_split_kernel<<<1u << pl.d1, kDpSplitThreads, 0, st>>>(ent, n, pl.d1, pl.d2, pl.tiles, off,
@@ -405,8 +408,7 @@ hipError_t launch_dedup_group(const uint8_t *sig, uint32_t sig_stride, const uin
         dp_starts_kernel<<<((1u << pl.d1) + 255) / 256, 256, 0, st>>>(off, n, pl.d1, pl.tiles, pstart);
     }
     dp_group_kernel<<<(unsigned)pl.nparts(), kDpGroupThreads, 0, st>>>(
-        parts, pstart, sig, sig_stride, gword, gmin, gcnt, gslot, res);
-    dp_emit_kernel<<<grid_for(n, 256), 256, 0, st>>>(res, n, rep_out, ref_out);
+        parts, pstart, sig, sig_stride, gword, gmin, gcnt, gslot, rep_out, ref_out);
     if (ev1)
         (void)hipEventRecord(ev1, st);
     return hipGetLastError();
