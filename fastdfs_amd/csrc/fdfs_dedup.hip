@@ -128,58 +128,17 @@ __global__ __launch_bounds__(kDpTileThreads) void dp_keys_kernel(
         counts[(uint64_t)k * tiles + blockIdx.x] = h[k];
 }
 
-// K3: (key32 << 32 | record) to its d1 bucket; ranks inside the tile from LDS
-// counters (unstable: order inside a partition does not matter)
-__global__ __launch_bounds__(kDpTileThreads) void dp_scatter_kernel(
-    const uint32_t *__restrict__ keys, const uint64_t *__restrict__ gk, uint64_t n, int d1,
-    uint64_t tiles, const uint64_t *__restrict__ off, ulonglong2 *__restrict__ ent)
+// Exclusive scan of cnt[0, nb) into out[] by the whole block (each thread
+// owns PER consecutive bins; nb <= PER * blockDim.x).
+template <int PER, int NT>
+__device__ __forceinline__ void block_scan_bins(const uint32_t *cnt, uint32_t *out, uint32_t nb,
+                                                uint32_t *wsum)
 {
-    __shared__ uint32_t cur[1 << kDpMaxD1];
-    __shared__ uint64_t bas[1 << kDpMaxD1];
-    for (int k = threadIdx.x; k < (1 << d1); k += blockDim.x) {
-        cur[k] = 0;
-        bas[k] = off[(uint64_t)k * tiles + blockIdx.x];
-    }
-    __syncthreads();
-    const uint64_t t0 = (uint64_t)blockIdx.x * kDpTile;
-    for (int it = 0; it < kDpTileItems; it++) {
-        const uint64_t r = t0 + (uint64_t)it * kDpTileThreads + threadIdx.x;
-        if (r < n) {
-            const uint32_t key = keys[r];
-            const uint32_t d = key >> (32 - d1);
-            const uint32_t rank = atomicAdd(&cur[d], 1u);
-            ent[bas[d] + rank] = make_ulonglong2(((uint64_t)key << 32) | (uint32_t)r, gk[r]);
-        }
-    }
-}
-
-// K4: one workgroup per d1 bucket: split by the next d2 bits into ent2 and
-// write the partition starts (pstart[nparts] = n).
-constexpr int kDpSplitThreads = 1024;
-
-__global__ __launch_bounds__(kDpSplitThreads) void dp_split_kernel(
-    const ulonglong2 *__restrict__ ent, uint64_t n, int d1, int d2, uint64_t tiles,
-    const uint64_t *__restrict__ off, ulonglong2 *__restrict__ ent2, uint32_t *__restrict__ pstart)
-{
-    __shared__ uint32_t h[1 << kDpMaxD2];
-    __shared__ uint32_t wsum[kDpSplitThreads / 64];
-    const uint32_t nd2 = 1u << d2;
-    const uint64_t s = off[(uint64_t)blockIdx.x * tiles];
-    const uint64_t e = (blockIdx.x + 1 == (1u << d1)) ? n : off[(uint64_t)(blockIdx.x + 1) * tiles];
-    const int sh = 32 - d1 - d2;
-    for (uint32_t k = threadIdx.x; k < nd2; k += blockDim.x)
-        h[k] = 0;
-    __syncthreads();
-    for (uint64_t i = s + threadIdx.x; i < e; i += blockDim.x)
-        atomicAdd(&h[(uint32_t)(ent[i].x >> (32 + sh)) & (nd2 - 1)], 1u);
-    __syncthreads();
-    // exclusive scan of h (nd2 <= 4096 = 4 per thread), in place
-    constexpr int kPer = (1 << kDpMaxD2) / kDpSplitThreads;
-    uint32_t v[kPer], sum = 0;
+    uint32_t v[PER], sum = 0;
 #pragma unroll
-    for (int q = 0; q < kPer; q++) {
-        const uint32_t k = threadIdx.x * kPer + q;
-        v[q] = k < nd2 ? h[k] : 0u;
+    for (int q = 0; q < PER; q++) {
+        const uint32_t k = threadIdx.x * PER + q;
+        v[q] = k < nb ? cnt[k] : 0u;
         sum += v[q];
     }
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
@@ -193,26 +152,132 @@ __global__ __launch_bounds__(kDpSplitThreads) void dp_split_kernel(
     if (lane == 63)
         wsum[wid] = x;
     __syncthreads();
-    uint32_t pre = 0;
+    uint32_t run = x - sum;
     for (int k = 0; k < wid; k++)
-        pre += wsum[k];
-    uint32_t run = pre + x - sum;
+        run += wsum[k];
 #pragma unroll
-    for (int q = 0; q < kPer; q++) {
-        const uint32_t k = threadIdx.x * kPer + q;
-        if (k < nd2) {
-            h[k] = run;
-            pstart[((uint64_t)blockIdx.x << d2) + k] = (uint32_t)(s + run);
-        }
+    for (int q = 0; q < PER; q++) {
+        const uint32_t k = threadIdx.x * PER + q;
+        if (k < nb)
+            out[k] = run;
         run += v[q];
     }
+    __syncthreads();
+}
+
+// K3: {key32 << 32 | record, gidx} to its d1 bucket.  The tile is ranked by
+// LDS counters (unstable: order inside a partition does not matter), sorted
+// by digit in LDS and written out as contiguous runs (one run per digit).
+__global__ __launch_bounds__(kDpTileThreads) void dp_scatter_kernel(
+    const uint32_t *__restrict__ keys, const uint64_t *__restrict__ gk, uint64_t n, int d1,
+    uint64_t tiles, const uint64_t *__restrict__ off, ulonglong2 *__restrict__ ent)
+{
+    __shared__ uint32_t cnt[1 << kDpMaxD1];
+    __shared__ uint32_t lst[1 << kDpMaxD1];
+    __shared__ uint64_t bas[1 << kDpMaxD1];
+    __shared__ uint32_t wsum[kDpTileThreads / 64];
+    __shared__ ulonglong2 stage[kDpTile];
+    const uint32_t nb = 1u << d1;
+    for (uint32_t k = threadIdx.x; k < nb; k += blockDim.x) {
+        cnt[k] = 0;
+        bas[k] = off[(uint64_t)k * tiles + blockIdx.x];
+    }
+    __syncthreads();
+    const uint64_t t0 = (uint64_t)blockIdx.x * kDpTile;
+    const uint32_t m = (uint32_t)((n - t0) < (uint64_t)kDpTile ? (n - t0) : (uint64_t)kDpTile);
+    uint32_t key[kDpTileItems], rank[kDpTileItems];
+#pragma unroll
+    for (int it = 0; it < kDpTileItems; it++) {
+        const uint32_t l = it * kDpTileThreads + threadIdx.x;
+        if (l < m) {
+            key[it] = keys[t0 + l];
+            rank[it] = atomicAdd(&cnt[key[it] >> (32 - d1)], 1u);
+        }
+    }
+    __syncthreads();
+    block_scan_bins<1, kDpTileThreads>(cnt, lst, nb, wsum);
+#pragma unroll
+    for (int it = 0; it < kDpTileItems; it++) {
+        const uint32_t l = it * kDpTileThreads + threadIdx.x;
+        if (l < m)
+            stage[lst[key[it] >> (32 - d1)] + rank[it]] =
+                make_ulonglong2(((uint64_t)key[it] << 32) | (uint32_t)(t0 + l), gk[t0 + l]);
+    }
+    __syncthreads();
+    for (uint32_t j = threadIdx.x; j < m; j += blockDim.x) {
+        const ulonglong2 en = stage[j];
+        const uint32_t d = (uint32_t)(en.x >> (64 - d1));
+        ent[bas[d] + (j - lst[d])] = en;
+    }
+}
+
+// K4: one workgroup per d1 bucket: split by the next d2 bits into ent2 and
+// write the partition starts (pstart[nparts] = n).  A first pass counts the
+// whole bucket; the second goes chunk by chunk (rank, LDS sort by digit,
+// contiguous runs out, per-digit cursors advanced by the chunk's counts).
+constexpr int kDpSplitThreads = 1024;
+constexpr int kDpSplitPer = 4;  // entries per thread per chunk
+constexpr int kDpChunk = kDpSplitThreads * kDpSplitPer;
+
+__global__ __launch_bounds__(kDpSplitThreads) void dp_split_kernel(
+    const ulonglong2 *__restrict__ ent, uint64_t n, int d1, int d2, uint64_t tiles,
+    const uint64_t *__restrict__ off, ulonglong2 *__restrict__ ent2, uint32_t *__restrict__ pstart)
+{
+    constexpr int NB = 1 << kDpMaxD2;
+    constexpr int PER = NB / kDpSplitThreads;
+    __shared__ uint32_t h[NB];    // bucket counts, then the running cursor (relative to s)
+    __shared__ uint32_t cc[NB];   // chunk counts
+    __shared__ uint32_t cl[NB];   // chunk-local starts
+    __shared__ uint32_t wsum[kDpSplitThreads / 64];
+    __shared__ ulonglong2 stage[kDpChunk];
+    const uint32_t nd2 = 1u << d2;
+    const uint64_t s = off[(uint64_t)blockIdx.x * tiles];
+    const uint64_t e = (blockIdx.x + 1 == (1u << d1)) ? n : off[(uint64_t)(blockIdx.x + 1) * tiles];
+    const int sh = 64 - d1 - d2;  // d2 digit = (entry.x >> sh) & (nd2 - 1)
+    for (uint32_t k = threadIdx.x; k < nd2; k += blockDim.x)
+        h[k] = 0;
+    __syncthreads();
+    for (uint64_t i = s + threadIdx.x; i < e; i += blockDim.x)
+        atomicAdd(&h[(uint32_t)(ent[i].x >> sh) & (nd2 - 1)], 1u);
+    __syncthreads();
+    block_scan_bins<PER, kDpSplitThreads>(h, h, nd2, wsum);
+    for (uint32_t k = threadIdx.x; k < nd2; k += blockDim.x)
+        pstart[((uint64_t)blockIdx.x << d2) + k] = (uint32_t)(s + h[k]);
     if (blockIdx.x + 1 == (1u << d1) && threadIdx.x == 0)
         pstart[(uint64_t)1 << (d1 + d2)] = (uint32_t)n;
-    __syncthreads();
-    for (uint64_t i = s + threadIdx.x; i < e; i += blockDim.x) {
-        const ulonglong2 en = ent[i];
-        const uint32_t pos = atomicAdd(&h[(uint32_t)(en.x >> (32 + sh)) & (nd2 - 1)], 1u);
-        ent2[s + pos] = en;
+    for (uint64_t c0 = s; c0 < e; c0 += kDpChunk) {
+        const uint32_t m = (uint32_t)((e - c0) < (uint64_t)kDpChunk ? (e - c0) : (uint64_t)kDpChunk);
+        for (uint32_t k = threadIdx.x; k < nd2; k += blockDim.x)
+            cc[k] = 0;
+        __syncthreads();
+        ulonglong2 en[kDpSplitPer];
+        uint32_t rk[kDpSplitPer];
+#pragma unroll
+        for (int q = 0; q < kDpSplitPer; q++) {
+            const uint32_t l = q * kDpSplitThreads + threadIdx.x;
+            if (l < m) {
+                en[q] = ent[c0 + l];
+                rk[q] = atomicAdd(&cc[(uint32_t)(en[q].x >> sh) & (nd2 - 1)], 1u);
+            }
+        }
+        __syncthreads();
+        block_scan_bins<PER, kDpSplitThreads>(cc, cl, nd2, wsum);
+#pragma unroll
+        for (int q = 0; q < kDpSplitPer; q++) {
+            const uint32_t l = q * kDpSplitThreads + threadIdx.x;
+            if (l < m)
+                stage[cl[(uint32_t)(en[q].x >> sh) & (nd2 - 1)] + rk[q]] = en[q];
+        }
+        __syncthreads();
+        for (uint32_t j = threadIdx.x; j < m; j += blockDim.x) {
+            const ulonglong2 v = stage[j];
+            const uint32_t d = (uint32_t)(v.x >> sh) & (nd2 - 1);
+            ent2[s + h[d] + (j - cl[d])] = v;
+        }
+        __syncthreads();
+        for (uint32_t k = threadIdx.x; k < nd2; k += blockDim.x)
+            h[k] += cc[k];
+        __syncthreads();
     }
 }
 
