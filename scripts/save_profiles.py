@@ -14,7 +14,7 @@ sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
 from pmc_summary import load  # noqa: E402
 
 BENCH_KERNEL = {"c2": ("sig_hash_kernel<true, 0, 0>", "sig_hash_kernel<SAR>"),
-                "c3": ("md5_stage_kernel<256>", "md5_stage_kernel<256>"),
+                "c3": ("md5_stage_kernel<true>", "md5_stage_kernel<SAR>"),
                 "c4": ("crc_seg_kernel<true, 2>", "crc_seg_kernel<SAR,2>")}
 
 
@@ -30,7 +30,7 @@ def main(src, dst):
             line = open(log).read().strip().split("\n")[-1]
             json.loads(line)
             open(os.path.join(dst, f"bench_{c}.json"), "w").write(line + "\n")
-    for c in ("c2", "c3", "c4"):
+    for c in ("c2", "c3", "c4", "c5"):
         for f in glob.glob(os.path.join(src, f"stats_{c}", "**", "*kernel_stats.csv"), recursive=True):
             rows = list(csv.DictReader(open(f)))
             with open(os.path.join(dst, f"kernel_stats_{c}.csv"), "w", newline="") as out:
@@ -40,6 +40,8 @@ def main(src, dst):
                     if "fdfs::" in r["Name"] or "rocclr" in r["Name"]:
                         r["Name"] = short(r["Name"])
                         w.writerow(r)
+        if c not in BENCH_KERNEL:
+            continue
         pm = {}
         for kind in ("fetch", "write"):
             d = load(os.path.join(src, f"{kind}_{c}"))
