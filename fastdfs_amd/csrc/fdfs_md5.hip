@@ -7,6 +7,12 @@
 #include "fdfs_device.hpp"
 #include "fdfs_kernels.hpp"
 
+#include <cstdlib>
+
+#ifndef MD5_CHAIN_ASM
+#define MD5_CHAIN_ASM 1
+#endif
+
 namespace fdfs {
 
 // ----------------------------------------------------------------- MD5 core
@@ -20,7 +26,21 @@ __device__ __forceinline__ uint32_t rotl(uint32_t x, int s)
 #define MD5_G(b, c, d) ((c) ^ ((d) & ((b) ^ (c))))
 #define MD5_H(b, c, d) ((b) ^ (c) ^ (d))
 #define MD5_I(b, c, d) ((c) ^ ((b) | ~(d)))
-#define MD5_STEP(FN, a, b, c, d, m, k, s) a = (b) + rotl((a) + FN(b, c, d) + (m) + (k), s)
+// The step's critical path is F -> add -> rotate -> add.  a, m and k are
+// known steps ahead, so (a + m + k) is summed off the path and the on-path
+// add is kept a single full-rate v_add_u32 (hipcc would otherwise fold it
+// into a v_add3_u32, a half-rate instruction on the chain).
+__device__ __forceinline__ uint32_t add_chain(uint32_t x, uint32_t y)
+{
+#if MD5_CHAIN_ASM
+    uint32_t r;
+    asm("v_add_u32_e32 %0, %1, %2" : "=v"(r) : "v"(x), "v"(y));
+    return r;
+#else
+    return x + y;
+#endif
+}
+#define MD5_STEP(FN, a, b, c, d, m, k, s) a = (b) + rotl(add_chain((a) + (m) + (k), FN(b, c, d)), s)
 
 __device__ __forceinline__ void md5_compress(uint32_t st[4], const uint32_t m[16])
 {
@@ -338,15 +358,21 @@ hipError_t launch_md5_stage(bool sar, const uint8_t *base, const uint64_t *offs,
     if (ncu[dev] == 0 &&
         (e = hipDeviceGetAttribute(&ncu[dev], hipDeviceAttributeMultiprocessorCount, dev)) != hipSuccess)
         return e;
+    static int onewg = -1;
+    if (onewg < 0) {  // A/B: FDFS_GPU_MD5_ONEWG=1 -> one workgroup per CU, plain largest-first
+        const char *ev = getenv("FDFS_GPU_MD5_ONEWG");
+        onewg = ev ? atoi(ev) : 0;
+    }
     constexpr unsigned kBlk = 64 * kMd5Waves;
     const unsigned grid = (n + kBlk - 1) / kBlk;
-    const uint32_t w1 = (uint32_t)ncu[dev] * kMd5Waves;
+    const uint32_t w1 = onewg ? 0xFFFFFFFFu : (uint32_t)ncu[dev] * kMd5Waves;
+    const size_t dyn = onewg ? 64 * 1024 : 0;  // LDS the kernel does not touch: 1 workgroup per CU
     if (sar)
-        md5_stage_kernel<true><<<grid, kBlk, 0, st>>>(base, offs, sizes, order, n, tabs, w1, crc_out,
-                                                      sig_out, codes_out);
+        md5_stage_kernel<true><<<grid, kBlk, dyn, st>>>(base, offs, sizes, order, n, tabs, w1, crc_out,
+                                                        sig_out, codes_out);
     else
-        md5_stage_kernel<false><<<grid, kBlk, 0, st>>>(base, offs, sizes, order, n, tabs, w1, crc_out,
-                                                       sig_out, codes_out);
+        md5_stage_kernel<false><<<grid, kBlk, dyn, st>>>(base, offs, sizes, order, n, tabs, w1, crc_out,
+                                                         sig_out, codes_out);
     return hipGetLastError();
 }
 
