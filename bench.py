@@ -142,6 +142,26 @@ def cpu_baseline(data, offs_np, sizes_np, method, variant, seconds, threads):
                       f"{dt:.1f} s", "cpu_model": cpu_model()}
 
 
+def cpu_dedup_baseline(sig: torch.Tensor, seconds: float):
+    """The oracle's grouping (sort by signature + run detection, the CPU
+    form of the FastDHT semantics) on one host core, over prefixes of the
+    bench's signatures that double until ~`seconds` of CPU work."""
+    from oracle import oracle as O
+    n, spent, m = 1 << 20, 0.0, 0
+    while True:
+        m = min(n, sig.shape[0])
+        host = sig[:m].cpu().numpy()
+        t0 = time.perf_counter()
+        O.dedup(host)
+        spent = time.perf_counter() - t0
+        if spent * 2.5 > seconds or m == sig.shape[0]:
+            break
+        n *= 2
+    return {"value": round(m / spent, 1), "unit": "files/s", "cores": 1, "kind": "port",
+            "sample": f"first {m} of the bench's signatures, oracle/fdfs_oracle.c orc_dedup "
+                      f"({cpu_model()})"}
+
+
 def cpu_model() -> str:
     try:
         for line in open("/proc/cpuinfo"):
@@ -163,6 +183,29 @@ def load_traffic(config: str, kernel: str):
     except (OSError, ValueError):
         pass
     return None, None
+
+
+SQ_KERNEL = {"c2": "sig_hash_kernel<true, 0, 0>", "c3": "md5_stage_kernel<true>"}
+
+
+def load_valu(config: str, avg_ms: float):
+    """VALU issue of the dominant kernel: SQ_INSTS_VALU per launch from the
+    committed rocprofv3 --pmc pass (profiles/r01/pmc_sq_<config>.txt; the
+    count does not depend on timing) over the live kernel time, in int32
+    lane-ops/s against VALU_PEAK_TOPS."""
+    path = os.path.join(ROOT, "profiles", "r01", f"pmc_sq_{config}.txt")
+    try:
+        for line in open(path):
+            name, _, js = line.partition(" {")
+            if name.strip() == SQ_KERNEL.get(config):
+                insts = json.loads("{" + js)["SQ_INSTS_VALU"]
+                tops = insts * 64 / (avg_ms * 1e-3) / 1e12
+                return {"insts_per_launch": round(insts), "achieved_tops": round(tops, 2),
+                        "peak_tops": VALU_PEAK_TOPS, "frac": round(tops / VALU_PEAK_TOPS, 4),
+                        "source": os.path.relpath(path, ROOT)}
+    except (OSError, ValueError, KeyError):
+        pass
+    return None
 
 
 def main():
@@ -225,6 +268,9 @@ def main():
                            "algorithmic_bytes_per_launch": nbytes}
         if tsrc:
             res["roofline"]["traffic_source"] = tsrc
+        valu = load_valu(args.config, avg_ms)
+        if valu:
+            res["valu"] = valu
         if method != F.SIG_CRC_ONLY:
             # dedup-only throughput of the same signatures (files/s, all ranks)
             _, sig, _ = ctx.sig_batch(data, offs_t, sizes_t, method=method)
@@ -282,7 +328,10 @@ def main():
                            "traffic": None,
                            "kernel": "dedup_group (dp_keys + scan + dp_scatter + dp_split + dp_group)",
                            "kernel_ms_avg": round(avg_ms, 4), "algorithmic_bytes_per_launch": nb}
-        res["cpu_baseline"] = None
+        if rank == 0 and world == 1 and not args.no_cpu_baseline:
+            res["cpu_baseline"] = cpu_dedup_baseline(sig, args.cpu_seconds)
+        else:
+            res["cpu_baseline"] = None
     if rank == 0:
         print(json.dumps(res), flush=True)
     ctx.close()

@@ -62,11 +62,14 @@ def main(src, dst):
                                  "HBM section), write = WRITE_SIZE x 1024",
                        "files": [f"{rel}/pmc_fetch_{c}.txt", f"{rel}/pmc_write_{c}.txt"]},
                       open(os.path.join(os.path.dirname(dst), f"pmc_{c}.json"), "w"), indent=1)
-    sq = load(os.path.join(src, "sq_c2"))
-    with open(os.path.join(dst, "pmc_sq_c2.txt"), "w") as out:
-        for k, v in sq.items():
-            if "fdfs::" in k:
-                out.write(f"{short(k)} {json.dumps(v)}\n")
+    for c in ("c2", "c3"):
+        if not os.path.isdir(os.path.join(src, f"sq_{c}")):
+            continue
+        sq = load(os.path.join(src, f"sq_{c}"))
+        with open(os.path.join(dst, f"pmc_sq_{c}.txt"), "w") as out:
+            for k, v in sq.items():
+                if "fdfs::" in k:
+                    out.write(f"{short(k)} {json.dumps(v)}\n")
     with open(os.path.join(dst, "probes_c2.txt"), "w") as out:
         for m in (1, 2):
             log = os.path.join(src, f"probe_c2_mode{m}.log")
