@@ -273,9 +273,22 @@ hipError_t launch_sig_hash(bool sar, const uint8_t *base, const uint64_t *offs,
         const char *ev = getenv("FDFS_GPU_HASH_MODE");
         mode = ev ? atoi(ev) : 0;
     }
-    const unsigned grid = (n + kHashBlock - 1) / kHashBlock;
-#define HASH_LAUNCH(S, M) \
-    sig_hash_kernel<S, 0, M><<<grid, kHashBlock, 0, st>>>(base, offs, sizes, order, n, tabs, crc_out, sig_out, codes_out)
+    static int tm = -1;
+    if (tm < 0) {  // FDFS_GPU_HASH_TM: CRC table form, 0 = slice-by-16 bytes, 2 = rotated rep8
+        const char *ev = getenv("FDFS_GPU_HASH_TM");
+        tm = ev ? atoi(ev) : 0;
+    }
+    const unsigned blk = tm == 2 ? 1024 : kHashBlock;
+    const unsigned grid = (n + blk - 1) / blk;
+#define HASH_LAUNCH(S, M)                                                                                \
+    do {                                                                                                 \
+        if (tm == 2)                                                                                     \
+            sig_hash_kernel<S, 2, M><<<grid, blk, 0, st>>>(base, offs, sizes, order, n, tabs, crc_out,   \
+                                                           sig_out, codes_out);                          \
+        else                                                                                             \
+            sig_hash_kernel<S, 0, M><<<grid, blk, 0, st>>>(base, offs, sizes, order, n, tabs, crc_out,   \
+                                                           sig_out, codes_out);                          \
+    } while (0)
     if (mode == 1)
         HASH_LAUNCH(true, 1);
     else if (mode == 2)
