@@ -63,6 +63,15 @@ int main(int argc, char *argv[])
         sizes[i] = (uint64_t)st.st_size;
         total += (sizes[i] + 15) & ~15ull;  /* 16-byte aligned file starts */
     }
+    /* the device first: without a GPU this fails loudly (ENODEV), there is
+     * no CPU path */
+    const char *u = getenv("FDFS_UNSIGNED_HASH");
+    fdfs_gpu_ctx *ctx = NULL;
+    int rc = fdfs_gpu_open(0, (u && *u == '1') ? FDFS_GPU_FLAG_UNSIGNED_HASH : 0, &ctx);
+    if (rc) {
+        printf("fdfs_gpu_open fail, errno: %d, error info: %s\n", rc, strerror(rc));
+        return rc;
+    }
     unsigned char *host = NULL;
     if (hipHostMalloc((void **)&host, total ? total : 16, 0) != hipSuccess)
         return ENOMEM;
@@ -73,13 +82,6 @@ int main(int argc, char *argv[])
                    __LINE__, argv[i + 1], e, strerror(e));
             return e;
         }
-    }
-    const char *u = getenv("FDFS_UNSIGNED_HASH");
-    fdfs_gpu_ctx *ctx = NULL;
-    int rc = fdfs_gpu_open(0, (u && *u == '1') ? FDFS_GPU_FLAG_UNSIGNED_HASH : 0, &ctx);
-    if (rc) {
-        printf("fdfs_gpu_open fail, errno: %d, error info: %s\n", rc, strerror(rc));
-        return rc;
     }
     void *d_data = NULL, *d_offs = NULL, *d_sizes = NULL, *d_crc = NULL;
     if (hipMalloc(&d_data, total ? total : 16) != hipSuccess ||
