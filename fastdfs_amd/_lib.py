@@ -35,6 +35,7 @@ EXPORTS = (
     "fdfs_gpu_trunk_pack",
     "fdfs_gpu_trunk_unpack",
     "fdfs_gpu_fdht_route",
+    "fdfs_gpu_fdht_route_keys",
     "fdfs_gpu_scrub",
     "fdfs_gpu_last_error",
 )
@@ -99,6 +100,9 @@ def load() -> ctypes.CDLL:
     L.fdfs_gpu_fdht_route.restype = i32
     L.fdfs_gpu_fdht_route.argtypes = [vp, vp, u64, ctypes.c_char_p, i32, u32, vp, vp, vp, vp, vp,
                                       vp, vp]
+    L.fdfs_gpu_fdht_route_keys.restype = i32
+    L.fdfs_gpu_fdht_route_keys.argtypes = [vp, vp, u32, vp, u64, ctypes.c_char_p, i32, u32, vp, vp,
+                                           vp, vp, vp, vp, vp]
     L.fdfs_gpu_scrub.restype = i32
     L.fdfs_gpu_scrub.argtypes = [vp, ctypes.POINTER(FdfsGpuBatch), vp, vp, vp, vp, vp]
     L.fdfs_gpu_last_error.restype = ctypes.c_char_p

@@ -248,6 +248,35 @@ class Context:
                  "fdfs_gpu_fdht_route")
         return kh, grp, srv, order, start
 
+    def fdht_route_keys(self, keys: torch.Tensor, namespace: bytes, group_count: int,
+                        key_len: torch.Tensor | None = None,
+                        servers_per_group: torch.Tensor | None = None, stream=None):
+        """FastDHT routing of (namespace, obj_id) keys given as records
+        uint8[n, stride] (stride % 4 == 0, <= 128), the first key_len[i]
+        (int32[n], default stride) bytes of each hashed.  Same outputs as
+        fdht_route."""
+        _check_dev(keys, "keys", torch.uint8)
+        if keys.dim() != 2:
+            raise ValueError("keys must be uint8[n, stride]")
+        if key_len is not None:
+            _check_dev(key_len, "key_len", torch.int32)
+        if servers_per_group is not None:
+            _check_dev(servers_per_group, "servers_per_group", torch.int32)
+        n, stride = keys.shape
+        dev = keys.device
+        kh = torch.empty(n, dtype=torch.int32, device=dev)
+        grp = torch.empty(n, dtype=torch.int32, device=dev)
+        srv = torch.empty(n, dtype=torch.int32, device=dev)
+        order = torch.empty(n, dtype=torch.int64, device=dev)
+        start = torch.empty(group_count + 1, dtype=torch.int64, device=dev)
+        self._rc(self._L.fdfs_gpu_fdht_route_keys(self._h, keys.data_ptr(), stride, _ptr(key_len), n,
+                                                  namespace, len(namespace), group_count,
+                                                  _ptr(servers_per_group), kh.data_ptr(),
+                                                  grp.data_ptr(), srv.data_ptr(), order.data_ptr(),
+                                                  start.data_ptr(), _stream_handle(stream)),
+                 "fdfs_gpu_fdht_route_keys")
+        return kh, grp, srv, order, start
+
     def scrub(self, data: torch.Tensor, offsets: torch.Tensor, sizes: torch.Tensor,
               expected_crc: torch.Tensor, stream=None):
         """Recompute every file's CRC32 and compare: (crc int32[n], bad uint8[n], nbad int32[1])."""

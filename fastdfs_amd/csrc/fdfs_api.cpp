@@ -444,18 +444,21 @@ int fdfs_gpu_trunk_unpack(fdfs_gpu_ctx *ctx, const uint8_t *hdr, uint32_t n, uin
     return e == hipSuccess ? 0 : fail(ctx, e, "trunk_unpack launch");
 }
 
-int fdfs_gpu_fdht_route(fdfs_gpu_ctx *ctx, const uint8_t *sig, uint64_t n, const char *ns,
-                        int ns_len, uint32_t group_count, const uint32_t *servers_per_group,
-                        int32_t *key_hash_out, uint32_t *group_out, uint32_t *server_out,
-                        uint64_t *order_out, uint64_t *group_start_out, void *stream)
+int fdfs_gpu_fdht_route_keys(fdfs_gpu_ctx *ctx, const uint8_t *keys, uint32_t key_stride,
+                             const uint32_t *key_len, uint64_t n, const char *ns, int ns_len,
+                             uint32_t group_count, const uint32_t *servers_per_group,
+                             int32_t *key_hash_out, uint32_t *group_out, uint32_t *server_out,
+                             uint64_t *order_out, uint64_t *group_start_out, void *stream)
 {
-    // FDHT_MAX_NAMESPACE_LEN (storage/fdht_client/fdht_types.h:23); an empty
-    // namespace is rejected like CALC_KEY_HASH_CODE does with an object id
+    // FDHT_MAX_NAMESPACE_LEN / FDHT_MAX_OBJECT_ID_LEN (storage/fdht_client/fdht_types.h:23-24);
+    // an empty namespace is rejected like CALC_KEY_HASH_CODE does with an object id
     if (!ctx || !ns || ns_len <= 0 || ns_len > 64 || group_count == 0 || !group_start_out)
         return EINVAL;
-    if (n && (!sig || !key_hash_out || !group_out || !server_out))
+    if (key_stride == 0 || key_stride > 128 || (key_stride & 3))
         return EINVAL;
-    if (reinterpret_cast<uintptr_t>(sig) & 7)  // the kernel reads each record as 3 x u64
+    if (n && (!keys || !key_hash_out || !group_out || !server_out))
+        return EINVAL;
+    if (reinterpret_cast<uintptr_t>(keys) & 3)  // the kernel reads each key as u32 words
         return EINVAL;
     DeviceGuard g(ctx->device);
     if (!g.ok)
@@ -468,10 +471,20 @@ int fdfs_gpu_fdht_route(fdfs_gpu_ctx *ctx, const uint8_t *sig, uint64_t n, const
     uint32_t *gcount = cv.take<uint32_t>(group_count);
     uint64_t *cursor = cv.take<uint64_t>(group_count);
     const uint32_t h0 = fdfs::pjw_prefix(ctx->sar, ns, ns_len);
-    hipError_t e = fdfs::launch_fdht_route(ctx->sar, sig, n, h0, group_count, servers_per_group,
-                                           key_hash_out, group_out, server_out, gcount,
-                                           group_start_out, cursor, order_out, st);
+    hipError_t e = fdfs::launch_fdht_route(ctx->sar, keys, key_stride, key_len, n, h0, group_count,
+                                           servers_per_group, key_hash_out, group_out, server_out,
+                                           gcount, group_start_out, cursor, order_out, st);
     return e == hipSuccess ? 0 : fail(ctx, e, "fdht_route launch");
+}
+
+int fdfs_gpu_fdht_route(fdfs_gpu_ctx *ctx, const uint8_t *sig, uint64_t n, const char *ns,
+                        int ns_len, uint32_t group_count, const uint32_t *servers_per_group,
+                        int32_t *key_hash_out, uint32_t *group_out, uint32_t *server_out,
+                        uint64_t *order_out, uint64_t *group_start_out, void *stream)
+{
+    return fdfs_gpu_fdht_route_keys(ctx, sig, 24, nullptr, n, ns, ns_len, group_count,
+                                    servers_per_group, key_hash_out, group_out, server_out, order_out,
+                                    group_start_out, stream);
 }
 
 int fdfs_gpu_scrub(fdfs_gpu_ctx *ctx, const fdfs_gpu_batch *batch, const uint32_t *expected_crc,

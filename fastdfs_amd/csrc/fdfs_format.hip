@@ -11,7 +11,7 @@
 //  * trunk_pack_kernel / trunk_unpack_kernel: trunk_pack_header /
 //    trunk_unpack_header (storage/trunk_mgr/trunk_shared.c:340-370).
 //  * fdht_route_kernel + group counting sort: the FastDHT partition of the
-//    dedup keys (ns, sig, "fid"): CALC_KEY_HASH_CODE
+//    dedup keys ((ns, sig, "fid"), (ns, file id, "ref" / "sig")): CALC_KEY_HASH_CODE
 //    (storage/fdht_client/fdht_client.c:256-305), group = hash % group_count
 //    (:375-376), server = get_connection's rotate-16 % count (:207-212), and
 //    the records ordered by group so each group's keys go out in one
@@ -196,10 +196,14 @@ __global__ void trunk_unpack_kernel(const uint8_t *__restrict__ hdr, uint32_t n,
         ext[7ull * i + k] = h[17 + k];
 }
 
-// key = ns || 0x01 || sig; the namespace prefix's PJW state is computed once
-// on the host (it is the same for every key) and passed as h0.
+// key = ns || 0x01 || obj_id; the namespace prefix's PJW state is computed
+// once on the host (it is the same for every key) and passed as h0.  The
+// obj ids are records of `stride` bytes (4-aligned), `lens[i]` (or `stride`)
+// of them hashed: 24-byte signatures for the "fid" keys, file-id strings
+// ("group/M00/..") for the "ref" and "sig" keys.
 template <bool SAR>
-__global__ void fdht_route_kernel(const uint8_t *__restrict__ sig, uint64_t n, uint32_t h0,
+__global__ void fdht_route_kernel(const uint8_t *__restrict__ keys, uint32_t stride,
+                                  const uint32_t *__restrict__ lens, uint64_t n, uint32_t h0,
                                   uint32_t group_count, const uint32_t *__restrict__ servers,
                                   int32_t *__restrict__ hash_out, uint32_t *__restrict__ group_out,
                                   uint32_t *__restrict__ server_out, uint32_t *__restrict__ gcount)
@@ -207,17 +211,22 @@ __global__ void fdht_route_kernel(const uint8_t *__restrict__ sig, uint64_t n, u
     const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n)
         return;
-    const uint2 *p = reinterpret_cast<const uint2 *>(sig + 24 * i);
+    const uint32_t *p = reinterpret_cast<const uint32_t *>(keys + (uint64_t)stride * i);
+    uint32_t len = lens ? lens[i] : stride;
+    if (len > stride)
+        len = stride;
     uint32_t h = pjw_step<SAR>(h0, 0x01u);  // FDHT_FULL_KEY_SEPERATOR
-#pragma unroll
-    for (int k = 0; k < 3; k++) {
-        const uint2 v = p[k];
-#pragma unroll
-        for (int q = 0; q < 4; q++)
-            h = pjw_step<SAR>(h, (v.x >> (8 * q)) & 0xFFu);
+    uint32_t k = 0;
+    for (; k + 4 <= len; k += 4) {
+        const uint32_t v = p[k >> 2];
 #pragma unroll
         for (int q = 0; q < 4; q++)
-            h = pjw_step<SAR>(h, (v.y >> (8 * q)) & 0xFFu);
+            h = pjw_step<SAR>(h, (v >> (8 * q)) & 0xFFu);
+    }
+    if (k < len) {
+        const uint32_t v = p[k >> 2];
+        for (int q = 0; k + q < len; q++)
+            h = pjw_step<SAR>(h, (v >> (8 * q)) & 0xFFu);
     }
     const int32_t kh = (int32_t)h & 0x7FFFFFFF;  // CALC_KEY_HASH_CODE: clear the sign
     const uint32_t g = (uint32_t)kh % group_count;
@@ -320,22 +329,25 @@ uint32_t pjw_prefix(bool sar, const char *ns, int len)
     return h;
 }
 
-hipError_t launch_fdht_route(bool sar, const uint8_t *sig, uint64_t n, uint32_t h0,
-                             uint32_t group_count, const uint32_t *servers, int32_t *hash_out,
-                             uint32_t *group_out, uint32_t *server_out, uint32_t *gcount,
-                             uint64_t *start, uint64_t *cursor, uint64_t *order, hipStream_t st)
+hipError_t launch_fdht_route(bool sar, const uint8_t *keys, uint32_t stride, const uint32_t *lens,
+                             uint64_t n, uint32_t h0, uint32_t group_count, const uint32_t *servers,
+                             int32_t *hash_out, uint32_t *group_out, uint32_t *server_out,
+                             uint32_t *gcount, uint64_t *start, uint64_t *cursor, uint64_t *order,
+                             hipStream_t st)
 {
     hipError_t e = hipMemsetAsync(gcount, 0, sizeof(uint32_t) * group_count, st);
     if (e != hipSuccess)
         return e;
-    if (sar)
-        fdht_route_kernel<true><<<blocks(n, 256), 256, 0, st>>>(sig, n, h0, group_count, servers,
-                                                               hash_out, group_out, server_out, gcount);
-    else
-        fdht_route_kernel<false><<<blocks(n, 256), 256, 0, st>>>(sig, n, h0, group_count, servers,
-                                                                hash_out, group_out, server_out, gcount);
+    if (n && sar)
+        fdht_route_kernel<true><<<blocks(n, 256), 256, 0, st>>>(keys, stride, lens, n, h0, group_count,
+                                                               servers, hash_out, group_out, server_out,
+                                                               gcount);
+    else if (n)
+        fdht_route_kernel<false><<<blocks(n, 256), 256, 0, st>>>(keys, stride, lens, n, h0, group_count,
+                                                                servers, hash_out, group_out, server_out,
+                                                                gcount);
     group_scan_kernel<<<1, 64, 0, st>>>(gcount, group_count, start, cursor);
-    if (order)
+    if (order && n)
         group_scatter_kernel<<<blocks(n, 256), 256, 0, st>>>(group_out, n, cursor, order);
     return hipGetLastError();
 }

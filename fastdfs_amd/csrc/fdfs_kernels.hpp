@@ -48,10 +48,11 @@ hipError_t launch_trunk_unpack(const uint8_t *hdr, uint32_t n, uint8_t *type, in
                                int32_t *size, uint32_t *crc, int32_t *mtime, uint8_t *ext,
                                hipStream_t st);
 uint32_t pjw_prefix(bool sar, const char *ns, int len);
-hipError_t launch_fdht_route(bool sar, const uint8_t *sig, uint64_t n, uint32_t h0,
-                             uint32_t group_count, const uint32_t *servers, int32_t *hash_out,
-                             uint32_t *group_out, uint32_t *server_out, uint32_t *gcount,
-                             uint64_t *start, uint64_t *cursor, uint64_t *order, hipStream_t st);
+hipError_t launch_fdht_route(bool sar, const uint8_t *keys, uint32_t stride, const uint32_t *lens,
+                             uint64_t n, uint32_t h0, uint32_t group_count, const uint32_t *servers,
+                             int32_t *hash_out, uint32_t *group_out, uint32_t *server_out,
+                             uint32_t *gcount, uint64_t *start, uint64_t *cursor, uint64_t *order,
+                             hipStream_t st);
 hipError_t launch_scrub(const uint32_t *crc, const uint32_t *expect, uint32_t n, uint8_t *bad,
                         uint32_t *nbad, hipStream_t st);
 

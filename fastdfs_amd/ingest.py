@@ -1,0 +1,88 @@
+"""Bulk / recovery ingest: the FastDHT state of a batch of stored files, in
+bulk.
+
+Today `storage_disk_recovery` (storage/storage_disk_recovery.c:512-761) and
+the sync receiver (storage/storage_service.c:5468-5779) re-store files
+without signatures, and a normal upload with `check_file_duplicate` pays one
+FastDHT round trip per file plus two SETs on a miss and an INC per link
+(storage/storage_service.c:2652,2714,2734,2984).  For a batch of files that
+already have their file ids, `recovery_records` computes, on the GPU:
+
+* the CRC32 and 24-byte signature of every file (fdfs_gpu_sig_batch);
+* the dedup decision (fdfs_gpu_dedup): the class source is the first file
+  of the batch with that signature, the class size is the "ref" count a
+  sequential ingest leaves (A9);
+* the three FastDHT record sets a sequential ingest writes, each routed to
+  its FastDHT group and server and ordered group by group so that one
+  `fdht_batch_set_ex` (storage/fdht_client/fdht_client.c:512) per group
+  replaces the per-file RPCs:
+    - "fid": key (ns, sig), value = the source's file id (:2714), sources only;
+    - "ref": key (ns, source file id), value = class size (:2734, :2984);
+    - "sig": key (ns, file id), value = sig, every file
+      (storage_set_link_file_meta, :2996-3004).
+
+This is the host side of the path, a thin composition of C-ABI calls (the
+same sequence a C caller makes); every byte of compute is a
+libfdfs_gpu kernel.
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass
+
+import torch
+
+from .api import Context
+
+
+@dataclass
+class Routed:
+    """One FastDHT record set: records i = 0..m-1 with key hash, group,
+    server; `order` lists them group by group, `group_start` the bounds."""
+    index: torch.Tensor        # int64[m]: the file each record belongs to
+    key_hash: torch.Tensor     # int32[m]
+    group: torch.Tensor        # int32[m]
+    server: torch.Tensor       # int32[m]
+    order: torch.Tensor        # int64[m]
+    group_start: torch.Tensor  # int64[group_count + 1]
+
+
+@dataclass
+class RecoveryBatch:
+    crc: torch.Tensor   # int32[n] (uint32 bit pattern)
+    sig: torch.Tensor   # uint8[n, 24]
+    rep: torch.Tensor   # int64[n]: ingest index of the class source
+    ref: torch.Tensor   # int32[n]: class size
+    fid: Routed         # sources only; key = sig, value = file_ids[index]
+    ref_rec: Routed     # sources only; key = file_ids[index], value = ref[index]
+    sig_rec: Routed     # every file; key = file_ids[index], value = sig[index]
+
+
+def recovery_records(ctx: Context, data: torch.Tensor, offsets: torch.Tensor, sizes: torch.Tensor,
+                     file_ids: torch.Tensor, file_id_len: torch.Tensor, namespace: bytes,
+                     group_count: int, servers_per_group: torch.Tensor | None = None,
+                     method: int = 1, stream=None) -> RecoveryBatch:
+    """file_ids: uint8[n, stride] (stride % 4 == 0, <= 128) holding each
+    file's id "group/M00/00/00/<name><ext>" in its first file_id_len[i]
+    (int32[n]) bytes; method: FDFS_SIG_HASH (1) or FDFS_SIG_MD5 (2)."""
+    if method not in (1, 2):
+        raise ValueError("method must be FDFS_SIG_HASH or FDFS_SIG_MD5 (dedup needs a signature)")
+    n = offsets.numel()
+    if file_ids.shape[0] != n or file_id_len.numel() != n:
+        raise ValueError("one file id per file")
+    crc, sig, _ = ctx.sig_batch(data, offsets, sizes, method=method, stream=stream)
+    rep, ref = ctx.dedup(sig, stream=stream)
+    idx = torch.arange(n, device=sig.device, dtype=torch.int64)
+    src = torch.nonzero(rep == idx).flatten()  # class sources, ingest order
+
+    def route(keys, lens, index):
+        kh, grp, srv, order, start = ctx.fdht_route_keys(keys, namespace, group_count, lens,
+                                                         servers_per_group, stream=stream)
+        return Routed(index, kh, grp, srv, order, start)
+
+    src_sig = sig.index_select(0, src).contiguous()
+    src_ids = file_ids.index_select(0, src).contiguous()
+    src_len = file_id_len.index_select(0, src).contiguous()
+    return RecoveryBatch(crc=crc, sig=sig, rep=rep, ref=ref,
+                         fid=route(src_sig, None, src),
+                         ref_rec=route(src_ids, src_len, src),
+                         sig_rec=route(file_ids, file_id_len, idx))

@@ -29,7 +29,8 @@
  *   trunk_pack_header / trunk_unpack_header
  *       storage/trunk_mgr/trunk_shared.c:340-370 -> fdfs_gpu_trunk_pack / _unpack
  *   CALC_KEY_HASH_CODE + group / server pick of the dedup keys
- *       storage/fdht_client/fdht_client.c:207-212,256-305,375-376 -> fdfs_gpu_fdht_route
+ *       storage/fdht_client/fdht_client.c:207-212,256-305,375-376 -> fdfs_gpu_fdht_route,
+ *       fdfs_gpu_fdht_route_keys
  *   (new) CRC scrub of stored files against their file-id CRCs -> fdfs_gpu_scrub
  */
 #ifndef FDFS_GPU_H
@@ -194,6 +195,19 @@ int fdfs_gpu_fdht_route(fdfs_gpu_ctx *ctx, const uint8_t *sig, uint64_t n, const
                         int ns_len, uint32_t group_count, const uint32_t *servers_per_group,
                         int32_t *key_hash_out, uint32_t *group_out, uint32_t *server_out,
                         uint64_t *order_out, uint64_t *group_start_out, void *stream);
+
+/* The same routing for any FastDHT object ids: `n` records of `key_stride`
+ * bytes (4-aligned device buffer, key_stride a multiple of 4 and <= 128 =
+ * FDHT_MAX_OBJECT_ID_LEN), the first key_len[i] bytes of record i hashed
+ * (key_len: device uint32[n], or NULL for key_stride bytes each).  The "ref"
+ * and "sig" keys of storage_set_link_file_meta (storage/storage_service.c:
+ * 2948-3020) use the file id string ("group/M00/00/00/..ext") as object id.
+ * fdfs_gpu_fdht_route is this call with 24-byte signature records. */
+int fdfs_gpu_fdht_route_keys(fdfs_gpu_ctx *ctx, const uint8_t *keys, uint32_t key_stride,
+                             const uint32_t *key_len, uint64_t n, const char *ns, int ns_len,
+                             uint32_t group_count, const uint32_t *servers_per_group,
+                             int32_t *key_hash_out, uint32_t *group_out, uint32_t *server_out,
+                             uint64_t *order_out, uint64_t *group_start_out, void *stream);
 
 /* Scrub: recompute the CRC32 of every file of the batch (as
  * FDFS_SIG_CRC_ONLY) and compare with expected_crc (e.g. from

@@ -587,11 +587,18 @@ void orc_fdht_route(const char *ns, int ns_len, const uint8_t sig[24], uint32_t 
                     uint32_t servers, int variant, int32_t *key_hash, uint32_t *group,
                     uint32_t *server)
 {
-    uint8_t key[64 + 1 + 24];
+    orc_fdht_route_key(ns, ns_len, sig, 24, group_count, servers, variant, key_hash, group, server);
+}
+
+void orc_fdht_route_key(const char *ns, int ns_len, const uint8_t *obj, int obj_len,
+                        uint32_t group_count, uint32_t servers, int variant, int32_t *key_hash,
+                        uint32_t *group, uint32_t *server)
+{
+    uint8_t key[64 + 1 + 128];
     memcpy(key, ns, (size_t)ns_len);
     key[ns_len] = 0x01;  /* FDHT_FULL_KEY_SEPERATOR */
-    memcpy(key + ns_len + 1, sig, 24);
-    int32_t h = orc_pjw_hash(key, (size_t)ns_len + 25, variant);
+    memcpy(key + ns_len + 1, obj, (size_t)obj_len);
+    int32_t h = orc_pjw_hash(key, (size_t)ns_len + 1 + (size_t)obj_len, variant);
     if (h < 0)
         h &= 0x7FFFFFFF;
     *key_hash = h;

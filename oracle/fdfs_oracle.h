@@ -132,6 +132,10 @@ void orc_trunk_pack(uint8_t file_type, int32_t alloc_size, int32_t file_size,
 void orc_fdht_route(const char *ns, int ns_len, const uint8_t sig[24], uint32_t group_count,
                     uint32_t servers, int variant, int32_t *key_hash, uint32_t *group,
                     uint32_t *server);
+/* The same for any object id (ns || 0x01 || obj, obj_len <= 128). */
+void orc_fdht_route_key(const char *ns, int ns_len, const uint8_t *obj, int obj_len,
+                        uint32_t group_count, uint32_t servers, int variant, int32_t *key_hash,
+                        uint32_t *group, uint32_t *server);
 
 #ifdef __cplusplus
 }

@@ -191,6 +191,9 @@ def _fmt_lib():
         L.orc_fdht_route.restype = None
         L.orc_fdht_route.argtypes = [ctypes.c_char_p, ctypes.c_int, vp, u32, u32, ctypes.c_int,
                                      vp, vp, vp]
+        L.orc_fdht_route_key.restype = None
+        L.orc_fdht_route_key.argtypes = [ctypes.c_char_p, ctypes.c_int, vp, ctypes.c_int, u32, u32,
+                                         ctypes.c_int, vp, vp, vp]
         L._fmt_ready = True
     return L
 
@@ -265,4 +268,23 @@ def fdht_route(ns: bytes, sig, group_count: int, servers_per_group,
         L.orc_fdht_route(ns, len(ns), sig[i].ctypes.data, group_count,
                          int(servers_per_group[g.value]), variant, kh[i:].ctypes.data,
                          grp[i:].ctypes.data, srv[i:].ctypes.data)
+    return kh, grp, srv
+
+
+def fdht_route_keys(ns: bytes, keys, lens, group_count: int, servers_per_group,
+                    variant: int = VARIANT_SIGNED):
+    """(key_hash i32, group u32, server u32) for obj ids keys[i, :lens[i]]."""
+    keys = np.ascontiguousarray(keys, np.uint8)
+    n = keys.shape[0]
+    kh, grp, srv = np.zeros(n, np.int32), np.zeros(n, np.uint32), np.zeros(n, np.uint32)
+    L = _fmt_lib()
+    for i in range(n):
+        g = ctypes.c_uint32()
+        row = np.ascontiguousarray(keys[i])
+        L.orc_fdht_route_key(ns, len(ns), row.ctypes.data, int(lens[i]), group_count, 1, variant,
+                             kh[i:].ctypes.data, ctypes.byref(g), srv[i:].ctypes.data)
+        grp[i] = g.value
+        L.orc_fdht_route_key(ns, len(ns), row.ctypes.data, int(lens[i]), group_count,
+                             int(servers_per_group[g.value]), variant, kh[i:].ctypes.data,
+                             grp[i:].ctypes.data, srv[i:].ctypes.data)
     return kh, grp, srv

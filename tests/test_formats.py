@@ -251,3 +251,89 @@ def test_gpu_scrub(oracle, ctxs):
     assert np.array_equal(crc.cpu().numpy().view(np.uint32), ocrc)
     assert set(np.nonzero(bad.cpu().numpy())[0]) == set(flip)
     assert int(nbad.item()) == 37
+
+
+# ---- FastDHT routing of file-id keys, recovery batch ----
+
+def _file_id_table(n, rng, stride=64):
+    """n file ids "group1/M00/XX/YY/<27 chars>.<ext>" as uint8[n, stride] + lengths."""
+    import base64 as b64
+    ids = np.zeros((n, stride), np.uint8)
+    lens = np.zeros(n, np.int32)
+    for i in range(n):
+        core = b64.urlsafe_b64encode(rng.integers(0, 256, 20, dtype=np.uint8).tobytes())[:27]
+        ext = [b"", b".jpg", b".c", b".part2.c"][i % 4]
+        s = b"group1/M%02X/%02X/%02X/" % (i % 3, rng.integers(0, 256), rng.integers(0, 256)) + core + ext
+        ids[i, :len(s)] = np.frombuffer(s, np.uint8)
+        lens[i] = len(s)
+    return ids, lens
+
+
+def test_fdht_route_keys_oracle_matches_sig_route(oracle):
+    rng = np.random.default_rng(12)
+    sig = rng.integers(0, 256, size=(50, 24), dtype=np.uint8)
+    servers = np.array([2, 3, 1], np.uint32)
+    a = oracle.fdht_route(b"ns", sig, 3, servers)
+    b = oracle.fdht_route_keys(b"ns", sig, np.full(50, 24), 3, servers)
+    for x, y in zip(a, b):
+        assert np.array_equal(x, y)
+    ids, lens = _file_id_table(20, rng)
+    kh, _, _ = oracle.fdht_route_keys(b"ns", ids, lens, 3, servers)
+    for i in range(20):
+        want = _pjw_py(b"ns\x01" + ids[i, :lens[i]].tobytes()) & 0x7FFFFFFF
+        assert int(kh[i]) == want
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("variant", [0, 1])
+def test_gpu_fdht_route_keys(oracle, ctxs, variant):
+    rng = np.random.default_rng(31 + variant)
+    ids, lens = _file_id_table(3000, rng)
+    servers = np.array([1, 2, 3, 4, 5], np.uint32)
+    kh, grp, srv, order, start = ctxs[variant].fdht_route_keys(
+        _cuda(ids), b"FastDFS", 5, _cuda(lens), _cuda(servers.view(np.int32)))
+    okh, ogrp, osrv = oracle.fdht_route_keys(b"FastDFS", ids, lens, 5, servers, variant)
+    assert np.array_equal(kh.cpu().numpy(), okh)
+    assert np.array_equal(grp.cpu().numpy().view(np.uint32), ogrp)
+    assert np.array_equal(srv.cpu().numpy().view(np.uint32), osrv)
+    g, o, st = grp.cpu().numpy(), order.cpu().numpy(), start.cpu().numpy()
+    assert np.array_equal(np.sort(o), np.arange(3000))
+    assert np.array_equal(g[o], np.repeat(np.arange(5), np.diff(st)))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("method", [1, 2])
+def test_gpu_recovery_records(oracle, ctxs, method):
+    from fastdfs_amd.ingest import recovery_records
+    rng = np.random.default_rng(40 + method)
+    # 400 distinct contents, 1000 files: duplicates across the batch
+    uniq = [rng.integers(0, 256, size=int(rng.integers(0, 20_000)), dtype=np.uint8) for _ in range(400)]
+    pick = rng.integers(0, 400, size=1000)
+    sizes = np.array([len(uniq[p]) for p in pick], np.int64)
+    offs = np.zeros_like(sizes)
+    offs[1:] = np.cumsum((sizes + 15) // 16 * 16)[:-1]
+    buf = np.zeros(int(offs[-1] + sizes[-1]) + 16, np.uint8)
+    for i, p in enumerate(pick):
+        buf[offs[i]:offs[i] + sizes[i]] = uniq[p]
+    ids, lens = _file_id_table(1000, rng)
+    servers = np.array([2, 1, 3, 2], np.uint32)
+    rb = recovery_records(ctxs[0], _cuda(buf), _cuda(offs), _cuda(sizes), _cuda(ids), _cuda(lens),
+                          b"FastDFS", 4, _cuda(servers.view(np.int32)), method=method)
+    ocrc, osig = oracle.dio_batch(buf, offs, sizes, method, 0, nthreads=4)
+    orep, oref = oracle.dedup(osig)
+    assert np.array_equal(rb.crc.cpu().numpy().view(np.uint32), ocrc)
+    assert np.array_equal(rb.sig.cpu().numpy(), osig)
+    assert np.array_equal(rb.rep.cpu().numpy(), orep.astype(np.int64))
+    assert np.array_equal(rb.ref.cpu().numpy(), oref.astype(np.int32))
+    src = np.nonzero(orep == np.arange(1000))[0]
+    assert np.array_equal(rb.fid.index.cpu().numpy(), src)
+    assert len(src) == len(np.unique(pick))
+    for rec, keys, klen in ((rb.fid, osig[src], np.full(len(src), 24)),
+                            (rb.ref_rec, ids[src], lens[src]),
+                            (rb.sig_rec, ids, lens)):
+        okh, ogrp, osrv = oracle.fdht_route_keys(b"FastDFS", keys, klen, 4, servers)
+        assert np.array_equal(rec.key_hash.cpu().numpy(), okh)
+        assert np.array_equal(rec.group.cpu().numpy().view(np.uint32), ogrp)
+        assert np.array_equal(rec.server.cpu().numpy().view(np.uint32), osrv)
+        o, st = rec.order.cpu().numpy(), rec.group_start.cpu().numpy()
+        assert np.array_equal(ogrp[o], np.repeat(np.arange(4), np.diff(st)).astype(np.uint32))
