@@ -328,6 +328,11 @@ def main():
                            "traffic": None,
                            "kernel": "dedup_group (dp_keys + scan + dp_scatter + dp_split + dp_group)",
                            "kernel_ms_avg": round(avg_ms, 4), "algorithmic_bytes_per_launch": nb}
+        if world == 1:
+            traffic, tsrc = load_traffic("c5", res["roofline"]["kernel"])
+            if traffic:
+                res["roofline"]["traffic"] = traffic
+                res["roofline"]["traffic_source"] = tsrc
         if rank == 0 and world == 1 and not args.no_cpu_baseline:
             res["cpu_baseline"] = cpu_dedup_baseline(sig, args.cpu_seconds)
         else:

@@ -25,7 +25,7 @@ step stats_c2 600 rocprofv3 --kernel-trace --stats -d $O/stats_c2 -o run --outpu
 step stats_c3 600 rocprofv3 --kernel-trace --stats -d $O/stats_c3 -o run --output-format csv -- $B --config c3 --steps 2 --warmup 1 || exit $?
 step stats_c4 600 rocprofv3 --kernel-trace --stats -d $O/stats_c4 -o run --output-format csv -- $B --config c4 $S || exit $?
 step stats_c5 600 rocprofv3 --kernel-trace --stats -d $O/stats_c5 -o run --output-format csv -- $B --config c5 $S || exit $?
-for c in c2 c3 c4; do
+for c in c2 c3 c4 c5; do
   step fetch_$c 300 rocprofv3 --pmc FETCH_SIZE -d $O/fetch_$c -o run --output-format csv -- $B --config $c --steps 1 --warmup 1 || exit $?
   step write_$c 300 rocprofv3 --pmc WRITE_SIZE -d $O/write_$c -o run --output-format csv -- $B --config $c --steps 1 --warmup 1 || exit $?
 done

@@ -18,6 +18,9 @@ BENCH_KERNEL = {"c2": ("sig_hash_kernel<true, 0, 0>", "sig_hash_kernel<SAR>"),
                 "c4": ("crc_seg_kernel<true, 2>", "crc_seg_kernel<SAR,2>")}
 
 
+BENCH_C5_KERNEL = "dedup_group (dp_keys + scan + dp_scatter + dp_split + dp_group)"
+
+
 def short(name):
     return name.split("(")[0].replace("void ", "").replace("fdfs::", "")
 
@@ -40,6 +43,32 @@ def main(src, dst):
                     if "fdfs::" in r["Name"] or "rocclr" in r["Name"]:
                         r["Name"] = short(r["Name"])
                         w.writerow(r)
+        if c == "c5":  # the dedup group is five kernels: traffic summed over them
+            tot = {}
+            for kind in ("fetch", "write"):
+                if not os.path.isdir(os.path.join(src, f"{kind}_{c}")):
+                    continue
+                d = load(os.path.join(src, f"{kind}_{c}"))
+                with open(os.path.join(dst, f"pmc_{kind}_{c}.txt"), "w") as out:
+                    for k, v in d.items():
+                        if "fdfs::" in k:
+                            out.write(f"{short(k)} {json.dumps(v)}\n")
+                for k, v in d.items():
+                    if any(x in k for x in ("dp_keys", "dp_scatter", "dp_split", "dp_group", "dp_starts",
+                                            "scan_reduce", "scan_sums", "scan_apply")):
+                        for m, val in v.items():
+                            tot[m] = tot.get(m, 0.0) + val
+            if "FETCH_SIZE" in tot and "WRITE_SIZE" in tot:
+                rd, wr = 2 * tot["FETCH_SIZE"] * 1024, tot["WRITE_SIZE"] * 1024
+                rel = os.path.relpath(dst, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+                json.dump({"kernel": BENCH_C5_KERNEL, "hbm_bytes_per_launch": round(rd + wr),
+                           "read_bytes": round(rd), "write_bytes": round(wr),
+                           "source": "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes, summed over the "
+                                     "dedup_group kernels; read = 2 x FETCH_SIZE x 1024 (gfx950 "
+                                     "correction), write = WRITE_SIZE x 1024",
+                           "files": [f"{rel}/pmc_fetch_{c}.txt", f"{rel}/pmc_write_{c}.txt"]},
+                          open(os.path.join(os.path.dirname(dst), f"pmc_{c}.json"), "w"), indent=1)
+            continue
         if c not in BENCH_KERNEL:
             continue
         pm = {}
