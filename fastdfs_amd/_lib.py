@@ -36,6 +36,7 @@ EXPORTS = (
     "fdfs_gpu_trunk_unpack",
     "fdfs_gpu_fdht_route",
     "fdfs_gpu_fdht_route_keys",
+    "fdfs_gpu_recovery_batch",
     "fdfs_gpu_scrub",
     "fdfs_gpu_last_error",
 )
@@ -52,6 +53,17 @@ class FdfsGpuBatch(ctypes.Structure):
         ("size", ctypes.c_void_p),
         ("n", ctypes.c_uint32),
     ]
+
+
+class FdfsGpuRouted(ctypes.Structure):
+    _fields_ = [(f, ctypes.c_void_p) for f in
+                ("index", "key_hash", "group", "server", "order", "group_start")]
+
+
+class FdfsGpuRecoveryOut(ctypes.Structure):
+    _fields_ = [("crc", ctypes.c_void_p), ("sig", ctypes.c_void_p), ("rep", ctypes.c_void_p),
+                ("ref", ctypes.c_void_p), ("nsources", ctypes.c_void_p),
+                ("fid", FdfsGpuRouted), ("ref_rec", FdfsGpuRouted), ("sig_rec", FdfsGpuRouted)]
 
 
 _lib = None
@@ -103,6 +115,10 @@ def load() -> ctypes.CDLL:
     L.fdfs_gpu_fdht_route_keys.restype = i32
     L.fdfs_gpu_fdht_route_keys.argtypes = [vp, vp, u32, vp, u64, ctypes.c_char_p, i32, u32, vp, vp,
                                            vp, vp, vp, vp, vp]
+    L.fdfs_gpu_recovery_batch.restype = i32
+    L.fdfs_gpu_recovery_batch.argtypes = [vp, ctypes.POINTER(FdfsGpuBatch), i32, vp, u32, vp,
+                                          ctypes.c_char_p, i32, u32, vp,
+                                          ctypes.POINTER(FdfsGpuRecoveryOut), vp]
     L.fdfs_gpu_scrub.restype = i32
     L.fdfs_gpu_scrub.argtypes = [vp, ctypes.POINTER(FdfsGpuBatch), vp, vp, vp, vp, vp]
     L.fdfs_gpu_last_error.restype = ctypes.c_char_p

@@ -3,6 +3,7 @@
 // comes from a gfx950 kernel, and a missing/failed device is an error.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cerrno>
 #include <cstdio>
 #include <cstring>
@@ -314,6 +315,10 @@ static int dedup_common(fdfs_gpu_ctx *ctx, const uint8_t *sig, uint32_t stride,
         return 0;
     if (!sig || !rep_out || !ref_out || n >= 0xFFFFFFFFull)
         return EINVAL;
+    // records are read as u64 words, rep written as u64
+    if ((reinterpret_cast<uintptr_t>(sig) | reinterpret_cast<uintptr_t>(gidx) |
+         reinterpret_cast<uintptr_t>(rep_out)) & 7)
+        return EINVAL;
     DeviceGuard g(ctx->device);
     if (!g.ok)
         return ENODEV;
@@ -350,6 +355,9 @@ int fdfs_gpu_dedup_bucket(fdfs_gpu_ctx *ctx, const uint8_t *sig, const uint64_t 
         return EINVAL;
     if (n && (!sig || !records_out))
         return EINVAL;
+    if ((reinterpret_cast<uintptr_t>(sig) | reinterpret_cast<uintptr_t>(gidx) |
+         reinterpret_cast<uintptr_t>(records_out) | reinterpret_cast<uintptr_t>(row_of_out)) & 7)
+        return EINVAL;  // u64 words
     DeviceGuard g(ctx->device);
     if (!g.ok)
         return ENODEV;
@@ -471,9 +479,9 @@ int fdfs_gpu_fdht_route_keys(fdfs_gpu_ctx *ctx, const uint8_t *keys, uint32_t ke
     uint32_t *gcount = cv.take<uint32_t>(group_count);
     uint64_t *cursor = cv.take<uint64_t>(group_count);
     const uint32_t h0 = fdfs::pjw_prefix(ctx->sar, ns, ns_len);
-    hipError_t e = fdfs::launch_fdht_route(ctx->sar, keys, key_stride, key_len, n, h0, group_count,
-                                           servers_per_group, key_hash_out, group_out, server_out,
-                                           gcount, group_start_out, cursor, order_out, st);
+    hipError_t e = fdfs::launch_fdht_route(ctx->sar, keys, key_stride, key_len, n, nullptr, h0,
+                                           group_count, servers_per_group, key_hash_out, group_out,
+                                           server_out, gcount, group_start_out, cursor, order_out, st);
     return e == hipSuccess ? 0 : fail(ctx, e, "fdht_route launch");
 }
 
@@ -485,6 +493,94 @@ int fdfs_gpu_fdht_route(fdfs_gpu_ctx *ctx, const uint8_t *sig, uint64_t n, const
     return fdfs_gpu_fdht_route_keys(ctx, sig, 24, nullptr, n, ns, ns_len, group_count,
                                     servers_per_group, key_hash_out, group_out, server_out, order_out,
                                     group_start_out, stream);
+}
+
+int fdfs_gpu_recovery_batch(fdfs_gpu_ctx *ctx, const fdfs_gpu_batch *batch, int method,
+                            const uint8_t *file_ids, uint32_t id_stride, const uint32_t *id_len,
+                            const char *ns, int ns_len, uint32_t group_count,
+                            const uint32_t *servers_per_group, fdfs_gpu_recovery_out *out,
+                            void *stream)
+{
+    if (!ctx || !batch || !out || (method != FDFS_SIG_HASH && method != FDFS_SIG_MD5))
+        return EINVAL;
+    if (!ns || ns_len <= 0 || ns_len > 64 || group_count == 0)
+        return EINVAL;
+    if (id_stride == 0 || id_stride > 128 || (id_stride & 3) ||
+        (reinterpret_cast<uintptr_t>(file_ids) & 3))
+        return EINVAL;
+    const uint64_t n = batch->n;
+    const fdfs_gpu_routed *sets[3] = {&out->fid, &out->ref_rec, &out->sig_rec};
+    for (const fdfs_gpu_routed *r : sets)
+        if (!r->group_start || (n && (!r->index || !r->key_hash || !r->group || !r->server)))
+            return EINVAL;
+    if (n && (!file_ids || !out->crc || !out->sig || !out->rep || !out->ref || !out->nsources))
+        return EINVAL;
+    if ((reinterpret_cast<uintptr_t>(out->sig) | reinterpret_cast<uintptr_t>(out->rep)) & 7)
+        return EINVAL;
+    DeviceGuard g(ctx->device);
+    if (!g.ok)
+        return ENODEV;
+    hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+    if (n == 0) {
+        for (const fdfs_gpu_routed *r : sets)
+            if (hipMemsetAsync(r->group_start, 0, 8ull * (group_count + 1), st) != hipSuccess)
+                return fail(ctx, hipGetLastError(), "recovery_batch memset");
+        return 0;
+    }
+    // workspace: region A (offset 0) is what the sig / dedup / route calls
+    // below carve for themselves; region B after it holds the compacted
+    // class sources, which must live across those calls
+    const size_t a_bytes = std::max(std::max(sig_ws_bytes(n), dedup_ws_bytes(n)),
+                                    align_up(4ull * group_count) + align_up(8ull * group_count));
+    const size_t b_bytes = align_up(8 * n) + align_up(8 * (n + 1)) +
+                           align_up(8 * fdfs::scan_workspace_elems(n)) + align_up(24 * n) +
+                           align_up((size_t)id_stride * n) + align_up(4 * n);
+    int rc = ensure_ws(ctx, a_bytes + b_bytes, st);
+    if (rc)
+        return rc;
+    Carve cv{static_cast<char *>(ctx->ws) + a_bytes};
+    uint64_t *flag = cv.take<uint64_t>(n);
+    uint64_t *pos = cv.take<uint64_t>(n + 1);
+    uint64_t *bsum = cv.take<uint64_t>(fdfs::scan_workspace_elems(n));
+    uint8_t *csig = cv.take<uint8_t>(24 * n);
+    uint8_t *cids = cv.take<uint8_t>((size_t)id_stride * n);
+    uint32_t *clen = cv.take<uint32_t>(n);
+    // 1. CRC32 + signature, 2. the dedup decision over the batch in order
+    if ((rc = fdfs_gpu_sig_batch(ctx, batch, method, out->crc, out->sig, nullptr, stream)))
+        return rc;
+    if ((rc = fdfs_gpu_dedup(ctx, out->sig, nullptr, n, out->rep, out->ref, stream)))
+        return rc;
+    // 3. class sources (rep[i] == i), compacted; sig_rec.index = 0..n-1
+    hipError_t e = fdfs::launch_sources(out->rep, n, out->sig, file_ids, id_stride, id_len, flag, pos,
+                                        bsum, out->sig_rec.index, out->fid.index, csig, cids, clen,
+                                        out->nsources, st);
+    if (e != hipSuccess)
+        return fail(ctx, e, "recovery_batch sources");
+    if (hipMemcpyAsync(out->ref_rec.index, out->fid.index, 8 * n, hipMemcpyDeviceToDevice, st) !=
+        hipSuccess)
+        return fail(ctx, hipGetLastError(), "recovery_batch copy");
+    // 4. the three record sets, routed per FastDHT group
+    Carve ca{static_cast<char *>(ctx->ws)};
+    uint32_t *gcount = ca.take<uint32_t>(group_count);
+    uint64_t *cursor = ca.take<uint64_t>(group_count);
+    const uint32_t h0 = fdfs::pjw_prefix(ctx->sar, ns, ns_len);
+    struct Job {
+        const fdfs_gpu_routed *r;
+        const uint8_t *keys;
+        uint32_t stride;
+        const uint32_t *lens;
+        const uint64_t *dcount;
+    } jobs[3] = {{&out->fid, csig, 24, nullptr, out->nsources},
+                 {&out->ref_rec, cids, id_stride, clen, out->nsources},
+                 {&out->sig_rec, file_ids, id_stride, id_len, nullptr}};
+    for (const Job &j : jobs) {
+        e = fdfs::launch_fdht_route(ctx->sar, j.keys, j.stride, j.lens, n, j.dcount, h0, group_count,
+                                    servers_per_group, j.r->key_hash, j.r->group, j.r->server, gcount,
+                                    j.r->group_start, cursor, j.r->order, st);
+        if (e != hipSuccess)
+            return fail(ctx, e, "recovery_batch route");
+    }
+    return 0;
 }
 
 int fdfs_gpu_scrub(fdfs_gpu_ctx *ctx, const fdfs_gpu_batch *batch, const uint32_t *expected_crc,

@@ -201,15 +201,18 @@ __global__ void trunk_unpack_kernel(const uint8_t *__restrict__ hdr, uint32_t n,
 // obj ids are records of `stride` bytes (4-aligned), `lens[i]` (or `stride`)
 // of them hashed: 24-byte signatures for the "fid" keys, file-id strings
 // ("group/M00/..") for the "ref" and "sig" keys.
+// dcount (device, optional): only the first *dcount records are live (the
+// class sources of a recovery batch, counted on the device).
 template <bool SAR>
 __global__ void fdht_route_kernel(const uint8_t *__restrict__ keys, uint32_t stride,
-                                  const uint32_t *__restrict__ lens, uint64_t n, uint32_t h0,
+                                  const uint32_t *__restrict__ lens, uint64_t n,
+                                  const uint64_t *__restrict__ dcount, uint32_t h0,
                                   uint32_t group_count, const uint32_t *__restrict__ servers,
                                   int32_t *__restrict__ hash_out, uint32_t *__restrict__ group_out,
                                   uint32_t *__restrict__ server_out, uint32_t *__restrict__ gcount)
 {
     const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= n)
+    if (i >= n || (dcount && i >= *dcount))
         return;
     const uint32_t *p = reinterpret_cast<const uint32_t *>(keys + (uint64_t)stride * i);
     uint32_t len = lens ? lens[i] : stride;
@@ -256,10 +259,11 @@ __global__ void group_scan_kernel(const uint32_t *__restrict__ gcount, uint32_t 
 }
 
 __global__ void group_scatter_kernel(const uint32_t *__restrict__ group, uint64_t n,
+                                     const uint64_t *__restrict__ dcount,
                                      uint64_t *__restrict__ cursor, uint64_t *__restrict__ order)
 {
     const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= n)
+    if (i >= n || (dcount && i >= *dcount))
         return;
     const uint64_t pos = atomicAdd(reinterpret_cast<unsigned long long *>(&cursor[group[i]]), 1ull);
     order[pos] = i;
@@ -330,25 +334,78 @@ uint32_t pjw_prefix(bool sar, const char *ns, int len)
 }
 
 hipError_t launch_fdht_route(bool sar, const uint8_t *keys, uint32_t stride, const uint32_t *lens,
-                             uint64_t n, uint32_t h0, uint32_t group_count, const uint32_t *servers,
-                             int32_t *hash_out, uint32_t *group_out, uint32_t *server_out,
-                             uint32_t *gcount, uint64_t *start, uint64_t *cursor, uint64_t *order,
-                             hipStream_t st)
+                             uint64_t n, const uint64_t *dcount, uint32_t h0, uint32_t group_count,
+                             const uint32_t *servers, int32_t *hash_out, uint32_t *group_out,
+                             uint32_t *server_out, uint32_t *gcount, uint64_t *start,
+                             uint64_t *cursor, uint64_t *order, hipStream_t st)
 {
     hipError_t e = hipMemsetAsync(gcount, 0, sizeof(uint32_t) * group_count, st);
     if (e != hipSuccess)
         return e;
     if (n && sar)
-        fdht_route_kernel<true><<<blocks(n, 256), 256, 0, st>>>(keys, stride, lens, n, h0, group_count,
-                                                               servers, hash_out, group_out, server_out,
-                                                               gcount);
+        fdht_route_kernel<true><<<blocks(n, 256), 256, 0, st>>>(keys, stride, lens, n, dcount, h0,
+                                                               group_count, servers, hash_out, group_out,
+                                                               server_out, gcount);
     else if (n)
-        fdht_route_kernel<false><<<blocks(n, 256), 256, 0, st>>>(keys, stride, lens, n, h0, group_count,
-                                                                servers, hash_out, group_out, server_out,
-                                                                gcount);
+        fdht_route_kernel<false><<<blocks(n, 256), 256, 0, st>>>(keys, stride, lens, n, dcount, h0,
+                                                                group_count, servers, hash_out,
+                                                                group_out, server_out, gcount);
     group_scan_kernel<<<1, 64, 0, st>>>(gcount, group_count, start, cursor);
     if (order && n)
-        group_scatter_kernel<<<blocks(n, 256), 256, 0, st>>>(group_out, n, cursor, order);
+        group_scatter_kernel<<<blocks(n, 256), 256, 0, st>>>(group_out, n, dcount, cursor, order);
+    return hipGetLastError();
+}
+
+// ---- recovery batch: the class sources, compacted on the device ----------
+
+__global__ void source_flag_kernel(const uint64_t *__restrict__ rep, uint64_t n,
+                                   uint64_t *__restrict__ flag, uint64_t *__restrict__ iota)
+{
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n)
+        return;
+    flag[i] = rep[i] == i ? 1u : 0u;  // the first file of its class (A9 "fid" source)
+    iota[i] = i;
+}
+
+// pos: exclusive scan of flag (pos[n] = number of sources)
+__global__ void source_compact_kernel(const uint64_t *__restrict__ flag, const uint64_t *__restrict__ pos,
+                                      uint64_t n, const uint8_t *__restrict__ sig,
+                                      const uint8_t *__restrict__ ids, uint32_t stride,
+                                      const uint32_t *__restrict__ lens, uint64_t *__restrict__ index,
+                                      uint8_t *__restrict__ csig, uint8_t *__restrict__ cids,
+                                      uint32_t *__restrict__ clens, uint64_t *__restrict__ nsrc)
+{
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i == 0)
+        *nsrc = pos[n];
+    if (i >= n || !flag[i])
+        return;
+    const uint64_t k = pos[i];
+    index[k] = i;
+    const uint2 *s = reinterpret_cast<const uint2 *>(sig + 24 * i);
+    uint2 *d = reinterpret_cast<uint2 *>(csig + 24 * k);
+    d[0] = s[0];
+    d[1] = s[1];
+    d[2] = s[2];
+    const uint32_t *a = reinterpret_cast<const uint32_t *>(ids + (uint64_t)stride * i);
+    uint32_t *b = reinterpret_cast<uint32_t *>(cids + (uint64_t)stride * k);
+    for (uint32_t w = 0; w < stride / 4; w++)
+        b[w] = a[w];
+    clens[k] = lens ? lens[i] : stride;
+}
+
+hipError_t launch_sources(const uint64_t *rep, uint64_t n, const uint8_t *sig, const uint8_t *ids,
+                          uint32_t stride, const uint32_t *lens, uint64_t *flag, uint64_t *pos,
+                          uint64_t *bsum, uint64_t *iota, uint64_t *index, uint8_t *csig,
+                          uint8_t *cids, uint32_t *clens, uint64_t *nsrc, hipStream_t st)
+{
+    source_flag_kernel<<<blocks(n, 256), 256, 0, st>>>(rep, n, flag, iota);
+    hipError_t e = launch_exclusive_scan(flag, n, pos, bsum, st);
+    if (e != hipSuccess)
+        return e;
+    source_compact_kernel<<<blocks(n, 256), 256, 0, st>>>(flag, pos, n, sig, ids, stride, lens, index,
+                                                          csig, cids, clens, nsrc);
     return hipGetLastError();
 }
 

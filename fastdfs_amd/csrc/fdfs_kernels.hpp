@@ -49,10 +49,14 @@ hipError_t launch_trunk_unpack(const uint8_t *hdr, uint32_t n, uint8_t *type, in
                                hipStream_t st);
 uint32_t pjw_prefix(bool sar, const char *ns, int len);
 hipError_t launch_fdht_route(bool sar, const uint8_t *keys, uint32_t stride, const uint32_t *lens,
-                             uint64_t n, uint32_t h0, uint32_t group_count, const uint32_t *servers,
-                             int32_t *hash_out, uint32_t *group_out, uint32_t *server_out,
-                             uint32_t *gcount, uint64_t *start, uint64_t *cursor, uint64_t *order,
-                             hipStream_t st);
+                             uint64_t n, const uint64_t *dcount, uint32_t h0, uint32_t group_count,
+                             const uint32_t *servers, int32_t *hash_out, uint32_t *group_out,
+                             uint32_t *server_out, uint32_t *gcount, uint64_t *start,
+                             uint64_t *cursor, uint64_t *order, hipStream_t st);
+hipError_t launch_sources(const uint64_t *rep, uint64_t n, const uint8_t *sig, const uint8_t *ids,
+                          uint32_t stride, const uint32_t *lens, uint64_t *flag, uint64_t *pos,
+                          uint64_t *bsum, uint64_t *iota, uint64_t *index, uint8_t *csig,
+                          uint8_t *cids, uint32_t *clens, uint64_t *nsrc, hipStream_t st);
 hipError_t launch_scrub(const uint32_t *crc, const uint32_t *expect, uint32_t n, uint8_t *bad,
                         uint32_t *nbad, hipStream_t st);
 

@@ -21,9 +21,9 @@ already have their file ids, `recovery_records` computes, on the GPU:
     - "sig": key (ns, file id), value = sig, every file
       (storage_set_link_file_meta, :2996-3004).
 
-This is the host side of the path, a thin composition of C-ABI calls (the
-same sequence a C caller makes); every byte of compute is a
-libfdfs_gpu kernel.
+The composition itself is C (fdfs_gpu_recovery_batch in libfdfs_gpu, the
+daemon's language); this module only wraps it for torch tensors.  Every
+byte of compute is a libfdfs_gpu kernel.
 """
 from __future__ import annotations
 
@@ -63,26 +63,47 @@ def recovery_records(ctx: Context, data: torch.Tensor, offsets: torch.Tensor, si
                      method: int = 1, stream=None) -> RecoveryBatch:
     """file_ids: uint8[n, stride] (stride % 4 == 0, <= 128) holding each
     file's id "group/M00/00/00/<name><ext>" in its first file_id_len[i]
-    (int32[n]) bytes; method: FDFS_SIG_HASH (1) or FDFS_SIG_MD5 (2)."""
+    (int32[n]) bytes; method: FDFS_SIG_HASH (1) or FDFS_SIG_MD5 (2).
+    One call of fdfs_gpu_recovery_batch (the whole composition runs in the
+    C library, stream-ordered); the fid / ref_rec sets are cut to the
+    device-counted number of class sources here."""
+    import ctypes
+
+    from . import _lib
+    from .api import _check_dev, _ptr, _stream_handle
     if method not in (1, 2):
         raise ValueError("method must be FDFS_SIG_HASH or FDFS_SIG_MD5 (dedup needs a signature)")
+    for t, nm, dt in ((data, "data", torch.uint8), (offsets, "offsets", torch.int64),
+                      (sizes, "sizes", torch.int64), (file_ids, "file_ids", torch.uint8),
+                      (file_id_len, "file_id_len", torch.int32)):
+        _check_dev(t, nm, dt)
+    if servers_per_group is not None:
+        _check_dev(servers_per_group, "servers_per_group", torch.int32)
     n = offsets.numel()
-    if file_ids.shape[0] != n or file_id_len.numel() != n:
-        raise ValueError("one file id per file")
-    crc, sig, _ = ctx.sig_batch(data, offsets, sizes, method=method, stream=stream)
-    rep, ref = ctx.dedup(sig, stream=stream)
-    idx = torch.arange(n, device=sig.device, dtype=torch.int64)
-    src = torch.nonzero(rep == idx).flatten()  # class sources, ingest order
+    if file_ids.dim() != 2 or file_ids.shape[0] != n or file_id_len.numel() != n:
+        raise ValueError("one file id record per file")
+    dev = data.device
 
-    def route(keys, lens, index):
-        kh, grp, srv, order, start = ctx.fdht_route_keys(keys, namespace, group_count, lens,
-                                                         servers_per_group, stream=stream)
-        return Routed(index, kh, grp, srv, order, start)
+    def e(dt, *shape):
+        return torch.empty(shape, dtype=dt, device=dev)
 
-    src_sig = sig.index_select(0, src).contiguous()
-    src_ids = file_ids.index_select(0, src).contiguous()
-    src_len = file_id_len.index_select(0, src).contiguous()
-    return RecoveryBatch(crc=crc, sig=sig, rep=rep, ref=ref,
-                         fid=route(src_sig, None, src),
-                         ref_rec=route(src_ids, src_len, src),
-                         sig_rec=route(file_ids, file_id_len, idx))
+    crc, sig, rep, ref, nsrc = e(torch.int32, n), e(torch.uint8, n, 24), e(torch.int64, n), \
+        e(torch.int32, n), e(torch.int64, 1)
+    sets = [[e(torch.int64, n), e(torch.int32, n), e(torch.int32, n), e(torch.int32, n),
+             e(torch.int64, n), e(torch.int64, group_count + 1)] for _ in range(3)]
+    out = _lib.FdfsGpuRecoveryOut(crc.data_ptr(), sig.data_ptr(), rep.data_ptr(), ref.data_ptr(),
+                                  nsrc.data_ptr(),
+                                  *[_lib.FdfsGpuRouted(*[t.data_ptr() for t in st]) for st in sets])
+    b = _lib.FdfsGpuBatch(data.data_ptr(), offsets.data_ptr(), sizes.data_ptr(), n)
+    ctx._rc(ctx._L.fdfs_gpu_recovery_batch(ctx._h, ctypes.byref(b), method, file_ids.data_ptr(),
+                                           file_ids.shape[1], file_id_len.data_ptr(), namespace,
+                                           len(namespace), group_count, _ptr(servers_per_group),
+                                           ctypes.byref(out), _stream_handle(stream)),
+            "fdfs_gpu_recovery_batch")
+    m = int(nsrc.item())  # synchronises the stream
+
+    def routed(st, k):
+        return Routed(st[0][:k], st[1][:k], st[2][:k], st[3][:k], st[4][:k], st[5])
+
+    return RecoveryBatch(crc=crc, sig=sig, rep=rep, ref=ref, fid=routed(sets[0], m),
+                         ref_rec=routed(sets[1], m), sig_rec=routed(sets[2], n))

@@ -32,6 +32,8 @@
  *       storage/fdht_client/fdht_client.c:207-212,256-305,375-376 -> fdfs_gpu_fdht_route,
  *       fdfs_gpu_fdht_route_keys
  *   (new) CRC scrub of stored files against their file-id CRCs -> fdfs_gpu_scrub
+ *   recovery / sync-receiver batch mode (storage/storage_disk_recovery.c:512-761,
+ *       storage/storage_service.c:5468-5779)  -> fdfs_gpu_recovery_batch
  */
 #ifndef FDFS_GPU_H
 #define FDFS_GPU_H
@@ -208,6 +210,47 @@ int fdfs_gpu_fdht_route_keys(fdfs_gpu_ctx *ctx, const uint8_t *keys, uint32_t ke
                              uint32_t group_count, const uint32_t *servers_per_group,
                              int32_t *key_hash_out, uint32_t *group_out, uint32_t *server_out,
                              uint64_t *order_out, uint64_t *group_start_out, void *stream);
+
+/* ---- Recovery / sync-receiver batch ----------------------
+ * Files that already carry their file ids (storage_disk_recovery,
+ * storage/storage_disk_recovery.c:512-761; the sync receiver,
+ * storage/storage_service.c:5468-5779) get in one stream-ordered call what a
+ * sequential ingest with check_file_duplicate leaves in FastDHT
+ * (storage/storage_service.c:2616-2785, 2948-3020):
+ *   crc / sig     CRC32 and 24-byte signature (fdfs_gpu_sig_batch, method
+ *                 FDFS_SIG_HASH or FDFS_SIG_MD5)
+ *   rep / ref     class source (first file of the batch with the signature)
+ *                 and class size (fdfs_gpu_dedup)
+ *   fid           key (ns, sig, "fid") -> file_ids[index] of the source;
+ *                 one record per class, the first *nsources entries
+ *   ref_rec       key (ns, source file id, "ref") -> class size; as fid
+ *   sig_rec       key (ns, file id, "sig") -> sig; one record per file
+ * each routed as fdfs_gpu_fdht_route_keys does (key hash, group, server,
+ * records ordered group by group).  file_ids: n records of id_stride bytes
+ * (4-aligned, <= 128), id_len[i] (device, or NULL) bytes of each. */
+typedef struct {
+    uint64_t *index;        /* [n] file of each record */
+    int32_t *key_hash;      /* [n] */
+    uint32_t *group;        /* [n] */
+    uint32_t *server;       /* [n] */
+    uint64_t *order;        /* [n] records group by group, or NULL */
+    uint64_t *group_start;  /* [group_count + 1] */
+} fdfs_gpu_routed;
+
+typedef struct {
+    uint32_t *crc;          /* [n] */
+    uint8_t *sig;           /* [n * 24], 8-aligned */
+    uint64_t *rep;          /* [n] */
+    uint32_t *ref;          /* [n] */
+    uint64_t *nsources;     /* device uint64: records in fid / ref_rec */
+    fdfs_gpu_routed fid, ref_rec, sig_rec;
+} fdfs_gpu_recovery_out;
+
+int fdfs_gpu_recovery_batch(fdfs_gpu_ctx *ctx, const fdfs_gpu_batch *batch, int method,
+                            const uint8_t *file_ids, uint32_t id_stride, const uint32_t *id_len,
+                            const char *ns, int ns_len, uint32_t group_count,
+                            const uint32_t *servers_per_group, fdfs_gpu_recovery_out *out,
+                            void *stream);
 
 /* Scrub: recompute the CRC32 of every file of the batch (as
  * FDFS_SIG_CRC_ONLY) and compare with expected_crc (e.g. from

@@ -155,3 +155,17 @@ def test_dedup_partition_plans(oracle, ctx, n):
     orep, oref = oracle.dedup(sig)
     assert np.array_equal(rep.cpu().numpy(), orep.astype(np.int64))
     assert np.array_equal(ref.cpu().numpy(), oref.astype(np.int32))
+
+
+def test_misaligned_records_rejected(ctx):
+    """Records are read as u64 words: a signature buffer off an 8-byte
+    boundary is EINVAL (0-or-errno convention), never a misaligned read."""
+    import errno
+    from fastdfs_amd import FdfsGpuError
+    buf = torch.zeros(24 * 100 + 8, dtype=torch.uint8, device="cuda")
+    with pytest.raises(FdfsGpuError) as ei:
+        ctx.dedup(buf[1:1 + 24 * 100])
+    assert ei.value.errno == errno.EINVAL
+    with pytest.raises(FdfsGpuError) as ei:
+        ctx.dedup_bucket(buf[4:4 + 24 * 100], None, 2)
+    assert ei.value.errno == errno.EINVAL
