@@ -46,7 +46,7 @@ def parse():
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=10)
     p.add_argument("--warmup", type=int, default=3)
-    p.add_argument("--config", default="c2", choices=["c2", "c3", "c4", "c5"])
+    p.add_argument("--config", default="c2", choices=["c1", "c2", "c3", "c4", "c5"])
     p.add_argument("--files", type=int, default=0, help="override files per GPU")
     p.add_argument("--cpu-seconds", type=float, default=10.0)
     p.add_argument("--cpu-threads", type=int, default=16)
@@ -218,8 +218,19 @@ def main():
            "higher_is_better": True, "vs_baseline": None, "dtype": "u8",
            "data": "synthetic (seeded sizes, random bytes generated in HBM)"}
 
-    if args.config in ("c2", "c3", "c4"):
-        if args.config == "c2":
+    if args.config in ("c1", "c2", "c3", "c4"):
+        if args.config == "c1":
+            # test/test_upload.c:32-39 (DEBUG): 65,560 files / 3,889,152,000 B
+            # of the six gen_files sizes, in a seeded random order
+            mix = [(5 << 10, 50000), (50 << 10, 10000), (200 << 10, 5000), (1 << 20, 500),
+                   (10 << 20, 50), (100 << 20, 10)]
+            sizes = np.concatenate([np.full(c, sz, np.int64) for sz, c in mix])
+            sizes = sizes[np.random.default_rng(1 + 1000 * rank).permutation(sizes.size)]
+            n = sizes.size
+            method, kernel, kname = F.SIG_HASH, _lib.KERNEL_SIG_LANE, "sig_hash_kernel<SAR>"
+            workload = ("config 1: test_upload DEBUG mix (gen_files sizes 5K..100M, 65,560 files), "
+                        "CRC32 + HASH_CODES4 signature + dedup per step")
+        elif args.config == "c2":
             n = args.files or 1_000_000
             sizes = C.small_files_sizes(n, seed=1 + 1000 * rank)
             method, kernel, kname = F.SIG_HASH, _lib.KERNEL_SIG_LANE, "sig_hash_kernel<SAR>"
@@ -284,6 +295,10 @@ def main():
         if rank == 0 and world == 1 and not args.no_cpu_baseline:
             res["cpu_baseline"] = cpu_baseline(data, C.layout(sizes)[0], sizes, method, variant,
                                                args.cpu_seconds, args.cpu_threads)
+            if args.config == "c1":  # one core as well as all of them
+                one = cpu_baseline(data, C.layout(sizes)[0], sizes, method, variant,
+                                   args.cpu_seconds / 2, 1)
+                res["cpu_baseline"]["single_thread"] = {k: one[k] for k in ("value", "unit", "sample")}
         else:
             res["cpu_baseline"] = None
     else:  # c5: dedup only, strong scaling over a fixed 100M-signature set
