@@ -82,6 +82,15 @@ __device__ __forceinline__ void h4_lane(const uint32_t *sD, const Rep8Lane &R8, 
     t = poly_word<33>(t, q.w);
 }
 
+// (a & m) ^ 0x80808080 in one VALU op (v_bitop3_b32, truth table 0x6A):
+// the b - 128 int8 operand of a lane, zero data past the file's end.
+__device__ __forceinline__ uint32_t and_xor80(uint32_t a, uint32_t m)
+{
+    uint32_t r;
+    asm("v_bitop3_b32 %0, %1, %2, %3 bitop3:0x6a" : "=v"(r) : "v"(a), "v"(m), "s"(0x80808080u));
+    return r;
+}
+
 template <bool SAR, int TM, int MODE>
 __global__ __launch_bounds__(TM == 2 ? 1024 : kHashBlock) void sig_hash_kernel(
     const uint8_t *__restrict__ base, const uint64_t *__restrict__ offs,
@@ -182,8 +191,8 @@ __global__ __launch_bounds__(TM == 2 ? 1024 : kHashBlock) void sig_hash_kernel(
                 }
                 // b - 128 as int8 (b ^ 0x80); a padded step is all-zero data
                 const uint32_t msk = ok ? 0xFFFFFFFFu : 0u;
-                const i32x4 A = {(int)((aq.x & msk) ^ 0x80808080u), (int)((aq.y & msk) ^ 0x80808080u),
-                                 (int)((aq.z & msk) ^ 0x80808080u), (int)((aq.w & msk) ^ 0x80808080u)};
+                const i32x4 A = {(int)and_xor80(aq.x, msk), (int)and_xor80(aq.y, msk),
+                                 (int)and_xor80(aq.z, msk), (int)and_xor80(aq.w, msk)};
                 const uint4 b31 = sB[(0 * 8 + q) * 64 + lane], b33 = sB[(1 * 8 + q) * 64 + lane];
                 const i32x4 B31 = {(int)b31.x, (int)b31.y, (int)b31.z, (int)b31.w};
                 const i32x4 B33 = {(int)b33.x, (int)b33.y, (int)b33.z, (int)b33.w};
