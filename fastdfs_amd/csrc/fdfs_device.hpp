@@ -159,76 +159,6 @@ __device__ __forceinline__ void h3_byte(uint32_t b, uint32_t &e, uint32_t &s, ui
     t = lshl_add<5>(t, t) + b;  // 33*t + b
 }
 
-template <bool SAR>
-__device__ __forceinline__ void h3_word(uint32_t w, uint32_t &e, uint32_t &s, uint32_t &t)
-{
-    h3_byte<SAR>(w & 0xFFu, e, s, t);
-    h3_byte<SAR>((w >> 8) & 0xFFu, e, s, t);
-    h3_byte<SAR>((w >> 16) & 0xFFu, e, s, t);
-    h3_byte<SAR>(w >> 24, e, s, t);
-}
-
-// ---- simple_hash / Time33 over 16 bytes at once ------------------------
-// Both are linear recurrences h = m*h + b over Z/2^32 (m = 31 / 33), so
-//   h_16 = m^16 * h_0 + sum_p m^(15-p) * b_p   (mod 2^32).
-// Each coefficient is split into byte planes; plane j of the sum is
-// sum_p byte_j(m^(15-p)) * b_p, four bytes at a time with v_dot4_u32_u8.
-// Planes whose coefficients are all zero are folded away at compile time.
-constexpr uint32_t pow_mod32(uint32_t m, int e)
-{
-    uint32_t r = 1;
-    for (int i = 0; i < e; i++)
-        r *= m;
-    return r;
-}
-
-template <uint32_t M>
-struct Poly16 {
-    // packed[w][j] = bytes k=0..3 of plane j of the coefficients of word w
-    static constexpr uint32_t coef(int w, int j)
-    {
-        uint32_t r = 0;
-        for (int k = 0; k < 4; k++)
-            r |= ((pow_mod32(M, 15 - (4 * w + k)) >> (8 * j)) & 0xFFu) << (8 * k);
-        return r;
-    }
-    static constexpr uint32_t m16 = pow_mod32(M, 16);
-};
-
-template <uint32_t M>
-__device__ __forceinline__ uint32_t poly16_step(uint32_t h, uint4 q)
-{
-    const uint32_t w[4] = {q.x, q.y, q.z, q.w};
-    uint32_t a[4] = {0, 0, 0, 0};
-#pragma unroll
-    for (int j = 0; j < 4; j++)
-#pragma unroll
-        for (int i = 0; i < 4; i++)
-            if (Poly16<M>::coef(i, j) != 0)
-                a[j] = __builtin_amdgcn_udot4(w[i], Poly16<M>::coef(i, j), a[j], false);
-    const uint32_t sum = a[0] + (a[1] << 8) + (a[2] << 16) + (a[3] << 24);
-    return h * Poly16<M>::m16 + sum;
-}
-
-// ELFHash_ex alone (the one hash of CALC_HASH_CODES4 with no parallel form).
-template <bool SAR>
-__device__ __forceinline__ void elf_byte(uint32_t b, uint32_t &e)
-{
-    e = (e << 4) + b;
-    const uint32_t x = e & 0xF0000000u;
-    e ^= SAR ? (uint32_t)((int32_t)x >> 24) : (x >> 24);
-    e &= ~x;
-}
-
-template <bool SAR>
-__device__ __forceinline__ void elf_word(uint32_t w, uint32_t &e)
-{
-    elf_byte<SAR>(w & 0xFFu, e);
-    elf_byte<SAR>((w >> 8) & 0xFFu, e);
-    elf_byte<SAR>((w >> 16) & 0xFFu, e);
-    elf_byte<SAR>(w >> 24, e);
-}
-
 // ---- ELFHash_ex, byte k of word w ------------------------------------------
 // t = (e << 4) + b; e = t ^ ((t >> 24) & ~0xF) (the top nibble is left
 // "dirty": the next step shifts it out).  The exact step also clears the
