@@ -37,6 +37,7 @@ EXPORTS = (
     "fdfs_gpu_fdht_route",
     "fdfs_gpu_fdht_route_keys",
     "fdfs_gpu_recovery_batch",
+    "fdfs_gpu_sig_batch_host",
     "fdfs_gpu_scrub",
     "fdfs_gpu_last_error",
 )
@@ -119,6 +120,8 @@ def load() -> ctypes.CDLL:
     L.fdfs_gpu_recovery_batch.argtypes = [vp, ctypes.POINTER(FdfsGpuBatch), i32, vp, u32, vp,
                                           ctypes.c_char_p, i32, u32, vp,
                                           ctypes.POINTER(FdfsGpuRecoveryOut), vp]
+    L.fdfs_gpu_sig_batch_host.restype = i32
+    L.fdfs_gpu_sig_batch_host.argtypes = [vp, ctypes.POINTER(FdfsGpuBatch), i32, vp, vp, vp, u64]
     L.fdfs_gpu_scrub.restype = i32
     L.fdfs_gpu_scrub.argtypes = [vp, ctypes.POINTER(FdfsGpuBatch), vp, vp, vp, vp, vp]
     L.fdfs_gpu_last_error.restype = ctypes.c_char_p

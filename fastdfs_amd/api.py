@@ -128,6 +128,36 @@ class Context:
         return crc_out, sig_out, codes_out
 
     # ----------------------------------------------------------------- dedup
+    def sig_batch_host(self, data, offsets, sizes, method: int = SIG_HASH, want_sig: bool = True,
+                       want_codes: bool = False, chunk_bytes: int = 0):
+        """fdfs_gpu_sig_batch_host: the batch in HOST memory (numpy arrays or
+        CPU tensors; a pinned tensor copies at the full PCIe rate), streamed
+        to the device in double-buffered windows and hashed there.  Returns
+        numpy (crc uint32[n], sig uint8[n,24] | None, codes int32[n,4] | None)."""
+        import numpy as np
+
+        def host(a, dt):
+            if isinstance(a, torch.Tensor):
+                if a.is_cuda:
+                    raise ValueError("sig_batch_host takes host buffers; use sig_batch for device ones")
+                a = a.numpy()
+            return np.ascontiguousarray(a, dtype=dt)
+        data_h = host(data, np.uint8)
+        offs_h = host(offsets, np.uint64)
+        sizes_h = host(sizes, np.uint64)
+        n = offs_h.size
+        if sizes_h.size != n:
+            raise ValueError("offsets and sizes differ in length")
+        crc = np.zeros(n, np.uint32)
+        sig = np.zeros((n, 24), np.uint8) if (want_sig and method != SIG_CRC_ONLY) else None
+        codes = np.zeros((n, 4), np.int32) if (want_codes and method != SIG_CRC_ONLY) else None
+        b = _lib.FdfsGpuBatch(data_h.ctypes.data, offs_h.ctypes.data, sizes_h.ctypes.data, n)
+        self._rc(self._L.fdfs_gpu_sig_batch_host(self._h, ctypes.byref(b), method, crc.ctypes.data,
+                                                 None if sig is None else sig.ctypes.data,
+                                                 None if codes is None else codes.ctypes.data,
+                                                 chunk_bytes), "fdfs_gpu_sig_batch_host")
+        return crc, sig, codes
+
     def dedup(self, sig: torch.Tensor, gidx: torch.Tensor | None = None, stream=None):
         """rep int64[n] (first ingest index of the class), ref int32[n] (class size)."""
         _check_dev(sig, "sig", torch.uint8)

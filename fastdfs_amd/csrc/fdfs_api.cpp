@@ -305,6 +305,185 @@ int fdfs_gpu_sig_batch(fdfs_gpu_ctx *ctx, const fdfs_gpu_batch *batch, int metho
     return e == hipSuccess ? 0 : fail(ctx, e, "sig_batch launch");
 }
 
+// ---- host-resident batches: chunked, double-buffered H2D / hash / D2H -------
+
+extern "C++" {
+namespace {
+
+struct HostChunk {
+    uint32_t i0, i1;   // files [i0, i1)
+    uint64_t lo, hi;   // host byte window copied for them
+};
+
+// Consecutive files whose byte ranges fit one window of <= chunk bytes (a
+// file larger than that is a chunk alone).  Packed batches (increasing
+// offsets) copy each byte once.
+std::vector<HostChunk> plan_host_chunks(const uint64_t *off, const uint64_t *sz, uint32_t n,
+                                        uint64_t chunk, uint32_t max_files)
+{
+    std::vector<HostChunk> out;
+    uint32_t i = 0;
+    while (i < n) {
+        HostChunk c{i, i + 1, off[i], off[i] + sz[i]};
+        for (uint32_t j = i + 1; j < n && j - i < max_files; j++) {
+            const uint64_t lo = std::min(c.lo, off[j]), hi = std::max(c.hi, off[j] + sz[j]);
+            if (hi - lo > chunk)
+                break;
+            c.lo = lo;
+            c.hi = hi;
+            c.i1 = j + 1;
+        }
+        out.push_back(c);
+        i = c.i1;
+    }
+    return out;
+}
+
+}  // namespace
+}  // extern "C++"
+
+int fdfs_gpu_sig_batch_host(fdfs_gpu_ctx *ctx, const fdfs_gpu_batch *hb, int method,
+                            uint32_t *crc_out, uint8_t *sig_out, int32_t *codes_out,
+                            uint64_t chunk_bytes)
+{
+    if (!ctx || !hb)
+        return EINVAL;
+    if (method != FDFS_SIG_CRC_ONLY && method != FDFS_SIG_HASH && method != FDFS_SIG_MD5)
+        return EINVAL;
+    const uint32_t n = hb->n;
+    if (n == 0)
+        return 0;
+    if (!hb->base || !hb->offset || !hb->size || !crc_out)
+        return EINVAL;
+    if (chunk_bytes == 0)
+        chunk_bytes = 256ull << 20;
+    constexpr uint32_t kMaxChunkFiles = 1u << 20;
+    DeviceGuard g(ctx->device);
+    if (!g.ok)
+        return ENODEV;
+    const auto chunks = plan_host_chunks(hb->offset, hb->size, n, chunk_bytes, kMaxChunkFiles);
+    uint64_t win = 0;
+    uint32_t maxf = 0;
+    for (const auto &c : chunks) {
+        win = std::max(win, c.hi - c.lo);
+        maxf = std::max(maxf, c.i1 - c.i0);
+    }
+    const bool want_sig = method != FDFS_SIG_CRC_ONLY && sig_out;
+    const bool want_codes = method != FDFS_SIG_CRC_ONLY && codes_out;
+    // two device slots: window bytes (16 B slack), offsets, sizes, outputs
+    const size_t slot = align_up(win + 16) + 2 * align_up(8ull * maxf) + align_up(4ull * maxf) +
+                        align_up(24ull * maxf) + align_up(16ull * maxf);
+    int rc = ensure_ws(ctx, sig_ws_bytes(maxf), nullptr);
+    if (rc)
+        return rc;
+    char *dmem = nullptr;
+    uint64_t *hmeta = nullptr;  // pinned offsets/sizes of the two slots
+    char *hres = nullptr;       // pinned results of the two slots (async D2H)
+    const size_t rslot = align_up(4ull * maxf) + align_up(24ull * maxf) + align_up(16ull * maxf);
+    hipStream_t cp = nullptr, cs = nullptr;
+    hipEvent_t copied[2] = {nullptr, nullptr}, done[2] = {nullptr, nullptr};
+    hipError_t e = hipMalloc(&dmem, 2 * slot);
+    if (e == hipSuccess)
+        e = hipHostMalloc(reinterpret_cast<void **>(&hmeta), 2 * 2 * 8ull * maxf, 0);
+    if (e == hipSuccess)
+        e = hipHostMalloc(reinterpret_cast<void **>(&hres), 2 * rslot, 0);
+    // chunk k's results: pinned slot -> the caller's arrays, once it is done
+    auto deliver = [&](size_t k) {
+        const HostChunk &c = chunks[k];
+        const uint32_t m = c.i1 - c.i0;
+        const char *r = hres + (k & 1) * rslot;
+        std::memcpy(crc_out + c.i0, r, 4ull * m);
+        if (want_sig)
+            std::memcpy(sig_out + 24ull * c.i0, r + align_up(4ull * maxf), 24ull * m);
+        if (want_codes)
+            std::memcpy(codes_out + 4ull * c.i0, r + align_up(4ull * maxf) + align_up(24ull * maxf),
+                        16ull * m);
+    };
+    if (e == hipSuccess)
+        e = hipStreamCreateWithFlags(&cp, hipStreamNonBlocking);
+    if (e == hipSuccess)
+        e = hipStreamCreateWithFlags(&cs, hipStreamNonBlocking);
+    for (int k = 0; k < 2 && e == hipSuccess; k++) {
+        e = hipEventCreateWithFlags(&copied[k], hipEventDisableTiming);
+        if (e == hipSuccess)
+            e = hipEventCreateWithFlags(&done[k], hipEventDisableTiming);
+    }
+    const uint8_t *hbase = static_cast<const uint8_t *>(hb->base);
+    for (size_t k = 0; k < chunks.size() && e == hipSuccess; k++) {
+        const HostChunk &c = chunks[k];
+        const uint32_t m = c.i1 - c.i0;
+        char *sl = dmem + (k & 1) * slot;
+        uint8_t *d_data = reinterpret_cast<uint8_t *>(sl);
+        uint64_t *d_off = reinterpret_cast<uint64_t *>(sl + align_up(win + 16));
+        uint64_t *d_sz = d_off + align_up(8ull * maxf) / 8;
+        uint32_t *d_crc = reinterpret_cast<uint32_t *>(reinterpret_cast<char *>(d_sz) + align_up(8ull * maxf));
+        uint8_t *d_sig = reinterpret_cast<uint8_t *>(d_crc) + align_up(4ull * maxf);
+        int32_t *d_codes = reinterpret_cast<int32_t *>(d_sig + align_up(24ull * maxf));
+        uint64_t *h_off = hmeta + (k & 1) * 2 * maxf, *h_sz = h_off + maxf;
+        // the slot is free once chunk k - 2 is hashed and its results are home
+        if (k >= 2) {
+            if ((e = hipEventSynchronize(done[k & 1])) != hipSuccess)
+                break;
+            deliver(k - 2);
+        }
+        char *hr = hres + (k & 1) * rslot;
+        for (uint32_t i = 0; i < m; i++) {  // rebased to the window, which lands 16-aligned
+            h_off[i] = hb->offset[c.i0 + i] - c.lo;
+            h_sz[i] = hb->size[c.i0 + i];
+        }
+        if ((e = hipMemcpyAsync(d_data, hbase + c.lo, c.hi - c.lo, hipMemcpyHostToDevice, cp)) != hipSuccess ||
+            (e = hipMemcpyAsync(d_off, h_off, 8ull * m, hipMemcpyHostToDevice, cp)) != hipSuccess ||
+            (e = hipMemcpyAsync(d_sz, h_sz, 8ull * m, hipMemcpyHostToDevice, cp)) != hipSuccess ||
+            (e = hipEventRecord(copied[k & 1], cp)) != hipSuccess ||
+            (e = hipStreamWaitEvent(cs, copied[k & 1], 0)) != hipSuccess)
+            break;
+        fdfs_gpu_batch b{d_data, d_off, d_sz, m};
+        rc = fdfs_gpu_sig_batch(ctx, &b, method, d_crc, want_sig ? d_sig : nullptr,
+                                want_codes ? d_codes : nullptr, cs);
+        if (rc)
+            break;
+        if ((e = hipMemcpyAsync(hr, d_crc, 4ull * m, hipMemcpyDeviceToHost, cs)) != hipSuccess)
+            break;
+        if (want_sig && (e = hipMemcpyAsync(hr + align_up(4ull * maxf), d_sig, 24ull * m,
+                                            hipMemcpyDeviceToHost, cs)) != hipSuccess)
+            break;
+        if (want_codes && (e = hipMemcpyAsync(hr + align_up(4ull * maxf) + align_up(24ull * maxf),
+                                              d_codes, 16ull * m, hipMemcpyDeviceToHost, cs)) != hipSuccess)
+            break;
+        if ((e = hipEventRecord(done[k & 1], cs)) != hipSuccess)
+            break;
+    }
+    if (cs) {
+        const hipError_t e2 = hipStreamSynchronize(cs);
+        if (e == hipSuccess)
+            e = e2;
+    }
+    if (e == hipSuccess && rc == 0)  // the last two chunks
+        for (size_t k = chunks.size() >= 2 ? chunks.size() - 2 : 0; k < chunks.size(); k++)
+            deliver(k);
+    if (cp)
+        (void)hipStreamSynchronize(cp);
+    for (int k = 0; k < 2; k++) {
+        if (copied[k])
+            (void)hipEventDestroy(copied[k]);
+        if (done[k])
+            (void)hipEventDestroy(done[k]);
+    }
+    if (cs)
+        (void)hipStreamDestroy(cs);
+    if (cp)
+        (void)hipStreamDestroy(cp);
+    if (hmeta)
+        (void)hipHostFree(hmeta);
+    if (hres)
+        (void)hipHostFree(hres);
+    if (dmem)
+        (void)hipFree(dmem);
+    if (rc)
+        return rc;
+    return e == hipSuccess ? 0 : fail(ctx, e, "sig_batch_host");
+}
+
 static int dedup_common(fdfs_gpu_ctx *ctx, const uint8_t *sig, uint32_t stride,
                         const uint64_t *gidx, uint32_t gstride, uint64_t n, uint64_t *rep_out,
                         uint32_t *ref_out, void *stream)

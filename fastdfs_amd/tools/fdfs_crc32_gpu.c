@@ -83,22 +83,11 @@ int main(int argc, char *argv[])
             return e;
         }
     }
-    void *d_data = NULL, *d_offs = NULL, *d_sizes = NULL, *d_crc = NULL;
-    if (hipMalloc(&d_data, total ? total : 16) != hipSuccess ||
-        hipMalloc(&d_offs, n * sizeof(uint64_t)) != hipSuccess ||
-        hipMalloc(&d_sizes, n * sizeof(uint64_t)) != hipSuccess ||
-        hipMalloc(&d_crc, n * sizeof(uint32_t)) != hipSuccess)
-        return ENOMEM;
-    if (hipMemcpy(d_data, host, total, hipMemcpyHostToDevice) != hipSuccess ||
-        hipMemcpy(d_offs, offs, n * sizeof(uint64_t), hipMemcpyHostToDevice) != hipSuccess ||
-        hipMemcpy(d_sizes, sizes, n * sizeof(uint64_t), hipMemcpyHostToDevice) != hipSuccess)
-        return EIO;
-    fdfs_gpu_batch b = {d_data, (const uint64_t *)d_offs, (const uint64_t *)d_sizes, (uint32_t)n};
-    rc = fdfs_gpu_sig_batch(ctx, &b, FDFS_SIG_CRC_ONLY, (uint32_t *)d_crc, NULL, NULL, NULL);
-    if (rc == 0 && hipMemcpy(crc, d_crc, n * sizeof(uint32_t), hipMemcpyDeviceToHost) != hipSuccess)
-        rc = EIO;
+    /* streamed to the device and hashed there (fdfs_gpu_sig_batch_host) */
+    fdfs_gpu_batch b = {host, offs, sizes, (uint32_t)n};
+    rc = fdfs_gpu_sig_batch_host(ctx, &b, FDFS_SIG_CRC_ONLY, crc, NULL, NULL, 0);
     if (rc) {
-        printf("fdfs_gpu_sig_batch fail, errno: %d, error info: %s (%s)\n", rc, strerror(rc),
+        printf("fdfs_gpu_sig_batch_host fail, errno: %d, error info: %s (%s)\n", rc, strerror(rc),
                fdfs_gpu_last_error(ctx));
         return rc;
     }

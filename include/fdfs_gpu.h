@@ -100,6 +100,19 @@ int fdfs_gpu_sig_batch(fdfs_gpu_ctx *ctx, const fdfs_gpu_batch *batch, int metho
                        uint32_t *crc_out, uint8_t *sig_out, int32_t *codes_out,
                        void *stream);
 
+/* The same for a batch in HOST memory (the daemon's receive buffers, the
+ * CLI's files): base/offset/size are host pointers, crc_out / sig_out /
+ * codes_out host arrays.  Files are streamed to the device in windows of at
+ * most chunk_bytes (0 = 256 MiB; a larger file goes alone), double-buffered
+ * on two internal streams: window k+1 crosses PCIe while window k is hashed,
+ * and each window's results come back as soon as they are ready.
+ * Synchronous: returns when every result is in host memory.  A pinned base
+ * (hipHostMalloc / hipHostRegister) copies at the full PCIe rate; batches
+ * with increasing offsets copy each byte once. */
+int fdfs_gpu_sig_batch_host(fdfs_gpu_ctx *ctx, const fdfs_gpu_batch *host_batch, int method,
+                            uint32_t *crc_out, uint8_t *sig_out, int32_t *codes_out,
+                            uint64_t chunk_bytes);
+
 /* Single-GPU duplicate grouping over n records in ingest order.
  *   sig:  device uint8_t[n*24]; gidx: device uint64_t[n] global ingest index
  *         of each record, or NULL for 0..n-1.

@@ -195,3 +195,29 @@ def test_md5_at_scale(oracle, ctxs):
         assert sig_np[i, 8:].tobytes() == hashlib.md5(d.tobytes()).digest(), i
     del data
     torch.cuda.empty_cache()
+
+
+@pytest.mark.parametrize("method", [0, 1, 2])
+def test_host_batch_streamed(oracle, ctxs, method):
+    """fdfs_gpu_sig_batch_host: a host batch streamed in small windows (many
+    chunks, a file larger than the window alone, unaligned starts, a gap)
+    gives the device path's results."""
+    rng = np.random.default_rng(90 + method)
+    sizes = rng.integers(0, 40_000, size=600).astype(np.int64)
+    sizes[[5, 300]] = [300_000, 1 << 20]  # larger than the 256 KiB window
+    offs = np.zeros_like(sizes)
+    offs[1:] = np.cumsum(sizes + rng.integers(0, 7, size=600))[:-1]
+    offs[400:] += 12345  # a gap inside the batch
+    buf = rng.integers(0, 256, size=int(offs[-1] + sizes[-1]) + 1, dtype=np.uint8)
+    crc, sig, codes = ctxs[0].sig_batch_host(buf, offs, sizes, method=method, want_codes=True,
+                                             chunk_bytes=256 << 10)
+    ocrc, osig = oracle.dio_batch(buf, offs, sizes, method, 0, nthreads=8)
+    assert np.array_equal(crc, ocrc)
+    if method:
+        assert np.array_equal(sig, osig)
+    # pinned host memory: the same, one default-size window
+    pinned = torch.from_numpy(buf).pin_memory()
+    crc2, sig2, _ = ctxs[0].sig_batch_host(pinned, offs, sizes, method=method)
+    assert np.array_equal(crc2, ocrc)
+    if method:
+        assert np.array_equal(sig2, osig)
