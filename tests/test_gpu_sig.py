@@ -175,6 +175,19 @@ def test_md5_staged_multiwave(oracle, ctxs):
     _check(oracle, ctxs[0], 0, buf, offs2, sz, methods=(2,))
 
 
+def test_md5_many_chunks(oracle, ctxs):
+    """More 64-file chunks than the MD5 kernel keeps wave pairs resident
+    (150K files = 2344 chunks > 2 x 4 pairs x 256 CUs), so pairs walk a chunk
+    sequence and their LDS handover counters run across chunks; two
+    misaligned files put lane-serial chunks inside those sequences."""
+    rng = np.random.default_rng(32)
+    sizes = rng.integers(0, 2600, 150_000)
+    buf, offs, sz = _packed(sizes, 16, rng, slack=64)
+    offs2 = offs.copy()
+    offs2[[5_000, 140_000]] += 5
+    _check(oracle, ctxs[0], 0, buf, offs2, sz, methods=(2,))
+
+
 def test_md5_at_scale(oracle, ctxs):
     """Config 3 shape (24K photos of 1-4 MiB, ~63 GB in HBM): a random sample
     of files matches the oracle's CRC and MD5 signature bit for bit, and the
