@@ -77,7 +77,7 @@ constexpr int kDpSlotsLog = 11;  // LDS table: 2048 slots
 constexpr int kDpSlots = 1 << kDpSlotsLog;
 constexpr uint32_t kDpCap = kDpSlots * 3 / 4;  // records per partition grouped in LDS
 constexpr uint64_t kDpEmpty = ~0ull;
-constexpr int kDpGroupThreads = 256;
+constexpr int kDpGroupThreads = 512;
 
 struct DpPlan {
     int d1, d2;          // partition bits: top d1 of key32 (K3), next d2 (K4)
@@ -165,18 +165,20 @@ __device__ __forceinline__ void block_scan_bins(const uint32_t *cnt, uint32_t *o
     __syncthreads();
 }
 
-// K3: {key32 << 32 | record, gidx} to its d1 bucket.  The tile is ranked by
-// LDS counters (unstable: order inside a partition does not matter), sorted
-// by digit in LDS and written out as contiguous runs (one run per digit).
+// K3: the 8-byte entry {key32 << 32 | record} to its d1 bucket.  The tile is
+// ranked by LDS counters (unstable: order inside a partition does not
+// matter), sorted by digit in LDS and written out as contiguous runs (one run
+// per digit).  The ingest index is not carried: dp_group reads it only for
+// records of multi-member classes.
 __global__ __launch_bounds__(kDpTileThreads) void dp_scatter_kernel(
-    const uint32_t *__restrict__ keys, const uint64_t *__restrict__ gk, uint64_t n, int d1,
-    uint64_t tiles, const uint64_t *__restrict__ off, ulonglong2 *__restrict__ ent)
+    const uint32_t *__restrict__ keys, uint64_t n, int d1, uint64_t tiles,
+    const uint64_t *__restrict__ off, uint64_t *__restrict__ ent)
 {
     __shared__ uint32_t cnt[1 << kDpMaxD1];
     __shared__ uint32_t lst[1 << kDpMaxD1];
     __shared__ uint64_t bas[1 << kDpMaxD1];
     __shared__ uint32_t wsum[kDpTileThreads / 64];
-    __shared__ ulonglong2 stage[kDpTile];
+    __shared__ uint64_t stage[kDpTile];
     const uint32_t nb = 1u << d1;
     for (uint32_t k = threadIdx.x; k < nb; k += blockDim.x) {
         cnt[k] = 0;
@@ -200,13 +202,12 @@ __global__ __launch_bounds__(kDpTileThreads) void dp_scatter_kernel(
     for (int it = 0; it < kDpTileItems; it++) {
         const uint32_t l = it * kDpTileThreads + threadIdx.x;
         if (l < m)
-            stage[lst[key[it] >> (32 - d1)] + rank[it]] =
-                make_ulonglong2(((uint64_t)key[it] << 32) | (uint32_t)(t0 + l), gk[t0 + l]);
+            stage[lst[key[it] >> (32 - d1)] + rank[it]] = ((uint64_t)key[it] << 32) | (uint32_t)(t0 + l);
     }
     __syncthreads();
     for (uint32_t j = threadIdx.x; j < m; j += blockDim.x) {
-        const ulonglong2 en = stage[j];
-        const uint32_t d = (uint32_t)(en.x >> (64 - d1));
+        const uint64_t en = stage[j];
+        const uint32_t d = (uint32_t)(en >> (64 - d1));
         ent[bas[d] + (j - lst[d])] = en;
     }
 }
@@ -220,8 +221,8 @@ constexpr int kDpSplitPer = 4;  // entries per thread per chunk
 constexpr int kDpChunk = kDpSplitThreads * kDpSplitPer;
 
 __global__ __launch_bounds__(kDpSplitThreads) void dp_split_kernel(
-    const ulonglong2 *__restrict__ ent, uint64_t n, int d1, int d2, uint64_t tiles,
-    const uint64_t *__restrict__ off, ulonglong2 *__restrict__ ent2, uint32_t *__restrict__ pstart)
+    const uint64_t *__restrict__ ent, uint64_t n, int d1, int d2, uint64_t tiles,
+    const uint64_t *__restrict__ off, uint64_t *__restrict__ ent2, uint32_t *__restrict__ pstart)
 {
     constexpr int NB = 1 << kDpMaxD2;
     constexpr int PER = NB / kDpSplitThreads;
@@ -229,7 +230,7 @@ __global__ __launch_bounds__(kDpSplitThreads) void dp_split_kernel(
     __shared__ uint32_t cc[NB];   // chunk counts
     __shared__ uint32_t cl[NB];   // chunk-local starts
     __shared__ uint32_t wsum[kDpSplitThreads / 64];
-    __shared__ ulonglong2 stage[kDpChunk];
+    __shared__ uint64_t stage[kDpChunk];
     const uint32_t nd2 = 1u << d2;
     const uint64_t s = off[(uint64_t)blockIdx.x * tiles];
     const uint64_t e = (blockIdx.x + 1 == (1u << d1)) ? n : off[(uint64_t)(blockIdx.x + 1) * tiles];
@@ -238,7 +239,7 @@ __global__ __launch_bounds__(kDpSplitThreads) void dp_split_kernel(
         h[k] = 0;
     __syncthreads();
     for (uint64_t i = s + threadIdx.x; i < e; i += blockDim.x)
-        atomicAdd(&h[(uint32_t)(ent[i].x >> sh) & (nd2 - 1)], 1u);
+        atomicAdd(&h[(uint32_t)(ent[i] >> sh) & (nd2 - 1)], 1u);
     __syncthreads();
     block_scan_bins<PER, kDpSplitThreads>(h, h, nd2, wsum);
     for (uint32_t k = threadIdx.x; k < nd2; k += blockDim.x)
@@ -250,14 +251,14 @@ __global__ __launch_bounds__(kDpSplitThreads) void dp_split_kernel(
         for (uint32_t k = threadIdx.x; k < nd2; k += blockDim.x)
             cc[k] = 0;
         __syncthreads();
-        ulonglong2 en[kDpSplitPer];
+        uint64_t en[kDpSplitPer];
         uint32_t rk[kDpSplitPer];
 #pragma unroll
         for (int q = 0; q < kDpSplitPer; q++) {
             const uint32_t l = q * kDpSplitThreads + threadIdx.x;
             if (l < m) {
                 en[q] = ent[c0 + l];
-                rk[q] = atomicAdd(&cc[(uint32_t)(en[q].x >> sh) & (nd2 - 1)], 1u);
+                rk[q] = atomicAdd(&cc[(uint32_t)(en[q] >> sh) & (nd2 - 1)], 1u);
             }
         }
         __syncthreads();
@@ -266,12 +267,12 @@ __global__ __launch_bounds__(kDpSplitThreads) void dp_split_kernel(
         for (int q = 0; q < kDpSplitPer; q++) {
             const uint32_t l = q * kDpSplitThreads + threadIdx.x;
             if (l < m)
-                stage[cl[(uint32_t)(en[q].x >> sh) & (nd2 - 1)] + rk[q]] = en[q];
+                stage[cl[(uint32_t)(en[q] >> sh) & (nd2 - 1)] + rk[q]] = en[q];
         }
         __syncthreads();
         for (uint32_t j = threadIdx.x; j < m; j += blockDim.x) {
-            const ulonglong2 v = stage[j];
-            const uint32_t d = (uint32_t)(v.x >> sh) & (nd2 - 1);
+            const uint64_t v = stage[j];
+            const uint32_t d = (uint32_t)(v >> sh) & (nd2 - 1);
             ent2[s + h[d] + (j - cl[d])] = v;
         }
         __syncthreads();
@@ -292,43 +293,78 @@ __global__ void dp_starts_kernel(const uint64_t *__restrict__ off, uint64_t n, i
         pstart[1u << d1] = (uint32_t)n;
 }
 
-// Insert entry i (record r, key) into an open-addressing table of `size`
-// slots (power of two when MASKED, else any size): claim by CAS of
-// {key, i - base}; an equal key is confirmed on the full signature against
-// the claimer's record.  Returns the slot.
-template <bool MASKED>
-__device__ __forceinline__ uint32_t dp_insert(uint64_t *word, uint32_t size, uint32_t key,
-                                              uint32_t local, uint32_t r, const ulonglong2 *ent,
-                                              uint64_t base, const uint8_t *sig, uint32_t stride)
+// Open-addressing tables (LDS or a partition's HBM region) hold one 64-bit
+// word per slot: {key32, claimer record}, set once by CAS and never changed.
+__device__ __forceinline__ uint32_t dp_home(uint32_t key, uint32_t size, bool masked)
 {
-    uint32_t slot = MASKED ? ((key * 0x9E3779B1u) >> (32 - kDpSlotsLog))
-                           : (uint32_t)(((uint64_t)(key * 0x9E3779B1u) * size) >> 32);
-    const uint64_t mine = ((uint64_t)key << 32) | local;
+    return masked ? ((key * 0x9E3779B1u) >> (32 - kDpSlotsLog))
+                  : (uint32_t)(((uint64_t)(key * 0x9E3779B1u) * size) >> 32);
+}
+
+__device__ __forceinline__ uint32_t dp_next(uint32_t slot, uint32_t size, bool masked)
+{
+    return masked ? ((slot + 1) & (kDpSlots - 1)) : (slot + 1 == size ? 0 : slot + 1);
+}
+
+// Key-only probe from `slot`: claim the first empty slot, or stop at the
+// first slot whose key equals ours.  Returns the slot; `owner` = its claimer
+// (r itself when this record claimed it).  Equal keys still need the
+// full-signature check (dp_insert continues past a mismatch).
+template <bool MASKED>
+__device__ __forceinline__ uint32_t dp_probe(uint64_t *word, uint32_t size, uint32_t key, uint32_t r,
+                                             uint32_t slot, uint32_t &owner)
+{
+    const uint64_t mine = ((uint64_t)key << 32) | r;
     for (;;) {
         uint64_t cur = word[slot];
         if (cur == kDpEmpty) {
             cur = atomicCAS(reinterpret_cast<unsigned long long *>(&word[slot]), kDpEmpty, mine);
-            if (cur == kDpEmpty)
+            if (cur == kDpEmpty) {
+                owner = r;
                 return slot;  // claimed
+            }
         }
         if ((uint32_t)(cur >> 32) == key) {
-            const uint32_t owner = (uint32_t)ent[base + (uint32_t)cur].x;
-            if (sig_equal(sig, stride, r, owner))
-                return slot;
+            owner = (uint32_t)cur;
+            return slot;
         }
-        slot = MASKED ? ((slot + 1) & (kDpSlots - 1)) : (slot + 1 == size ? 0 : slot + 1);
+        slot = dp_next(slot, size, MASKED);
     }
 }
 
+// Full insert from `slot`: probe, confirm an equal key on the 24 bytes, walk
+// on past a key collision with a different signature.
+template <bool MASKED>
+__device__ __forceinline__ uint32_t dp_insert(uint64_t *word, uint32_t size, uint32_t key, uint32_t r,
+                                              uint32_t slot, const uint8_t *sig, uint32_t stride,
+                                              uint32_t &owner)
+{
+    for (;;) {
+        slot = dp_probe<MASKED>(word, size, key, r, slot, owner);
+        if (owner == r || sig_equal(sig, stride, r, owner))
+            return slot;
+        slot = dp_next(slot, size, MASKED);
+    }
+}
+
+__device__ __forceinline__ uint64_t gidx_of(const uint64_t *gidx, uint32_t gstride, uint32_t r)
+{
+    return gstride ? gidx[(uint64_t)r * gstride] : (uint64_t)r;
+}
+
 // Only records of classes with more than one member are written (random
-// stores); K1 already wrote every record's singleton answer.
+// stores); K1 already wrote every record's singleton answer.  The class
+// minimum needs ingest indices only there: every member that joined a
+// claimed slot folds min(own, claimer's) into the slot, so a class of k > 1
+// members gets all k indices and a singleton reads none.
 constexpr int kDpEpt = (kDpCap + kDpGroupThreads - 1) / kDpGroupThreads;  // entries per thread
 
-__global__ __launch_bounds__(kDpGroupThreads) void dp_group_kernel(
-    const ulonglong2 *__restrict__ ent, const uint32_t *__restrict__ pstart,
-    const uint8_t *__restrict__ sig, uint32_t stride, uint64_t *__restrict__ gword,
-    uint64_t *__restrict__ gmin, uint32_t *__restrict__ gcnt, uint32_t *__restrict__ gslot,
-    uint64_t *__restrict__ rep_out, uint32_t *__restrict__ ref_out)
+__global__ __launch_bounds__(kDpGroupThreads) __attribute__((amdgpu_waves_per_eu(8))) void dp_group_kernel(
+    const uint64_t *__restrict__ ent, const uint32_t *__restrict__ pstart,
+    const uint8_t *__restrict__ sig, uint32_t stride, const uint64_t *__restrict__ gidx,
+    uint32_t gstride, uint64_t *__restrict__ gword, uint64_t *__restrict__ gmin,
+    uint32_t *__restrict__ gcnt, uint32_t *__restrict__ gslot, uint64_t *__restrict__ rep_out,
+    uint32_t *__restrict__ ref_out)
 {
     __shared__ uint64_t word[kDpSlots];
     __shared__ uint64_t mn[kDpSlots];
@@ -339,11 +375,11 @@ __global__ __launch_bounds__(kDpGroupThreads) void dp_group_kernel(
         return;
     if (cnt <= kDpCap) {
         // all of this thread's entries in flight at once
-        ulonglong2 en[kDpEpt];
+        uint64_t en[kDpEpt];
 #pragma unroll
         for (int k = 0; k < kDpEpt; k++) {
             const uint32_t l = threadIdx.x + k * kDpGroupThreads;
-            en[k] = l < cnt ? ent[s + l] : make_ulonglong2(0, 0);
+            en[k] = l < cnt ? ent[s + l] : 0ull;
         }
         for (int k = threadIdx.x; k < kDpSlots; k += blockDim.x) {
             word[k] = kDpEmpty;
@@ -351,16 +387,48 @@ __global__ __launch_bounds__(kDpGroupThreads) void dp_group_kernel(
             cn[k] = 0;
         }
         __syncthreads();
-        uint32_t slot[kDpEpt];
+        // (1) key-only probes: LDS only
+        uint32_t slot[kDpEpt], own[kDpEpt];
+#pragma unroll
+        for (int k = 0; k < kDpEpt; k++) {
+            const uint32_t l = threadIdx.x + k * kDpGroupThreads;
+            own[k] = (uint32_t)en[k];
+            if (l < cnt) {
+                const uint32_t key = (uint32_t)(en[k] >> 32);
+                slot[k] = dp_probe<true>(word, kDpSlots, key, (uint32_t)en[k], dp_home(key, kDpSlots, true),
+                                         own[k]);
+            }
+        }
+        // (2) confirmations of every joined entry issued together: both
+        // signature rows and both ingest indices per entry
+        uint64_t ra[kDpEpt], rb[kDpEpt], rc[kDpEpt], oa[kDpEpt], ob[kDpEpt], oc[kDpEpt];
+        uint64_t gr[kDpEpt], go[kDpEpt];
+#pragma unroll
+        for (int k = 0; k < kDpEpt; k++) {
+            const uint32_t r = (uint32_t)en[k];
+            if (own[k] != r) {
+                load_sig(sig + (uint64_t)r * stride, ra[k], rb[k], rc[k]);
+                load_sig(sig + (uint64_t)own[k] * stride, oa[k], ob[k], oc[k]);
+                gr[k] = gidx_of(gidx, gstride, r);
+                go[k] = gidx_of(gidx, gstride, own[k]);
+            }
+        }
 #pragma unroll
         for (int k = 0; k < kDpEpt; k++) {
             const uint32_t l = threadIdx.x + k * kDpGroupThreads;
             if (l < cnt) {
-                slot[k] = dp_insert<true>(word, kDpSlots, (uint32_t)(en[k].x >> 32), l,
-                                          (uint32_t)en[k].x, ent, s, sig, stride);
-                atomicMin(reinterpret_cast<unsigned long long *>(&mn[slot[k]]),
-                          (unsigned long long)en[k].y);
+                const uint32_t r = (uint32_t)en[k];
+                if (own[k] != r && !(ra[k] == oa[k] && rb[k] == ob[k] && rc[k] == oc[k])) {
+                    // 32-bit key collision with a different signature: walk on
+                    slot[k] = dp_insert<true>(word, kDpSlots, (uint32_t)(en[k] >> 32), r,
+                                              dp_next(slot[k], kDpSlots, true), sig, stride, own[k]);
+                    if (own[k] != r)
+                        go[k] = gidx_of(gidx, gstride, own[k]);
+                }
                 atomicAdd(&cn[slot[k]], 1u);
+                if (own[k] != r)
+                    atomicMin(reinterpret_cast<unsigned long long *>(&mn[slot[k]]),
+                              (unsigned long long)(gr[k] < go[k] ? gr[k] : go[k]));
             }
         }
         __syncthreads();
@@ -370,7 +438,7 @@ __global__ __launch_bounds__(kDpGroupThreads) void dp_group_kernel(
             if (l < cnt) {
                 const uint32_t c = cn[slot[k]];
                 if (c > 1) {
-                    const uint32_t r = (uint32_t)en[k].x;
+                    const uint32_t r = (uint32_t)en[k];
                     rep_out[r] = mn[slot[k]];
                     ref_out[r] = c;
                 }
@@ -391,18 +459,22 @@ __global__ __launch_bounds__(kDpGroupThreads) void dp_group_kernel(
     }
     __syncthreads();
     for (uint32_t l = threadIdx.x; l < cnt; l += blockDim.x) {
-        const ulonglong2 en = ent[s + l];
-        const uint32_t slot = dp_insert<false>(w, size, (uint32_t)(en.x >> 32), l, (uint32_t)en.x, ent,
-                                               s, sig, stride);
-        atomicMin(reinterpret_cast<unsigned long long *>(&m[slot]), (unsigned long long)en.y);
+        const uint64_t en = ent[s + l];
+        const uint32_t r = (uint32_t)en, key = (uint32_t)(en >> 32);
+        uint32_t o;
+        const uint32_t slot = dp_insert<false>(w, size, key, r, dp_home(key, size, false), sig, stride, o);
         atomicAdd(&c[slot], 1u);
+        if (o != r) {
+            const uint64_t a = gidx_of(gidx, gstride, r), b = gidx_of(gidx, gstride, o);
+            atomicMin(reinterpret_cast<unsigned long long *>(&m[slot]), (unsigned long long)(a < b ? a : b));
+        }
         gslot[s + l] = slot;
     }
     __syncthreads();
     for (uint32_t l = threadIdx.x; l < cnt; l += blockDim.x) {
         const uint32_t slot = gslot[s + l];
         if (c[slot] > 1) {
-            const uint32_t r = (uint32_t)ent[s + l].x;
+            const uint32_t r = (uint32_t)ent[s + l];
             rep_out[r] = m[slot];
             ref_out[r] = c[slot];
         }
@@ -417,7 +489,7 @@ uint64_t dedup_ws_bytes(uint64_t n)
     const DpPlan pl = dp_plan(n);
     const uint64_t ncnt = (1ull << pl.d1) * pl.tiles;
     return al(4 * n) + al(8 * n) + al(8 * (ncnt + 1)) + al(8 * (ncnt + 1)) +
-           al(8 * scan_workspace_elems(ncnt)) + al(16 * n) + al(16 * n) + al(4 * (pl.nparts() + 1)) +
+           al(8 * scan_workspace_elems(ncnt)) + al(8 * n) + al(8 * n) + al(4 * (pl.nparts() + 1)) +
            al(16 * n) + al(16 * n);
 }
 
@@ -447,8 +519,8 @@ hipError_t launch_dedup_group(const uint8_t *sig, uint32_t sig_stride, const uin
     uint64_t *counts = reinterpret_cast<uint64_t *>(take(8 * (ncnt + 1)));
     uint64_t *off = reinterpret_cast<uint64_t *>(take(8 * (ncnt + 1)));
     uint64_t *bsum = reinterpret_cast<uint64_t *>(take(8 * scan_workspace_elems(ncnt)));
-    ulonglong2 *ent = reinterpret_cast<ulonglong2 *>(take(16 * n));
-    ulonglong2 *ent2 = reinterpret_cast<ulonglong2 *>(take(16 * n));
+    uint64_t *ent = reinterpret_cast<uint64_t *>(take(8 * n));
+    uint64_t *ent2 = reinterpret_cast<uint64_t *>(take(8 * n));
     uint32_t *pstart = reinterpret_cast<uint32_t *>(take(4 * (pl.nparts() + 1)));
     uint64_t *gword = reinterpret_cast<uint64_t *>(take(16 * n));  // oversized-partition tables
     uint64_t *gmin = reinterpret_cast<uint64_t *>(take(16 * n));
@@ -462,9 +534,8 @@ hipError_t launch_dedup_group(const uint8_t *sig, uint32_t sig_stride, const uin
                                                                   counts);
     if ((e = launch_exclusive_scan(counts, ncnt, off, bsum, st)) != hipSuccess)
         return e;
-    dp_scatter_kernel<<<(unsigned)pl.tiles, kDpTileThreads, 0, st>>>(keys, rep_out, n, pl.d1, pl.tiles, off,
-                                                                     ent);
-    const ulonglong2 *parts = ent;
+    dp_scatter_kernel<<<(unsigned)pl.tiles, kDpTileThreads, 0, st>>>(keys, n, pl.d1, pl.tiles, off, ent);
+    const uint64_t *parts = ent;
     if (pl.d2) {
         dp_split_kernel<<<1u << pl.d1, kDpSplitThreads, 0, st>>>(ent, n, pl.d1, pl.d2, pl.tiles, off,
                                                                   ent2, pstart);
@@ -473,7 +544,7 @@ hipError_t launch_dedup_group(const uint8_t *sig, uint32_t sig_stride, const uin
         dp_starts_kernel<<<((1u << pl.d1) + 255) / 256, 256, 0, st>>>(off, n, pl.d1, pl.tiles, pstart);
     }
     dp_group_kernel<<<(unsigned)pl.nparts(), kDpGroupThreads, 0, st>>>(
-        parts, pstart, sig, sig_stride, gword, gmin, gcnt, gslot, rep_out, ref_out);
+        parts, pstart, sig, sig_stride, gidx, gidx_stride, gword, gmin, gcnt, gslot, rep_out, ref_out);
     if (ev1)
         (void)hipEventRecord(ev1, st);
     return hipGetLastError();
