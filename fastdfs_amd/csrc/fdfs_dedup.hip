@@ -347,11 +347,14 @@ __device__ __forceinline__ uint32_t dp_insert(uint64_t *word, uint32_t size, uin
     }
 }
 
-__device__ __forceinline__ uint64_t gidx_of(const uint64_t *gidx, uint32_t gstride, uint32_t r)
+// A record's ingest index, from its own rep_out slot (dp_keys wrote
+// gidx[r] there): the multi-member records read here are the ones whose
+// rep_out line is written at the end, so the read brings in the line the
+// random store lands on instead of touching a third array.
+__device__ __forceinline__ uint64_t gidx_of(const uint64_t *rep, uint32_t gstride, uint32_t r)
 {
-    return gstride ? gidx[(uint64_t)r * gstride] : (uint64_t)r;
+    return gstride ? rep[r] : (uint64_t)r;
 }
-
 // Only records of classes with more than one member are written (random
 // stores); K1 already wrote every record's singleton answer.  The class
 // minimum needs ingest indices only there: every member that joined a
@@ -361,8 +364,7 @@ constexpr int kDpEpt = (kDpCap + kDpGroupThreads - 1) / kDpGroupThreads;  // ent
 
 __global__ __launch_bounds__(kDpGroupThreads) __attribute__((amdgpu_waves_per_eu(8))) void dp_group_kernel(
     const uint64_t *__restrict__ ent, const uint32_t *__restrict__ pstart,
-    const uint8_t *__restrict__ sig, uint32_t stride, const uint64_t *__restrict__ gidx,
-    uint32_t gstride, uint64_t *__restrict__ gword, uint64_t *__restrict__ gmin,
+    const uint8_t *__restrict__ sig, uint32_t stride, uint32_t gstride, uint64_t *__restrict__ gword, uint64_t *__restrict__ gmin,
     uint32_t *__restrict__ gcnt, uint32_t *__restrict__ gslot, uint64_t *__restrict__ rep_out,
     uint32_t *__restrict__ ref_out)
 {
@@ -409,8 +411,8 @@ __global__ __launch_bounds__(kDpGroupThreads) __attribute__((amdgpu_waves_per_eu
             if (own[k] != r) {
                 load_sig(sig + (uint64_t)r * stride, ra[k], rb[k], rc[k]);
                 load_sig(sig + (uint64_t)own[k] * stride, oa[k], ob[k], oc[k]);
-                gr[k] = gidx_of(gidx, gstride, r);
-                go[k] = gidx_of(gidx, gstride, own[k]);
+                gr[k] = gidx_of(rep_out, gstride, r);
+                go[k] = gidx_of(rep_out, gstride, own[k]);
             }
         }
 #pragma unroll
@@ -423,7 +425,7 @@ __global__ __launch_bounds__(kDpGroupThreads) __attribute__((amdgpu_waves_per_eu
                     slot[k] = dp_insert<true>(word, kDpSlots, (uint32_t)(en[k] >> 32), r,
                                               dp_next(slot[k], kDpSlots, true), sig, stride, own[k]);
                     if (own[k] != r)
-                        go[k] = gidx_of(gidx, gstride, own[k]);
+                        go[k] = gidx_of(rep_out, gstride, own[k]);
                 }
                 atomicAdd(&cn[slot[k]], 1u);
                 if (own[k] != r)
@@ -465,7 +467,7 @@ __global__ __launch_bounds__(kDpGroupThreads) __attribute__((amdgpu_waves_per_eu
         const uint32_t slot = dp_insert<false>(w, size, key, r, dp_home(key, size, false), sig, stride, o);
         atomicAdd(&c[slot], 1u);
         if (o != r) {
-            const uint64_t a = gidx_of(gidx, gstride, r), b = gidx_of(gidx, gstride, o);
+            const uint64_t a = gidx_of(rep_out, gstride, r), b = gidx_of(rep_out, gstride, o);
             atomicMin(reinterpret_cast<unsigned long long *>(&m[slot]), (unsigned long long)(a < b ? a : b));
         }
         gslot[s + l] = slot;
@@ -544,7 +546,7 @@ hipError_t launch_dedup_group(const uint8_t *sig, uint32_t sig_stride, const uin
         dp_starts_kernel<<<((1u << pl.d1) + 255) / 256, 256, 0, st>>>(off, n, pl.d1, pl.tiles, pstart);
     }
     dp_group_kernel<<<(unsigned)pl.nparts(), kDpGroupThreads, 0, st>>>(
-        parts, pstart, sig, sig_stride, gidx, gidx_stride, gword, gmin, gcnt, gslot, rep_out, ref_out);
+        parts, pstart, sig, sig_stride, gidx_stride, gword, gmin, gcnt, gslot, rep_out, ref_out);
     if (ev1)
         (void)hipEventRecord(ev1, st);
     return hipGetLastError();
