@@ -65,9 +65,11 @@ __device__ __forceinline__ uint32_t crc16(const uint32_t *sD, const Rep8Lane &R8
 
 template <bool SAR, int TM>
 __device__ __forceinline__ void h4_lane(const uint32_t *sD, const Rep8Lane &R8, uint32_t K16,
-                                        uint4 q, uint32_t &c, uint32_t &e, uint32_t &s, uint32_t &t)
+                                        uint4 q, bool do_crc, uint32_t &c, uint32_t &e, uint32_t &s,
+                                        uint32_t &t)
 {
-    c = crc16<SAR, TM>(sD, R8, K16, c, q);
+    if (do_crc)
+        c = crc16<SAR, TM>(sD, R8, K16, c, q);
     elf_word4<SAR, false>(q.x, e);
     elf_word4<SAR, false>(q.y, e);
     elf_word4<SAR, false>(q.z, e);
@@ -95,7 +97,7 @@ template <bool SAR, int TM, int MODE>
 __global__ __launch_bounds__(TM == 2 ? 1024 : kHashBlock) void sig_hash_kernel(
     const uint8_t *__restrict__ base, const uint64_t *__restrict__ offs,
     const uint64_t *__restrict__ sizes, const uint32_t *__restrict__ order, uint32_t n,
-    const DevTables *__restrict__ tabs, uint32_t *__restrict__ crc_out,
+    const DevTables *__restrict__ tabs, uint64_t big_min, uint32_t *__restrict__ crc_out,
     uint8_t *__restrict__ sig_out, int32_t *__restrict__ codes_out)
 {
     __shared__ uint32_t sD[TM == 2 ? kRep8Dwords : 16 * 256];
@@ -124,6 +126,12 @@ __global__ __launch_bounds__(TM == 2 ? 1024 : kHashBlock) void sig_hash_kernel(
     const uint8_t *p = valid ? base + offs[f] : safe;
     uint32_t c = 0xFFFFFFFFu;  // CRC32_XINIT (storage/storage_service.c:7149)
     uint32_t e = 0, s = 0, t = 0;  // INIT_HASH_CODES4 (storage/storage_service.c:7156)
+    // Files of >= big_min bytes leave their CRC to the segmented kernel
+    // (launch_sig_lane runs it before this one and patches the outputs
+    // after): their waves are few and issue-bound, the CRC is ~30% of their
+    // instructions, and once a wave's smaller files have ended its CRC
+    // blocks run with an empty exec mask and are branched over.
+    const bool do_crc = L < big_min;
 
     // bytes to 16-byte alignment, then vectors to 128-byte alignment (lane-serial)
     uint64_t head = (16u - ((uintptr_t)p & 15u)) & 15u;
@@ -131,7 +139,8 @@ __global__ __launch_bounds__(TM == 2 ? 1024 : kHashBlock) void sig_hash_kernel(
         head = L;
     for (uint64_t k = 0; k < head; k++) {
         const uint32_t b = p[k];
-        c = crc_byte<SAR>(sT, c, b);
+        if (do_crc)
+            c = crc_byte<SAR>(sT, c, b);
         h3_byte<SAR>(b, e, s, t);
     }
     const uint4 *v = reinterpret_cast<const uint4 *>(p + head);
@@ -140,7 +149,7 @@ __global__ __launch_bounds__(TM == 2 ? 1024 : kHashBlock) void sig_hash_kernel(
     if (lead > nvec)
         lead = nvec;
     for (uint64_t j = 0; j < lead; j++)
-        h4_lane<SAR, TM>(sD, R8, K16, v[j], c, e, s, t);
+        h4_lane<SAR, TM>(sD, R8, K16, v[j], do_crc, c, e, s, t);
 
     // whole 128-byte lines: the wave steps in lockstep to its longest file
     const uint32_t nsteps = (uint32_t)((nvec - lead) >> 3);
@@ -183,7 +192,8 @@ __global__ __launch_bounds__(TM == 2 ? 1024 : kHashBlock) void sig_hash_kernel(
                     continue;
                 }
                 if (ok) {
-                    c = crc16<SAR, TM>(sD, R8, K16, c, aq);
+                    if (do_crc)
+                        c = crc16<SAR, TM>(sD, R8, K16, c, aq);
                     elf_word4<SAR, false>(aq.x, e);
                     elf_word4<SAR, false>(aq.y, e);
                     elf_word4<SAR, false>(aq.z, e);
@@ -252,16 +262,18 @@ __global__ __launch_bounds__(TM == 2 ? 1024 : kHashBlock) void sig_hash_kernel(
     }
 
     for (uint64_t jv = lead + 8 * (uint64_t)nsteps; jv < nvec; jv++)
-        h4_lane<SAR, TM>(sD, R8, K16, v[jv], c, e, s, t);
+        h4_lane<SAR, TM>(sD, R8, K16, v[jv], do_crc, c, e, s, t);
     for (uint64_t k = head + (nvec << 4); k < L; k++) {  // the last (L - head) & 15 bytes
         const uint32_t b = p[k];
-        c = crc_byte<SAR>(sT, c, b);
+        if (do_crc)
+            c = crc_byte<SAR>(sT, c, b);
         h3_byte<SAR>(b, e, s, t);
     }
     if (!valid)
         return;
     c ^= 0xFFFFFFFFu;  // CRC32_FINAL / FINISH_HASH_CODES4 (storage/storage_dio.c:500,508)
-    crc_out[f] = c;
+    if (do_crc)
+        crc_out[f] = c;  // else big_patch_kernel puts the segmented CRC in all three outputs
     if (sig_out) {  // STORAGE_GEN_FILE_SIGNATURE (storage/storage_service.c:106-120)
         uint2 *sp = reinterpret_cast<uint2 *>(sig_out + 24ull * f);
         sp[0] = make_uint2(bswap32((uint32_t)(L >> 32)), bswap32((uint32_t)L));
@@ -274,7 +286,7 @@ __global__ __launch_bounds__(TM == 2 ? 1024 : kHashBlock) void sig_hash_kernel(
 
 hipError_t launch_sig_hash(bool sar, const uint8_t *base, const uint64_t *offs,
                            const uint64_t *sizes, uint32_t n, const uint32_t *order,
-                           const DevTables *tabs, uint32_t *crc_out, uint8_t *sig_out,
+                           const DevTables *tabs, uint64_t big_min, uint32_t *crc_out, uint8_t *sig_out,
                            int32_t *codes_out, hipStream_t st)
 {
     static int mode = -1;
@@ -292,10 +304,10 @@ hipError_t launch_sig_hash(bool sar, const uint8_t *base, const uint64_t *offs,
 #define HASH_LAUNCH(S, M)                                                                                \
     do {                                                                                                 \
         if (tm == 2)                                                                                     \
-            sig_hash_kernel<S, 2, M><<<grid, blk, 0, st>>>(base, offs, sizes, order, n, tabs, crc_out,   \
+            sig_hash_kernel<S, 2, M><<<grid, blk, 0, st>>>(base, offs, sizes, order, n, tabs, big_min, crc_out, \
                                                            sig_out, codes_out);                          \
         else                                                                                             \
-            sig_hash_kernel<S, 0, M><<<grid, blk, 0, st>>>(base, offs, sizes, order, n, tabs, crc_out,   \
+            sig_hash_kernel<S, 0, M><<<grid, blk, 0, st>>>(base, offs, sizes, order, n, tabs, big_min, crc_out, \
                                                            sig_out, codes_out);                          \
     } while (0)
     if (mode == 1)

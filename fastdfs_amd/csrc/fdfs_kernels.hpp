@@ -16,10 +16,19 @@ constexpr int kLaneWsDwords = 2 * kSizeBins;  // size-bin histogram + cursors
 uint64_t scan_workspace_elems(uint64_t n);
 hipError_t launch_exclusive_scan(const uint64_t *in, uint64_t n, uint64_t *out, uint64_t *bsum,
                                  hipStream_t st);
+// HASH method: files of at least kBigCrcMin bytes get their CRC from the
+// segmented kernel (a wave of such files is issue-bound, see fdfs_hash.hip).
+constexpr uint64_t kBigCrcMin = 4ull << 20;
+struct BigCrcWs {  // device arrays of n entries (seg_first n + 1)
+    uint32_t *nbig;
+    uint64_t *offs, *sizes, *seg_first;
+    uint32_t *crc;
+};
 hipError_t launch_sig_lane(bool sar, int method, const uint8_t *base, const uint64_t *offs,
                            const uint64_t *sizes, uint32_t n, uint32_t *hist, uint32_t *order,
-                           const DevTables *tabs, uint32_t *crc_out, uint8_t *sig_out,
-                           int32_t *codes_out, hipStream_t st, hipEvent_t ev0, hipEvent_t ev1);
+                           const BigCrcWs *big, const DevTables *tabs, uint32_t *crc_out,
+                           uint8_t *sig_out, int32_t *codes_out, unsigned seg_grid, hipStream_t st,
+                           hipEvent_t ev0, hipEvent_t ev1);
 hipError_t launch_crc_seg(bool sar, const uint8_t *base, const uint64_t *offs, const uint64_t *sizes,
                           uint32_t n, uint64_t *nseg, uint64_t *seg_first, uint64_t *bsum,
                           const DevTables *tabs, uint32_t *crc_out, unsigned grid, hipStream_t st,
@@ -30,7 +39,7 @@ hipError_t launch_md5_stage(bool sar, const uint8_t *base, const uint64_t *offs,
                             int32_t *codes_out, hipStream_t st);
 hipError_t launch_sig_hash(bool sar, const uint8_t *base, const uint64_t *offs,
                            const uint64_t *sizes, uint32_t n, const uint32_t *order,
-                           const DevTables *tabs, uint32_t *crc_out, uint8_t *sig_out,
+                           const DevTables *tabs, uint64_t big_min, uint32_t *crc_out, uint8_t *sig_out,
                            int32_t *codes_out, hipStream_t st);
 int crc_seg_blocks_per_cu();
 int crc_table_mode();

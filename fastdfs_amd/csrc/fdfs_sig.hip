@@ -187,9 +187,10 @@ __device__ __forceinline__ uint32_t crc_final_const(uint64_t L)
 template <bool SAR, int TM>
 __global__ __launch_bounds__(kSegBlock) void crc_seg_kernel(
     const uint8_t *__restrict__ base, const uint64_t *__restrict__ offs,
-    const uint64_t *__restrict__ sizes, const uint64_t *__restrict__ seg_first, uint32_t n,
-    const DevTables *__restrict__ tabs, uint32_t *__restrict__ crc_out)
+    const uint64_t *__restrict__ sizes, const uint64_t *__restrict__ seg_first, uint32_t n_host,
+    const uint32_t *__restrict__ n_dev, const DevTables *__restrict__ tabs, uint32_t *__restrict__ crc_out)
 {
+    const uint32_t n = n_dev ? *n_dev : n_host;  // file count, or written by big_plan_kernel
     // TM 2 (64 KiB conflict-free tables): the reduction tables stay in
     // global memory (24 lookups per segment).  TM 0: everything in LDS.
     constexpr int kD = TM == 2 ? kRep8Dwords : 16 * 256;
@@ -449,6 +450,94 @@ __global__ __launch_bounds__(kScanBlock) void scan_apply_kernel(const uint64_t *
         out[n] = run;
 }
 
+// ------------------------------------------------- big-file CRC offload (HASH)
+// Files of >= kBigCrcMin bytes (a power of two, so exactly the size bins from
+// bin(kBigCrcMin) up) are the first nbig entries of the size-descending
+// order.  One block lists them for crc_seg_kernel: compacted offsets/sizes,
+// the exclusive scan of their 64 KiB segment counts, zeroed CRC slots.
+__global__ __launch_bounds__(1024) void big_plan_kernel(
+    const uint32_t *__restrict__ hist, const uint32_t *__restrict__ order,
+    const uint64_t *__restrict__ offs, const uint64_t *__restrict__ sizes, uint32_t n,
+    uint32_t *__restrict__ nbig_out, uint64_t *__restrict__ boffs, uint64_t *__restrict__ bsizes,
+    uint64_t *__restrict__ seg_first, uint32_t *__restrict__ bcrc)
+{
+    __shared__ uint32_t wsum[16];
+    __shared__ uint64_t wsum64[16];
+    __shared__ uint32_t nb_s;
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    const uint32_t b0 = size_bin(kBigCrcMin);
+    uint32_t cnt = 0;
+    for (uint32_t b = b0 + threadIdx.x; b < kSizeBins; b += blockDim.x)
+        cnt += hist[b];
+#pragma unroll
+    for (int o = 32; o; o >>= 1)
+        cnt += __shfl_xor(cnt, o);
+    if (lane == 0)
+        wsum[wid] = cnt;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        uint32_t t = 0;
+        for (int k = 0; k < (int)(blockDim.x >> 6); k++)
+            t += wsum[k];
+        nb_s = t < n ? t : n;
+        *nbig_out = nb_s;
+    }
+    __syncthreads();
+    const uint32_t nbig = nb_s;
+    uint64_t carry = 0;
+    for (uint32_t i0 = 0; i0 < nbig; i0 += blockDim.x) {
+        const uint32_t i = i0 + threadIdx.x;
+        uint64_t ns = 0;
+        if (i < nbig) {
+            const uint32_t f = order[i];
+            const uint64_t L = sizes[f];
+            boffs[i] = offs[f];
+            bsizes[i] = L;
+            bcrc[i] = 0;  // crc_seg_kernel accumulates multi-segment files by XOR
+            ns = (L + kSegBytes - 1) / kSegBytes;
+        }
+        uint64_t x = ns;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const uint64_t y = __shfl_up(x, o);
+            if (lane >= o)
+                x += y;
+        }
+        if (lane == 63)
+            wsum64[wid] = x;
+        __syncthreads();
+        uint64_t before = carry;
+        for (int k = 0; k < wid; k++)
+            before += wsum64[k];
+        if (i < nbig)
+            seg_first[i] = before + x - ns;
+        uint64_t tot = 0;
+        for (int k = 0; k < (int)(blockDim.x >> 6); k++)
+            tot += wsum64[k];
+        carry += tot;
+        __syncthreads();
+    }
+    if (threadIdx.x == 0)
+        seg_first[nbig] = carry;
+}
+
+// After the lane kernel: the segmented CRCs of the big files into crc_out,
+// the signature's CRC field (be32 at byte 8) and codes[0].
+__global__ void big_patch_kernel(const uint32_t *__restrict__ nbig, const uint32_t *__restrict__ order,
+                                 const uint32_t *__restrict__ bcrc, uint32_t *__restrict__ crc_out,
+                                 uint8_t *__restrict__ sig_out, int32_t *__restrict__ codes_out)
+{
+    const uint32_t nb = *nbig;
+    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < nb; i += gridDim.x * blockDim.x) {
+        const uint32_t f = order[i], c = bcrc[i];
+        crc_out[f] = c;
+        if (sig_out)
+            *reinterpret_cast<uint32_t *>(sig_out + 24ull * f + 8) = bswap32(c);
+        if (codes_out)
+            codes_out[4ull * f] = (int32_t)c;
+    }
+}
+
 // ------------------------------------------------------------------ launchers
 
 hipError_t launch_exclusive_scan(const uint64_t *in, uint64_t n, uint64_t *out, uint64_t *bsum,
@@ -465,10 +554,15 @@ hipError_t launch_exclusive_scan(const uint64_t *in, uint64_t n, uint64_t *out, 
 
 uint64_t scan_workspace_elems(uint64_t n) { return (n + kScanTile - 1) / kScanTile + 1; }
 
+static hipError_t crc_seg_run(bool sar, const uint8_t *base, const uint64_t *offs, const uint64_t *sizes,
+                              const uint64_t *seg_first, uint32_t n, const uint32_t *n_dev,
+                              const DevTables *tabs, uint32_t *crc_out, unsigned grid, hipStream_t st);
+
 hipError_t launch_sig_lane(bool sar, int method, const uint8_t *base, const uint64_t *offs,
                            const uint64_t *sizes, uint32_t n, uint32_t *hist, uint32_t *order,
-                           const DevTables *tabs, uint32_t *crc_out, uint8_t *sig_out,
-                           int32_t *codes_out, hipStream_t st, hipEvent_t ev0, hipEvent_t ev1)
+                           const BigCrcWs *big, const DevTables *tabs, uint32_t *crc_out,
+                           uint8_t *sig_out, int32_t *codes_out, unsigned seg_grid, hipStream_t st,
+                           hipEvent_t ev0, hipEvent_t ev1)
 {
     hipError_t e = hipMemsetAsync(hist, 0, sizeof(uint32_t) * kSizeBins * 2, st);
     if (e != hipSuccess)
@@ -478,16 +572,45 @@ hipError_t launch_sig_lane(bool sar, int method, const uint8_t *base, const uint
     bin_hist_kernel<<<hb < 1024 ? hb : 1024, 256, 0, st>>>(sizes, n, hist);
     bin_scan_kernel<<<1, 1024, 0, st>>>(hist, cursor);
     bin_scatter_kernel<<<hb, 1024, 0, st>>>(sizes, n, cursor, order);
+    const bool offload = method == 1 && big != nullptr;
+    if (offload) {  // CRC of the files >= kBigCrcMin by the segmented kernel, before the lane kernel
+        big_plan_kernel<<<1, 1024, 0, st>>>(hist, order, offs, sizes, n, big->nbig, big->offs, big->sizes,
+                                            big->seg_first, big->crc);
+        if ((e = crc_seg_run(sar, base, big->offs, big->sizes, big->seg_first, n, big->nbig, tabs, big->crc,
+                             seg_grid, st)) != hipSuccess)
+            return e;
+    }
     if (ev0)
         (void)hipEventRecord(ev0, st);
     e = (method == 2) ? launch_md5_stage(sar, base, offs, sizes, n, order, tabs, crc_out, sig_out,
                                          codes_out, st)
-                      : launch_sig_hash(sar, base, offs, sizes, n, order, tabs, crc_out, sig_out,
-                                        codes_out, st);
+                      : launch_sig_hash(sar, base, offs, sizes, n, order, tabs,
+                                        offload ? kBigCrcMin : ~0ull, crc_out, sig_out, codes_out, st);
     if (e != hipSuccess)
         return e;
     if (ev1)
         (void)hipEventRecord(ev1, st);
+    if (offload)
+        big_patch_kernel<<<256, 256, 0, st>>>(big->nbig, order, big->crc, crc_out, sig_out, codes_out);
+    return hipGetLastError();
+}
+
+static hipError_t crc_seg_run(bool sar, const uint8_t *base, const uint64_t *offs, const uint64_t *sizes,
+                              const uint64_t *seg_first, uint32_t n, const uint32_t *n_dev,
+                              const DevTables *tabs, uint32_t *crc_out, unsigned grid, hipStream_t st)
+{
+    const int tm = crc_table_mode();
+#define SEG_LAUNCH(S, T) \
+    crc_seg_kernel<S, T><<<grid, kSegBlock, 0, st>>>(base, offs, sizes, seg_first, n, n_dev, tabs, crc_out)
+    if (sar && tm == 2)
+        SEG_LAUNCH(true, 2);
+    else if (sar)
+        SEG_LAUNCH(true, 0);
+    else if (tm == 2)
+        SEG_LAUNCH(false, 2);
+    else
+        SEG_LAUNCH(false, 0);
+#undef SEG_LAUNCH
     return hipGetLastError();
 }
 
@@ -502,18 +625,8 @@ hipError_t launch_crc_seg(bool sar, const uint8_t *base, const uint64_t *offs, c
         return e;
     if (ev0)
         (void)hipEventRecord(ev0, st);
-    const int tm = crc_table_mode();
-#define SEG_LAUNCH(S, T) \
-    crc_seg_kernel<S, T><<<grid, kSegBlock, 0, st>>>(base, offs, sizes, seg_first, n, tabs, crc_out)
-    if (sar && tm == 2)
-        SEG_LAUNCH(true, 2);
-    else if (sar)
-        SEG_LAUNCH(true, 0);
-    else if (tm == 2)
-        SEG_LAUNCH(false, 2);
-    else
-        SEG_LAUNCH(false, 0);
-#undef SEG_LAUNCH
+    if ((e = crc_seg_run(sar, base, offs, sizes, seg_first, n, nullptr, tabs, crc_out, grid, st)) != hipSuccess)
+        return e;
     if (ev1)
         (void)hipEventRecord(ev1, st);
     return hipGetLastError();

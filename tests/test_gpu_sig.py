@@ -133,6 +133,27 @@ def test_large_file_segmented(oracle, ctxs, variant):
     _check(oracle, ctxs[variant], variant, buf, offs, sz, methods=(0,))
 
 
+@pytest.mark.parametrize("variant", [0, 1])
+@pytest.mark.parametrize("align", [16, 1])
+def test_big_file_crc_offload(oracle, ctxs, variant, align):
+    """HASH method with whole waves of files >= 4 MiB (kBigCrcMin): their CRC
+    comes from the segmented kernel and is patched into crc_out, the
+    signature and the codes; files at and just below the threshold, a mixed
+    wave and small files in the same batch."""
+    rng = np.random.default_rng(31 + variant * 2 + (align == 1))
+    big = rng.integers(4 << 20, (4 << 20) + 300_000, size=130)
+    sizes = np.concatenate([big, [4 << 20, (4 << 20) - 1, (4 << 20) + 1, 9 << 20],
+                            rng.integers(0, 70000, 200)])
+    rng.shuffle(sizes)
+    buf, offs, sz = _packed(sizes, align, rng)
+    dev_batch = _to_dev(buf, offs, sz)
+    _check(oracle, ctxs[variant], variant, buf, offs, sz, methods=(1,), dev_batch=dev_batch)
+    crc, _, codes = _gpu(ctxs[variant], dev_batch, 1)
+    assert np.array_equal(codes[:, 0].view(np.uint32), crc)
+    crc0, _, _ = _gpu(ctxs[variant], dev_batch, 0)
+    assert np.array_equal(crc0, crc)
+
+
 def test_crc_paths_agree_at_scale(oracle, ctxs):
     """Config 2 at full size (1M files, ~34.8 GB in HBM): the three kernels'
     CRCs agree for every file (size-independent property) and a random sample
