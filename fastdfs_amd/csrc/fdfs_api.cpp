@@ -80,7 +80,8 @@ size_t sig_ws_bytes(uint64_t n)
 {
     size_t lane = align_up(sizeof(uint32_t) * fdfs::kLaneWsDwords) + align_up(sizeof(uint32_t) * n) +
                   align_up(sizeof(uint32_t)) + 2 * align_up(sizeof(uint64_t) * n) +
-                  align_up(sizeof(uint64_t) * (n + 1)) + align_up(sizeof(uint32_t) * n);  // + BigCrcWs
+                  align_up(sizeof(uint64_t) * (n + 1)) + align_up(sizeof(uint32_t) * n) +
+                  align_up(2 * sizeof(uint32_t) * n);  // + BigCrcWs
     size_t seg = align_up(sizeof(uint64_t) * n) + align_up(sizeof(uint64_t) * (n + 1)) +
                  align_up(sizeof(uint64_t) * fdfs::scan_workspace_elems(n));
     return lane > seg ? lane : seg;  // one path per call
@@ -305,6 +306,7 @@ int fdfs_gpu_sig_batch(fdfs_gpu_ctx *ctx, const fdfs_gpu_batch *batch, int metho
         big.sizes = cv.take<uint64_t>(n);
         big.seg_first = cv.take<uint64_t>((size_t)n + 1);
         big.crc = cv.take<uint32_t>(n);
+        big.poly = cv.take<uint32_t>(2 * (size_t)n);
         hipEvent_t a, b;
         timing_pair(ctx, FDFS_KERNEL_SIG_LANE, a, b);
         e = fdfs::launch_sig_lane(ctx->sar, method, base, batch->offset, batch->size, n, hist,

@@ -65,10 +65,10 @@ __device__ __forceinline__ uint32_t crc16(const uint32_t *sD, const Rep8Lane &R8
 
 template <bool SAR, int TM>
 __device__ __forceinline__ void h4_lane(const uint32_t *sD, const Rep8Lane &R8, uint32_t K16,
-                                        uint4 q, bool do_crc, uint32_t &c, uint32_t &e, uint32_t &s,
+                                        uint4 q, bool small, uint32_t &c, uint32_t &e, uint32_t &s,
                                         uint32_t &t)
 {
-    if (do_crc)
+    if (small)
         c = crc16<SAR, TM>(sD, R8, K16, c, q);
     elf_word4<SAR, false>(q.x, e);
     elf_word4<SAR, false>(q.y, e);
@@ -126,12 +126,13 @@ __global__ __launch_bounds__(TM == 2 ? 1024 : kHashBlock) void sig_hash_kernel(
     const uint8_t *p = valid ? base + offs[f] : safe;
     uint32_t c = 0xFFFFFFFFu;  // CRC32_XINIT (storage/storage_service.c:7149)
     uint32_t e = 0, s = 0, t = 0;  // INIT_HASH_CODES4 (storage/storage_service.c:7156)
-    // Files of >= big_min bytes leave their CRC to the segmented kernel
-    // (launch_sig_lane runs it before this one and patches the outputs
-    // after): their waves are few and issue-bound, the CRC is ~30% of their
-    // instructions, and once a wave's smaller files have ended its CRC
-    // blocks run with an empty exec mask and are branched over.
-    const bool do_crc = L < big_min;
+    // Files of >= big_min bytes leave their CRC, simple_hash and Time33 to
+    // segment-parallel kernels (launch_sig_lane runs them before this one
+    // and patches the outputs after) and keep only ELFHash here: their waves
+    // are few and issue-bound, the rest is ~half of their instructions, and
+    // once a wave's smaller files have ended its CRC blocks run with an
+    // empty exec mask (branched over) and its MFMA steps are skipped.
+    const bool small = L < big_min;
 
     // bytes to 16-byte alignment, then vectors to 128-byte alignment (lane-serial)
     uint64_t head = (16u - ((uintptr_t)p & 15u)) & 15u;
@@ -139,7 +140,7 @@ __global__ __launch_bounds__(TM == 2 ? 1024 : kHashBlock) void sig_hash_kernel(
         head = L;
     for (uint64_t k = 0; k < head; k++) {
         const uint32_t b = p[k];
-        if (do_crc)
+        if (small)
             c = crc_byte<SAR>(sT, c, b);
         h3_byte<SAR>(b, e, s, t);
     }
@@ -149,7 +150,7 @@ __global__ __launch_bounds__(TM == 2 ? 1024 : kHashBlock) void sig_hash_kernel(
     if (lead > nvec)
         lead = nvec;
     for (uint64_t j = 0; j < lead; j++)
-        h4_lane<SAR, TM>(sD, R8, K16, v[j], do_crc, c, e, s, t);
+        h4_lane<SAR, TM>(sD, R8, K16, v[j], small, c, e, s, t);
 
     // whole 128-byte lines: the wave steps in lockstep to its longest file
     const uint32_t nsteps = (uint32_t)((nvec - lead) >> 3);
@@ -177,9 +178,17 @@ __global__ __launch_bounds__(TM == 2 ? 1024 : kHashBlock) void sig_hash_kernel(
         const uint4 *w = v + lead;
         // One 128-byte step: lane hashes for files not yet ended, then the
         // two polynomial MFMAs per vector for every lane.
+        // Steps only run the polynomial MFMAs while a lane below big_min is
+        // still hashing (big files get simple/Time33 from poly_seg_kernel):
+        // nexec counts them for the padding undo below.
+        uint32_t nexec = 0;
         auto step = [&](const u32x4 (&a)[8], bool ok) {
+            const bool mon = __any(ok && small);
+            nexec += mon ? 1u : 0u;
 #pragma unroll
             for (int r = 0; r < 4; r++) {
+                if (!mon)
+                    break;
                 C31[r] = (int)((uint32_t)C31[r] * m31) + k31[r];
                 C33[r] = (int)((uint32_t)C33[r] * m33) + k33[r];
             }
@@ -192,13 +201,15 @@ __global__ __launch_bounds__(TM == 2 ? 1024 : kHashBlock) void sig_hash_kernel(
                     continue;
                 }
                 if (ok) {
-                    if (do_crc)
+                    if (small)
                         c = crc16<SAR, TM>(sD, R8, K16, c, aq);
                     elf_word4<SAR, false>(aq.x, e);
                     elf_word4<SAR, false>(aq.y, e);
                     elf_word4<SAR, false>(aq.z, e);
                     elf_word4<SAR, true>(aq.w, e);
                 }
+                if (!mon)
+                    continue;
                 // b - 128 as int8 (b ^ 0x80); a padded step is all-zero data
                 const uint32_t msk = ok ? 0xFFFFFFFFu : 0u;
                 const i32x4 A = {(int)and_xor80(aq.x, msk), (int)and_xor80(aq.y, msk),
@@ -256,23 +267,23 @@ __global__ __launch_bounds__(TM == 2 ? 1024 : kHashBlock) void sig_hash_kernel(
                 s33 = ys;
             }
         }
-        const uint32_t pad = nmax - nsteps;
+        const uint32_t pad = nexec - nsteps;  // (garbage for big-file lanes: patched)
         s = s31 * pow_dev(tabs->pm.inv128[0], pad);
         t = s33 * pow_dev(tabs->pm.inv128[1], pad);
     }
 
     for (uint64_t jv = lead + 8 * (uint64_t)nsteps; jv < nvec; jv++)
-        h4_lane<SAR, TM>(sD, R8, K16, v[jv], do_crc, c, e, s, t);
+        h4_lane<SAR, TM>(sD, R8, K16, v[jv], small, c, e, s, t);
     for (uint64_t k = head + (nvec << 4); k < L; k++) {  // the last (L - head) & 15 bytes
         const uint32_t b = p[k];
-        if (do_crc)
+        if (small)
             c = crc_byte<SAR>(sT, c, b);
         h3_byte<SAR>(b, e, s, t);
     }
     if (!valid)
         return;
     c ^= 0xFFFFFFFFu;  // CRC32_FINAL / FINISH_HASH_CODES4 (storage/storage_dio.c:500,508)
-    if (do_crc)
+    if (small)
         crc_out[f] = c;  // else big_patch_kernel puts the segmented CRC in all three outputs
     if (sig_out) {  // STORAGE_GEN_FILE_SIGNATURE (storage/storage_service.c:106-120)
         uint2 *sp = reinterpret_cast<uint2 *>(sig_out + 24ull * f);
@@ -282,6 +293,86 @@ __global__ __launch_bounds__(TM == 2 ? 1024 : kHashBlock) void sig_hash_kernel(
     }
     if (codes_out)
         reinterpret_cast<int4 *>(codes_out)[f] = make_int4((int)c, (int)e, (int)s, (int)t);
+}
+
+// simple_hash_ex / Time33Hash_ex of the files >= kBigCrcMin, segment-parallel
+// (INIT_HASH_CODES4 starts both at 0, so a file's hash is the polynomial
+// sum_pos b_pos M^(L-1-pos) mod 2^32 and splits over any cut).  One wave per
+// 64 KiB segment of the big-file list big_plan_kernel made; lane l hashes
+// the segment's l-th KiB (Horner, 16-byte loads when the file is aligned),
+// scales it by M^(bytes after it in the file) and the wave's sum is added
+// into the file's slot (mod 2^32 addition commutes).  Multiplicative orders
+// of 31 and 33 mod 2^32 divide 2^30, so exponents are reduced mod 2^30.
+constexpr int kPolyBlock = 256;
+
+__global__ __launch_bounds__(kPolyBlock) void poly_seg_kernel(
+    const uint8_t *__restrict__ base, const uint64_t *__restrict__ boffs,
+    const uint64_t *__restrict__ bsizes, const uint64_t *__restrict__ seg_first,
+    const uint32_t *__restrict__ nbig, uint32_t *__restrict__ bpoly)
+{
+    const uint32_t nb = *nbig;
+    const uint64_t total = seg_first[nb];
+    const int lane = threadIdx.x & 63;
+    const uint64_t nw = (uint64_t)gridDim.x * (kPolyBlock / 64);
+    for (uint64_t sg = (uint64_t)blockIdx.x * (kPolyBlock / 64) + (threadIdx.x >> 6); sg < total; sg += nw) {
+        uint32_t lo = 0, hi = nb;  // last file with seg_first <= sg
+        while (hi - lo > 1) {
+            const uint32_t mid = (lo + hi) >> 1;
+            if (seg_first[mid] <= sg)
+                lo = mid;
+            else
+                hi = mid;
+        }
+        const uint32_t f = lo;
+        const uint64_t L = bsizes[f];
+        const uint8_t *fp = base + boffs[f];
+        const uint64_t s0 = (sg - seg_first[f]) * kSegBytes + (uint64_t)lane * 1024;
+        const uint64_t s1 = s0 + 1024 < L ? s0 + 1024 : L;
+        uint32_t h31 = 0, h33 = 0;
+        if (s0 < s1) {
+            const uint8_t *q = fp + s0;
+            uint64_t k = 0;
+            const uint64_t len = s1 - s0;
+            if ((((uintptr_t)q) & 15u) == 0) {
+                for (; k + 16 <= len; k += 16) {
+                    const uint4 v = *reinterpret_cast<const uint4 *>(q + k);
+                    h31 = poly_word<31>(h31, v.x);
+                    h33 = poly_word<33>(h33, v.x);
+                    h31 = poly_word<31>(h31, v.y);
+                    h33 = poly_word<33>(h33, v.y);
+                    h31 = poly_word<31>(h31, v.z);
+                    h33 = poly_word<33>(h33, v.z);
+                    h31 = poly_word<31>(h31, v.w);
+                    h33 = poly_word<33>(h33, v.w);
+                }
+            }
+            for (; k < len; k++) {
+                const uint32_t b = q[k];
+                h31 = h31 * 31u + b;
+                h33 = h33 * 33u + b;
+            }
+            const uint32_t e = (uint32_t)((L - s1) & 0x3FFFFFFFull);
+            h31 *= pow_dev(31u, e);
+            h33 *= pow_dev(33u, e);
+        }
+#pragma unroll
+        for (int o = 32; o; o >>= 1) {
+            h31 += __shfl_xor(h31, o);
+            h33 += __shfl_xor(h33, o);
+        }
+        if (lane == 0) {
+            atomicAdd(&bpoly[2ull * f], h31);
+            atomicAdd(&bpoly[2ull * f + 1], h33);
+        }
+    }
+}
+
+hipError_t launch_poly_seg(const uint8_t *base, const uint64_t *boffs, const uint64_t *bsizes,
+                           const uint64_t *seg_first, const uint32_t *nbig, uint32_t *bpoly,
+                           unsigned grid, hipStream_t st)
+{
+    poly_seg_kernel<<<grid, kPolyBlock, 0, st>>>(base, boffs, bsizes, seg_first, nbig, bpoly);
+    return hipGetLastError();
 }
 
 hipError_t launch_sig_hash(bool sar, const uint8_t *base, const uint64_t *offs,

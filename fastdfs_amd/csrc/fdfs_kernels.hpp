@@ -16,14 +16,19 @@ constexpr int kLaneWsDwords = 2 * kSizeBins;  // size-bin histogram + cursors
 uint64_t scan_workspace_elems(uint64_t n);
 hipError_t launch_exclusive_scan(const uint64_t *in, uint64_t n, uint64_t *out, uint64_t *bsum,
                                  hipStream_t st);
-// HASH method: files of at least kBigCrcMin bytes get their CRC from the
-// segmented kernel (a wave of such files is issue-bound, see fdfs_hash.hip).
+// HASH method: files of at least kBigCrcMin bytes get their CRC, simple_hash
+// and Time33 from segment-parallel kernels (a wave of such files is
+// issue-bound, see fdfs_hash.hip); their lanes keep only ELFHash.
 constexpr uint64_t kBigCrcMin = 4ull << 20;
 struct BigCrcWs {  // device arrays of n entries (seg_first n + 1)
     uint32_t *nbig;
     uint64_t *offs, *sizes, *seg_first;
     uint32_t *crc;
+    uint32_t *poly;  // [2n]: simple_hash, Time33 per big file
 };
+hipError_t launch_poly_seg(const uint8_t *base, const uint64_t *boffs, const uint64_t *bsizes,
+                           const uint64_t *seg_first, const uint32_t *nbig, uint32_t *bpoly,
+                           unsigned grid, hipStream_t st);
 hipError_t launch_sig_lane(bool sar, int method, const uint8_t *base, const uint64_t *offs,
                            const uint64_t *sizes, uint32_t n, uint32_t *hist, uint32_t *order,
                            const BigCrcWs *big, const DevTables *tabs, uint32_t *crc_out,

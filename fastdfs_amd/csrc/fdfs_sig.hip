@@ -459,7 +459,7 @@ __global__ __launch_bounds__(1024) void big_plan_kernel(
     const uint32_t *__restrict__ hist, const uint32_t *__restrict__ order,
     const uint64_t *__restrict__ offs, const uint64_t *__restrict__ sizes, uint32_t n,
     uint32_t *__restrict__ nbig_out, uint64_t *__restrict__ boffs, uint64_t *__restrict__ bsizes,
-    uint64_t *__restrict__ seg_first, uint32_t *__restrict__ bcrc)
+    uint64_t *__restrict__ seg_first, uint32_t *__restrict__ bcrc, uint32_t *__restrict__ bpoly)
 {
     __shared__ uint32_t wsum[16];
     __shared__ uint64_t wsum64[16];
@@ -494,6 +494,8 @@ __global__ __launch_bounds__(1024) void big_plan_kernel(
             boffs[i] = offs[f];
             bsizes[i] = L;
             bcrc[i] = 0;  // crc_seg_kernel accumulates multi-segment files by XOR
+            bpoly[2ull * i] = 0;  // poly_seg_kernel adds segment contributions
+            bpoly[2ull * i + 1] = 0;
             ns = (L + kSegBytes - 1) / kSegBytes;
         }
         uint64_t x = ns;
@@ -521,20 +523,28 @@ __global__ __launch_bounds__(1024) void big_plan_kernel(
         seg_first[nbig] = carry;
 }
 
-// After the lane kernel: the segmented CRCs of the big files into crc_out,
-// the signature's CRC field (be32 at byte 8) and codes[0].
+// After the lane kernel: the big files' segmented CRC, simple_hash and
+// Time33 into crc_out, their signature fields and codes[0], [2], [3].
 __global__ void big_patch_kernel(const uint32_t *__restrict__ nbig, const uint32_t *__restrict__ order,
-                                 const uint32_t *__restrict__ bcrc, uint32_t *__restrict__ crc_out,
-                                 uint8_t *__restrict__ sig_out, int32_t *__restrict__ codes_out)
+                                 const uint32_t *__restrict__ bcrc, const uint32_t *__restrict__ bpoly,
+                                 uint32_t *__restrict__ crc_out, uint8_t *__restrict__ sig_out,
+                                 int32_t *__restrict__ codes_out)
 {
     const uint32_t nb = *nbig;
     for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < nb; i += gridDim.x * blockDim.x) {
-        const uint32_t f = order[i], c = bcrc[i];
+        const uint32_t f = order[i], c = bcrc[i], s = bpoly[2ull * i], t = bpoly[2ull * i + 1];
         crc_out[f] = c;
-        if (sig_out)
-            *reinterpret_cast<uint32_t *>(sig_out + 24ull * f + 8) = bswap32(c);
-        if (codes_out)
+        if (sig_out) {  // be32 crc at 8, be32 simple at 16, be32 Time33 at 20
+            uint32_t *sp = reinterpret_cast<uint32_t *>(sig_out + 24ull * f);
+            sp[2] = bswap32(c);
+            sp[4] = bswap32(s);
+            sp[5] = bswap32(t);
+        }
+        if (codes_out) {
             codes_out[4ull * f] = (int32_t)c;
+            codes_out[4ull * f + 2] = (int32_t)s;
+            codes_out[4ull * f + 3] = (int32_t)t;
+        }
     }
 }
 
@@ -575,9 +585,12 @@ hipError_t launch_sig_lane(bool sar, int method, const uint8_t *base, const uint
     const bool offload = method == 1 && big != nullptr;
     if (offload) {  // CRC of the files >= kBigCrcMin by the segmented kernel, before the lane kernel
         big_plan_kernel<<<1, 1024, 0, st>>>(hist, order, offs, sizes, n, big->nbig, big->offs, big->sizes,
-                                            big->seg_first, big->crc);
+                                            big->seg_first, big->crc, big->poly);
         if ((e = crc_seg_run(sar, base, big->offs, big->sizes, big->seg_first, n, big->nbig, tabs, big->crc,
                              seg_grid, st)) != hipSuccess)
+            return e;
+        if ((e = launch_poly_seg(base, big->offs, big->sizes, big->seg_first, big->nbig, big->poly, seg_grid,
+                                 st)) != hipSuccess)
             return e;
     }
     if (ev0)
@@ -591,7 +604,8 @@ hipError_t launch_sig_lane(bool sar, int method, const uint8_t *base, const uint
     if (ev1)
         (void)hipEventRecord(ev1, st);
     if (offload)
-        big_patch_kernel<<<256, 256, 0, st>>>(big->nbig, order, big->crc, crc_out, sig_out, codes_out);
+        big_patch_kernel<<<256, 256, 0, st>>>(big->nbig, order, big->crc, big->poly, crc_out, sig_out,
+                                              codes_out);
     return hipGetLastError();
 }
 
