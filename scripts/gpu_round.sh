@@ -1,6 +1,6 @@
 # Full round-end evidence on one MI355X: smoke, every gpu test, bench lines for
 # all configs, rocprofv3 kernel stats and separate HBM PMC passes.
-# Usage: TAG=r01 bash scripts/gpu_round.sh   (results under gpurun_out/round_$TAG)
+# Usage: TAG=r01 [PART=1|2] bash scripts/gpu_round.sh   (results under gpurun_out/round_$TAG)
 export TMPDIR=/tmp
 TAG=${TAG:-r01}
 O=gpurun_out/round_$TAG
@@ -11,6 +11,8 @@ step() {  # name timeout cmd...   (every GPU step under its own time limit)
   echo "$name=$rc"; return $rc
 }
 B="python3 bench.py --no-cpu-baseline"
+S="--steps 3 --warmup 1"
+if [ "${PART:-all}" != 2 ]; then  # PART=1: tests, bench lines, kernel stats
 step smoke 300 python3 -u -c "import __graft_entry__ as g; g.smoke()" || exit $?
 step pytest 900 python3 -u -m pytest tests -m gpu -v --timeout 300 --timeout-method thread; rc=$?
 tail -3 $O/pytest.log
@@ -19,12 +21,15 @@ step bench_c2 600 python3 bench.py || exit $?
 step bench_c3 600 $B --config c3 --steps 3 --warmup 1 || exit $?
 step bench_c4 600 python3 bench.py --config c4 || exit $?
 step bench_c5 600 python3 bench.py --config c5 --steps 5 --warmup 1 || exit $?
-for c in c2 c3 c4; do tail -1 $O/bench_$c.log | cut -c1-300; done
-S="--steps 3 --warmup 1"
+step bench_c1 900 python3 bench.py --config c1 --steps 3 --warmup 1 || exit $?
+for c in c1 c2 c3 c4 c5; do tail -1 $O/bench_$c.log | cut -c1-300; done
 step stats_c2 600 rocprofv3 --kernel-trace --stats -d $O/stats_c2 -o run --output-format csv -- $B $S || exit $?
 step stats_c3 600 rocprofv3 --kernel-trace --stats -d $O/stats_c3 -o run --output-format csv -- $B --config c3 --steps 2 --warmup 1 || exit $?
 step stats_c4 600 rocprofv3 --kernel-trace --stats -d $O/stats_c4 -o run --output-format csv -- $B --config c4 $S || exit $?
 step stats_c5 600 rocprofv3 --kernel-trace --stats -d $O/stats_c5 -o run --output-format csv -- $B --config c5 $S || exit $?
+step stats_c1 900 rocprofv3 --kernel-trace --stats -d $O/stats_c1 -o run --output-format csv -- $B --config c1 --steps 2 --warmup 1 || exit $?
+fi
+if [ "${PART:-all}" != 1 ]; then  # PART=2: PMC passes and probes
 for c in c2 c3 c4 c5; do
   step fetch_$c 300 rocprofv3 --pmc FETCH_SIZE -d $O/fetch_$c -o run --output-format csv -- $B --config $c --steps 1 --warmup 1 || exit $?
   step write_$c 300 rocprofv3 --pmc WRITE_SIZE -d $O/write_$c -o run --output-format csv -- $B --config $c --steps 1 --warmup 1 || exit $?
@@ -34,4 +39,5 @@ step sq_c2 300 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_AN
 for m in 1 2; do
   FDFS_GPU_HASH_MODE=$m step probe_c2_mode$m 300 $B || exit $?
 done
+fi
 echo done

@@ -27,13 +27,13 @@ def short(name):
 
 def main(src, dst):
     os.makedirs(dst, exist_ok=True)
-    for c in ("c2", "c3", "c4", "c5"):
+    for c in ("c1", "c2", "c3", "c4", "c5"):
         log = os.path.join(src, f"bench_{c}.log")
         if os.path.exists(log):
             line = open(log).read().strip().split("\n")[-1]
             json.loads(line)
             open(os.path.join(dst, f"bench_{c}.json"), "w").write(line + "\n")
-    for c in ("c2", "c3", "c4", "c5"):
+    for c in ("c1", "c2", "c3", "c4", "c5"):
         for f in glob.glob(os.path.join(src, f"stats_{c}", "**", "*kernel_stats.csv"), recursive=True):
             rows = list(csv.DictReader(open(f)))
             with open(os.path.join(dst, f"kernel_stats_{c}.csv"), "w", newline="") as out:
