@@ -217,7 +217,7 @@ __global__ __launch_bounds__(kDpTileThreads) void dp_scatter_kernel(
 // whole bucket; the second goes chunk by chunk (rank, LDS sort by digit,
 // contiguous runs out, per-digit cursors advanced by the chunk's counts).
 constexpr int kDpSplitThreads = 1024;
-constexpr int kDpSplitPer = 4;  // entries per thread per chunk
+constexpr int kDpSplitPer = 8;  // entries per thread per chunk
 constexpr int kDpChunk = kDpSplitThreads * kDpSplitPer;
 
 __global__ __launch_bounds__(kDpSplitThreads) void dp_split_kernel(
