@@ -35,6 +35,8 @@
 #include "fdfs_device.hpp"
 #include "fdfs_kernels.hpp"
 
+#include <cstdlib>
+
 namespace fdfs {
 
 __device__ __forceinline__ uint64_t fmix64(uint64_t k)
@@ -217,9 +219,9 @@ __global__ __launch_bounds__(kDpTileThreads) void dp_scatter_kernel(
 // whole bucket; the second goes chunk by chunk (rank, LDS sort by digit,
 // contiguous runs out, per-digit cursors advanced by the chunk's counts).
 constexpr int kDpSplitThreads = 1024;
-constexpr int kDpSplitPer = 8;  // entries per thread per chunk
-constexpr int kDpChunk = kDpSplitThreads * kDpSplitPer;
+constexpr int kDpSplitPer = 8;  // entries per thread per chunk (FDFS_GPU_DEDUP_SPLIT=4: A/B)
 
+template <int PER_T>
 __global__ __launch_bounds__(kDpSplitThreads) void dp_split_kernel(
     const uint64_t *__restrict__ ent, uint64_t n, int d1, int d2, uint64_t tiles,
     const uint64_t *__restrict__ off, uint64_t *__restrict__ ent2, uint32_t *__restrict__ pstart)
@@ -230,6 +232,7 @@ __global__ __launch_bounds__(kDpSplitThreads) void dp_split_kernel(
     __shared__ uint32_t cc[NB];   // chunk counts
     __shared__ uint32_t cl[NB];   // chunk-local starts
     __shared__ uint32_t wsum[kDpSplitThreads / 64];
+    constexpr int kDpChunk = kDpSplitThreads * PER_T;
     __shared__ uint64_t stage[kDpChunk];
     const uint32_t nd2 = 1u << d2;
     const uint64_t s = off[(uint64_t)blockIdx.x * tiles];
@@ -251,10 +254,10 @@ __global__ __launch_bounds__(kDpSplitThreads) void dp_split_kernel(
         for (uint32_t k = threadIdx.x; k < nd2; k += blockDim.x)
             cc[k] = 0;
         __syncthreads();
-        uint64_t en[kDpSplitPer];
-        uint32_t rk[kDpSplitPer];
+        uint64_t en[PER_T];
+        uint32_t rk[PER_T];
 #pragma unroll
-        for (int q = 0; q < kDpSplitPer; q++) {
+        for (int q = 0; q < PER_T; q++) {
             const uint32_t l = q * kDpSplitThreads + threadIdx.x;
             if (l < m) {
                 en[q] = ent[c0 + l];
@@ -264,7 +267,7 @@ __global__ __launch_bounds__(kDpSplitThreads) void dp_split_kernel(
         __syncthreads();
         block_scan_bins<PER, kDpSplitThreads>(cc, cl, nd2, wsum);
 #pragma unroll
-        for (int q = 0; q < kDpSplitPer; q++) {
+        for (int q = 0; q < PER_T; q++) {
             const uint32_t l = q * kDpSplitThreads + threadIdx.x;
             if (l < m)
                 stage[cl[(uint32_t)(en[q] >> sh) & (nd2 - 1)] + rk[q]] = en[q];
@@ -539,8 +542,17 @@ hipError_t launch_dedup_group(const uint8_t *sig, uint32_t sig_stride, const uin
     dp_scatter_kernel<<<(unsigned)pl.tiles, kDpTileThreads, 0, st>>>(keys, n, pl.d1, pl.tiles, off, ent);
     const uint64_t *parts = ent;
     if (pl.d2) {
-        dp_split_kernel<<<1u << pl.d1, kDpSplitThreads, 0, st>>>(ent, n, pl.d1, pl.d2, pl.tiles, off,
-                                                                  ent2, pstart);
+        static int per = -1;
+        if (per < 0) {
+            const char *ev = getenv("FDFS_GPU_DEDUP_SPLIT");
+            per = (ev && atoi(ev) == 4) ? 4 : kDpSplitPer;
+        }
+        if (per == 4)
+            dp_split_kernel<4><<<1u << pl.d1, kDpSplitThreads, 0, st>>>(ent, n, pl.d1, pl.d2, pl.tiles, off,
+                                                                     ent2, pstart);
+        else
+            dp_split_kernel<kDpSplitPer><<<1u << pl.d1, kDpSplitThreads, 0, st>>>(ent, n, pl.d1, pl.d2, pl.tiles,
+                                                                               off, ent2, pstart);
         parts = ent2;
     } else {
         dp_starts_kernel<<<((1u << pl.d1) + 255) / 256, 256, 0, st>>>(off, n, pl.d1, pl.tiles, pstart);
