@@ -350,13 +350,19 @@ __device__ __forceinline__ uint32_t dp_insert(uint64_t *word, uint32_t size, uin
     }
 }
 
-// A record's ingest index, from its own rep_out slot (dp_keys wrote
-// gidx[r] there): the multi-member records read here are the ones whose
-// rep_out line is written at the end, so the read brings in the line the
-// random store lands on instead of touching a third array.
-__device__ __forceinline__ uint64_t gidx_of(const uint64_t *rep, uint32_t gstride, uint32_t r)
+// A record's ingest index for the class minimum (only multi-member classes
+// read it).  GM_ROW: the 32-byte exchange rows carry it at byte 24, on the
+// line the confirmation just read.  GM_REP: from the record's own rep_out
+// slot (dp_keys wrote gidx[r] there): the line its final store lands on,
+// instead of a third array.  GM_INDEX: no gidx, the record index itself.
+enum { GM_INDEX = 0, GM_REP = 1, GM_ROW = 2 };
+
+__device__ __forceinline__ uint64_t gidx_of(const uint64_t *rep, const uint8_t *sig, uint32_t stride,
+                                            int gmode, uint32_t r)
 {
-    return gstride ? rep[r] : (uint64_t)r;
+    if (gmode == GM_ROW)
+        return *reinterpret_cast<const uint64_t *>(sig + (uint64_t)r * stride + 24);
+    return gmode == GM_REP ? rep[r] : (uint64_t)r;
 }
 // Only records of classes with more than one member are written (random
 // stores); K1 already wrote every record's singleton answer.  The class
@@ -367,7 +373,7 @@ constexpr int kDpEpt = (kDpCap + kDpGroupThreads - 1) / kDpGroupThreads;  // ent
 
 __global__ __launch_bounds__(kDpGroupThreads) __attribute__((amdgpu_waves_per_eu(8))) void dp_group_kernel(
     const uint64_t *__restrict__ ent, const uint32_t *__restrict__ pstart,
-    const uint8_t *__restrict__ sig, uint32_t stride, uint32_t gstride, uint64_t *__restrict__ gword, uint64_t *__restrict__ gmin,
+    const uint8_t *__restrict__ sig, uint32_t stride, int gmode, uint64_t *__restrict__ gword, uint64_t *__restrict__ gmin,
     uint32_t *__restrict__ gcnt, uint32_t *__restrict__ gslot, uint64_t *__restrict__ rep_out,
     uint32_t *__restrict__ ref_out)
 {
@@ -414,8 +420,8 @@ __global__ __launch_bounds__(kDpGroupThreads) __attribute__((amdgpu_waves_per_eu
             if (own[k] != r) {
                 load_sig(sig + (uint64_t)r * stride, ra[k], rb[k], rc[k]);
                 load_sig(sig + (uint64_t)own[k] * stride, oa[k], ob[k], oc[k]);
-                gr[k] = gidx_of(rep_out, gstride, r);
-                go[k] = gidx_of(rep_out, gstride, own[k]);
+                gr[k] = gidx_of(rep_out, sig, stride, gmode, r);
+                go[k] = gidx_of(rep_out, sig, stride, gmode, own[k]);
             }
         }
 #pragma unroll
@@ -428,7 +434,7 @@ __global__ __launch_bounds__(kDpGroupThreads) __attribute__((amdgpu_waves_per_eu
                     slot[k] = dp_insert<true>(word, kDpSlots, (uint32_t)(en[k] >> 32), r,
                                               dp_next(slot[k], kDpSlots, true), sig, stride, own[k]);
                     if (own[k] != r)
-                        go[k] = gidx_of(rep_out, gstride, own[k]);
+                        go[k] = gidx_of(rep_out, sig, stride, gmode, own[k]);
                 }
                 atomicAdd(&cn[slot[k]], 1u);
                 if (own[k] != r)
@@ -470,7 +476,7 @@ __global__ __launch_bounds__(kDpGroupThreads) __attribute__((amdgpu_waves_per_eu
         const uint32_t slot = dp_insert<false>(w, size, key, r, dp_home(key, size, false), sig, stride, o);
         atomicAdd(&c[slot], 1u);
         if (o != r) {
-            const uint64_t a = gidx_of(rep_out, gstride, r), b = gidx_of(rep_out, gstride, o);
+            const uint64_t a = gidx_of(rep_out, sig, stride, gmode, r), b = gidx_of(rep_out, sig, stride, gmode, o);
             atomicMin(reinterpret_cast<unsigned long long *>(&m[slot]), (unsigned long long)(a < b ? a : b));
         }
         gslot[s + l] = slot;
@@ -557,8 +563,12 @@ hipError_t launch_dedup_group(const uint8_t *sig, uint32_t sig_stride, const uin
     } else {
         dp_starts_kernel<<<((1u << pl.d1) + 255) / 256, 256, 0, st>>>(off, n, pl.d1, pl.tiles, pstart);
     }
+    const int gmode = !gidx_stride ? GM_INDEX
+                      : (gidx == reinterpret_cast<const uint64_t *>(sig + 24) && 8 * gidx_stride == sig_stride)
+                          ? GM_ROW
+                          : GM_REP;
     dp_group_kernel<<<(unsigned)pl.nparts(), kDpGroupThreads, 0, st>>>(
-        parts, pstart, sig, sig_stride, gidx_stride, gword, gmin, gcnt, gslot, rep_out, ref_out);
+        parts, pstart, sig, sig_stride, gmode, gword, gmin, gcnt, gslot, rep_out, ref_out);
     if (ev1)
         (void)hipEventRecord(ev1, st);
     return hipGetLastError();
