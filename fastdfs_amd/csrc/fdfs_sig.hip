@@ -191,6 +191,8 @@ __global__ __launch_bounds__(kSegBlock) void crc_seg_kernel(
     const uint32_t *__restrict__ n_dev, const DevTables *__restrict__ tabs, uint32_t *__restrict__ crc_out)
 {
     const uint32_t n = n_dev ? *n_dev : n_host;  // file count, or written by big_plan_kernel
+    if (seg_first[n] == 0)  // nothing to do (e.g. no big file): skip the table fill
+        return;
     // TM 2 (64 KiB conflict-free tables): the reduction tables stay in
     // global memory (24 lookups per segment).  TM 0: everything in LDS.
     constexpr int kD = TM == 2 ? kRep8Dwords : 16 * 256;
