@@ -6,7 +6,10 @@ step = the whole upload-path signature work for the batch
 (fdfs_gpu_sig_batch, FDFS_SIG_HASH: CRC32 + INIT/CALC/FINISH_HASH_CODES4 +
 STORAGE_GEN_FILE_SIGNATURE for every file) followed by the bulk dedup of the
 step's signatures across all ranks (bucket -> RCCL all-to-all -> group ->
-all-to-all back).  Weak scaling: every rank owns its own batch.
+all-to-all back).  Weak scaling: every rank owns its own batch.  The same
+line carries "dedup_100m": config 5's 100M-signature dedup split over the
+run's ranks (strong scaling), so the 1/2/4/8-GPU runs of the default bench
+give the dedup scaling curve too.
 
 Other workloads: --config c3 (MD5 method, 1-4 MiB files), c4 (1 GiB files,
 CRC-only segmented path), c5 (dedup only, 100M signatures, strong scaling).
@@ -210,6 +213,41 @@ def load_valu(config: str, avg_ms: float):
     return None
 
 
+def c5_signatures(total, world, rank, dev):
+    """Config 5's signature set: `total` records, 10% duplicates drawn
+    uniformly from the 90% unique ones (seed 5); every rank derives the same
+    global set and takes its contiguous share.  Returns (sig, gidx)."""
+    per = total // world
+    g = torch.Generator(device=dev)
+    g.manual_seed(5)
+    nu = total - total // 10
+    uniq_idx = torch.randint(0, nu, (total - nu,), generator=g, device=dev)
+    lo, hi = rank * per, (rank + 1) * per if rank < world - 1 else total
+    idx = torch.arange(lo, hi, device=dev, dtype=torch.int64)
+    src = torch.where(idx < nu, idx, uniq_idx[(idx - nu).clamp(min=0, max=max(total - nu - 1, 0))])
+    # signature bytes = fixed mix of the unique id (deterministic, 16 random-looking bytes)
+    sig = torch.zeros((hi - lo, 24), dtype=torch.uint8, device=dev)
+    x = (src * (0x9E3779B97F4A7C15 - (1 << 64))) ^ 0x5DEECE66D
+    for k in range(2):
+        x = x ^ (x >> 31)
+        x = x * 0x7FB5D329728EA185
+        sig[:, 8 + 8 * k: 16 + 8 * k] = x.contiguous().view(torch.uint8).view(-1, 8)
+    sig[:, 5:8] = (src % 251).to(torch.uint8).view(-1, 1)
+    return sig, idx
+
+
+def dedup_strong(ctx, sig, gidx, world, steps, warmup):
+    """Timed dedup steps over one signature set (all ranks): (seconds for
+    `steps`, mean ms of the rank's dedup_group kernels)."""
+    ctx.reserve(0, 2 * sig.shape[0])
+    ctx.set_timing(True)
+    ctx.read_timing(_lib.KERNEL_DEDUP)
+    dt = timed(lambda: dedup_step(ctx, sig, gidx, world), steps, warmup, world)
+    kms, launches = ctx.read_timing(_lib.KERNEL_DEDUP)
+    ctx.set_timing(False)
+    return dt, kms / max(launches, 1)
+
+
 def main():
     args = parse()
     world, rank, local = setup_dist(args)
@@ -294,6 +332,19 @@ def main():
                "crc_variant": "unsigned" if variant else "signed", "align": 16,
                "parallelism": f"dp{world} (files sharded, dedup all-to-all)"}
         res["config"] = cfg
+        if args.config == "c2" and not args.files:
+            # config 5's 100M-record dedup, strong-scaled over the ranks of
+            # this run: the driver's 1/2/4/8-GPU runs of the default bench
+            # give its scaling curve
+            total = 100_000_000
+            sig5, gidx5 = c5_signatures(total, world, rank, dev)
+            st5 = min(args.steps, 5)
+            ddt, dms = dedup_strong(ctx, sig5, gidx5, world, st5, 1)
+            res["dedup_100m"] = {"files_per_s": round(total * st5 / ddt, 1),
+                                 "ms_per_step": round(ddt / st5 * 1e3, 3), "records_total": total,
+                                 "scaling": "strong", "group_kernel_ms_avg": round(dms, 4),
+                                 "workload": "config 5 (10% duplicates), bucket + RCCL all-to-all + group"}
+            del sig5, gidx5
         if rank == 0 and world == 1 and not args.no_cpu_baseline:
             res["cpu_baseline"] = cpu_baseline(data, C.layout(sizes)[0], sizes, method, variant,
                                                args.cpu_seconds, args.cpu_threads)
@@ -305,39 +356,17 @@ def main():
             res["cpu_baseline"] = None
     else:  # c5: dedup only, strong scaling over a fixed 100M-signature set
         total = args.files or 100_000_000
-        per = total // world
-        g = torch.Generator(device=dev)
-        g.manual_seed(5)
-        # every rank derives the same global set; takes its contiguous share
-        nu = total - total // 10
-        uniq_idx = torch.randint(0, nu, (total - nu,), generator=g, device=dev)
-        lo, hi = rank * per, (rank + 1) * per if rank < world - 1 else total
-        idx = torch.arange(lo, hi, device=dev, dtype=torch.int64)
-        src = torch.where(idx < nu, idx, uniq_idx[(idx - nu).clamp(min=0, max=max(total - nu - 1, 0))])
-        # signature bytes = fixed mix of the unique id (deterministic, 16 random-looking bytes)
-        sig = torch.zeros((hi - lo, 24), dtype=torch.uint8, device=dev)
-        x = (src * (0x9E3779B97F4A7C15 - (1 << 64))) ^ 0x5DEECE66D
-        for k in range(2):
-            x = x ^ (x >> 31)
-            x = x * 0x7FB5D329728EA185
-            sig[:, 8 + 8 * k: 16 + 8 * k] = x.contiguous().view(torch.uint8).view(-1, 8)
-        sig[:, 5:8] = (src % 251).to(torch.uint8).view(-1, 1)
-        gidx = idx
-        ctx.reserve(0, 2 * (hi - lo))
-        ctx.set_timing(True)
-        dt = timed(lambda: dedup_step(ctx, sig, gidx, world), args.steps, args.warmup, world)
-        kms, launches = ctx.read_timing(_lib.KERNEL_DEDUP)
-        ctx.set_timing(False)
+        sig, gidx = c5_signatures(total, world, rank, dev)
+        dt, avg_ms = dedup_strong(ctx, sig, gidx, world, args.steps, args.warmup)
         res.update({"metric": METRIC, "value": round(total * args.steps / dt, 1),
                     "unit": "files/s", "ms_per_step": round(dt / args.steps * 1e3, 3),
                     "scaling": "strong",
                     "config": {"workload": "config 5: 100M-file dedup, 10% duplicates, "
                                            "bucket + RCCL all-to-all + hash grouping",
                                "records_total": total, "parallelism": f"dp{world}"}})
-        avg_ms = kms / max(launches, 1)
         # algorithmic bytes per record: the 32-byte row {sig, gidx} read once,
         # rep (8 B) + ref (4 B) written once
-        m = float(hi - lo) if world == 1 else float(total) / world
+        m = float(total) / world
         nb = m * 44.0
         res["roofline"] = {"bound": "hbm", "achieved": round(nb / (avg_ms * 1e-3) / 1e9, 1),
                            "peak": HBM_PEAK_GBS, "unit": "GB/s",

@@ -105,3 +105,19 @@ def test_shard_lpt_balances_and_covers():
 def test_shard_lpt_huge_file_alone():
     parts = shard_lpt(np.array([1 << 30, 10, 10, 10]), 2)
     assert [len(p) for p in parts] in ([1, 3], [3, 1])
+
+
+@pytest.mark.parametrize("world", [2, 3, 8])
+def test_c5_signature_shares(world):
+    """bench.py's config-5 set: the ranks' contiguous shares concatenate to
+    the one-rank set (what the strong-scaled dedup line relies on), with
+    10% of the records duplicating earlier unique ones."""
+    import bench
+    total = 10_000
+    one, gidx1 = bench.c5_signatures(total, 1, 0, torch.device("cpu"))
+    parts = [bench.c5_signatures(total, world, r, torch.device("cpu")) for r in range(world)]
+    assert torch.equal(torch.cat([p[0] for p in parts]), one)
+    assert torch.equal(torch.cat([p[1] for p in parts]), gidx1)
+    assert torch.equal(gidx1, torch.arange(total))
+    uniq = np.unique(one.numpy(), axis=0).shape[0]
+    assert uniq <= total - total // 10 and uniq > total * 0.85
