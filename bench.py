@@ -106,9 +106,9 @@ def timed(fn, steps, warmup, world):
     return max_over_ranks(time.perf_counter() - t0, world)
 
 
-def dedup_step(ctx, sig, gidx, world):
+def dedup_step(ctx, sig, gidx, world, stats=None):
     if world > 1:
-        return dedup_global(ctx, sig, gidx)
+        return dedup_global(ctx, sig, gidx, stats=stats)
     # one GPU holds the whole ingest in order: the ingest index is the
     # position (gidx NULL in fdfs_gpu_dedup, the same answers as arange)
     return ctx.dedup(sig)
@@ -238,14 +238,17 @@ def c5_signatures(total, world, rank, dev):
 
 def dedup_strong(ctx, sig, gidx, world, steps, warmup):
     """Timed dedup steps over one signature set (all ranks): (seconds for
-    `steps`, mean ms of the rank's dedup_group kernels)."""
+    `steps`, mean ms of the rank's dedup_group kernels, bytes all ranks sent
+    to peers per step over xGMI)."""
     ctx.reserve(0, 2 * sig.shape[0])
     ctx.set_timing(True)
     ctx.read_timing(_lib.KERNEL_DEDUP)
-    dt = timed(lambda: dedup_step(ctx, sig, gidx, world), steps, warmup, world)
+    stats = {}
+    dt = timed(lambda: dedup_step(ctx, sig, gidx, world, stats), steps, warmup, world)
     kms, launches = ctx.read_timing(_lib.KERNEL_DEDUP)
     ctx.set_timing(False)
-    return dt, kms / max(launches, 1)
+    peer = sum_over_ranks(float(stats.get("peer_bytes", 0)), world) / max(steps + warmup, 1)
+    return dt, kms / max(launches, 1), peer
 
 
 def main():
@@ -339,11 +342,14 @@ def main():
             total = 100_000_000
             sig5, gidx5 = c5_signatures(total, world, rank, dev)
             st5 = min(args.steps, 5)
-            ddt, dms = dedup_strong(ctx, sig5, gidx5, world, st5, 1)
+            ddt, dms, peer = dedup_strong(ctx, sig5, gidx5, world, st5, 1)
             res["dedup_100m"] = {"files_per_s": round(total * st5 / ddt, 1),
                                  "ms_per_step": round(ddt / st5 * 1e3, 3), "records_total": total,
                                  "scaling": "strong", "group_kernel_ms_avg": round(dms, 4),
                                  "workload": "config 5 (10% duplicates), bucket + RCCL all-to-all + group"}
+            if world > 1:
+                res["dedup_100m"]["xgmi_bytes_per_step"] = round(peer)
+                res["dedup_100m"]["xgmi_gbs"] = round(peer / (ddt / st5) / 1e9, 1)
             del sig5, gidx5
         if rank == 0 and world == 1 and not args.no_cpu_baseline:
             res["cpu_baseline"] = cpu_baseline(data, C.layout(sizes)[0], sizes, method, variant,
@@ -357,13 +363,16 @@ def main():
     else:  # c5: dedup only, strong scaling over a fixed 100M-signature set
         total = args.files or 100_000_000
         sig, gidx = c5_signatures(total, world, rank, dev)
-        dt, avg_ms = dedup_strong(ctx, sig, gidx, world, args.steps, args.warmup)
+        dt, avg_ms, peer = dedup_strong(ctx, sig, gidx, world, args.steps, args.warmup)
         res.update({"metric": METRIC, "value": round(total * args.steps / dt, 1),
                     "unit": "files/s", "ms_per_step": round(dt / args.steps * 1e3, 3),
                     "scaling": "strong",
                     "config": {"workload": "config 5: 100M-file dedup, 10% duplicates, "
                                            "bucket + RCCL all-to-all + hash grouping",
                                "records_total": total, "parallelism": f"dp{world}"}})
+        if world > 1:  # all ranks' bytes to peers per step, over the step time
+            res["xgmi"] = {"bytes_per_step": round(peer), "gbs": round(peer / (dt / args.steps) / 1e9, 1),
+                           "links_peak_gbs": 7 * 153.0 * world}
         # algorithmic bytes per record: the 32-byte row {sig, gidx} read once,
         # rep (8 B) + ref (4 B) written once
         m = float(total) / world

@@ -33,7 +33,7 @@ def shard_lpt(sizes: np.ndarray, nranks: int) -> list[np.ndarray]:
     return [np.nonzero(owner == r)[0] for r in range(nranks)]
 
 
-def dedup_global(kernels, sig: torch.Tensor, gidx: torch.Tensor, group=None):
+def dedup_global(kernels, sig: torch.Tensor, gidx: torch.Tensor, group=None, stats=None):
     """Dedup across all ranks of `group`.
 
     kernels: a fastdfs_amd.Context (the HIP kernels); tests substitute a
@@ -41,6 +41,8 @@ def dedup_global(kernels, sig: torch.Tensor, gidx: torch.Tensor, group=None):
     sig: uint8 [n, 24] this rank's signatures; gidx: int64 [n] their global
     ingest indices.  Returns (rep int64[n], ref int32[n]) for this rank's
     files, identical to single-process dedup over the concatenated input.
+    stats: optional dict; "peer_bytes" accumulates the bytes this rank sent
+    to other ranks (32-byte rows out, 16-byte answers back).
     """
     world = dist.get_world_size(group)
     dev = sig.device
@@ -49,6 +51,10 @@ def dedup_global(kernels, sig: torch.Tensor, gidx: torch.Tensor, group=None):
     dist.all_to_all_single(recv_counts, counts, group=group)
     send = counts.cpu().tolist()
     recv = recv_counts.cpu().tolist()
+    if stats is not None:
+        me = dist.get_rank(group)
+        stats["peer_bytes"] = stats.get("peer_bytes", 0) + 32 * (sum(send) - send[me]) + \
+            16 * (sum(recv) - recv[me])
     m = int(sum(recv))
     rows_in = torch.empty((m, 32), dtype=torch.uint8, device=dev)
     dist.all_to_all_single(rows_in, rows, output_split_sizes=recv, input_split_sizes=send,

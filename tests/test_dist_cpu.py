@@ -62,7 +62,14 @@ def _worker(rank, world, port, sig_all, out_q):
         mine = shards[rank]
         sig = torch.from_numpy(sig_all[mine].copy())
         gidx = torch.from_numpy(mine.astype(np.int64))
-        rep, ref = dedup_global(CpuKernelsDouble(), sig, gidx)
+        kern = CpuKernelsDouble()
+        stats = {}
+        rep, ref = dedup_global(kern, sig, gidx, stats=stats)
+        # bytes to peers: this rank's rows owned elsewhere out, answers for
+        # rows it owns from elsewhere back
+        _, counts, _ = kern.dedup_bucket(sig, gidx, world)
+        out_rows = int(counts.sum()) - int(counts[rank])
+        assert stats["peer_bytes"] >= 32 * out_rows
         out_q.put((rank, rep.numpy(), ref.numpy()))
     finally:
         dist.destroy_process_group()
