@@ -322,6 +322,9 @@ def main():
                            "algorithmic_bytes_per_launch": nbytes}
         if tsrc:
             res["roofline"]["traffic_source"] = tsrc
+        if args.config == "c1":
+            res["roofline"]["note"] = ("bound by the lane-serial ELFHash of the ten 100 MB files (one wave "
+                                       "issues ~1 VALU instruction per 8.5 cycles), not by HBM; DESIGN.md §7")
         valu = load_valu(args.config, avg_ms)
         if valu:
             res["valu"] = valu
