@@ -38,7 +38,9 @@
 
 namespace fdfs {
 
-constexpr int kHashBlock = 512;
+// 256 threads: four workgroups (33 KB of tables each) per CU at 4 waves per
+// SIMD; 512-thread workgroups ran 4 % slower (profiles/r01/hash_block_ab.txt).
+constexpr int kHashBlock = 256;
 
 typedef int i32x4 __attribute__((ext_vector_type(4)));
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
