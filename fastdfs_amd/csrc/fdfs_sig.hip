@@ -318,25 +318,31 @@ __global__ void bin_hist_kernel(const uint64_t *__restrict__ sizes, uint32_t n,
             atomicAdd(&hist[b], h[b]);
 }
 
-// Descending exclusive scan of the bin histogram (one block of kSizeBins threads / 2).
+// Descending exclusive scan of the bin histogram (one block of kSizeBins / 2
+// threads, two bins each: wave shuffles, then the waves' totals).
 __global__ __launch_bounds__(1024) void bin_scan_kernel(const uint32_t *__restrict__ hist,
                                                         uint32_t *__restrict__ cursor)
 {
-    __shared__ uint32_t s[kSizeBins];
-    for (int b = threadIdx.x; b < kSizeBins; b += blockDim.x)
-        s[b] = hist[kSizeBins - 1 - b];  // reversed: largest bin first
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        uint32_t run = 0;
-        for (int b = 0; b < kSizeBins; b++) {
-            const uint32_t c = s[b];
-            s[b] = run;
-            run += c;
-        }
+    static_assert(kSizeBins == 2 * 1024, "two bins per thread");
+    __shared__ uint32_t wsum[16];
+    const int t = threadIdx.x, lane = t & 63, wid = t >> 6;
+    // thread t owns reversed positions 2t, 2t + 1 (largest bin first)
+    const uint32_t a = hist[kSizeBins - 1 - 2 * t], b = hist[kSizeBins - 2 - 2 * t];
+    uint32_t x = a + b;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t y = __shfl_up(x, o);
+        if (lane >= o)
+            x += y;
     }
+    if (lane == 63)
+        wsum[wid] = x;
     __syncthreads();
-    for (int b = threadIdx.x; b < kSizeBins; b += blockDim.x)
-        cursor[kSizeBins - 1 - b] = s[b];
+    uint32_t run = x - (a + b);
+    for (int k = 0; k < wid; k++)
+        run += wsum[k];
+    cursor[kSizeBins - 1 - 2 * t] = run;
+    cursor[kSizeBins - 2 - 2 * t] = run + a;
 }
 
 __global__ __launch_bounds__(1024) void bin_scatter_kernel(const uint64_t *__restrict__ sizes,
