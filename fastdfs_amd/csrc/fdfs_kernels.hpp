@@ -10,7 +10,7 @@ struct DevTables;
 constexpr uint64_t kSegBytes = 64 * 1024;  // CRC segment owned by one wave
 constexpr int kSegBlock = 512;             // threads per crc_seg_kernel workgroup
 constexpr int kSizeBins = 2048;            // size bins of the lane-path counting sort
-constexpr int kLaneWsDwords = 2 * kSizeBins;  // size-bin histogram + cursors
+constexpr int kLaneWsDwords = 2 * kSizeBins + 64;  // size-bin histogram + cursors + MD5 chunk queue
 
 // signature path (fdfs_sig.hip)
 uint64_t scan_workspace_elems(uint64_t n);
@@ -40,7 +40,7 @@ hipError_t launch_crc_seg(bool sar, const uint8_t *base, const uint64_t *offs, c
                           hipEvent_t ev0, hipEvent_t ev1);
 hipError_t launch_md5_stage(bool sar, const uint8_t *base, const uint64_t *offs,
                             const uint64_t *sizes, uint32_t n, const uint32_t *order,
-                            const DevTables *tabs, uint32_t *crc_out, uint8_t *sig_out,
+                            const DevTables *tabs, uint32_t *queue, uint32_t *crc_out, uint8_t *sig_out,
                             int32_t *codes_out, hipStream_t st);
 hipError_t launch_sig_hash(bool sar, const uint8_t *base, const uint64_t *offs,
                            const uint64_t *sizes, uint32_t n, const uint32_t *order,

@@ -211,8 +211,8 @@ template <bool SAR>
 __global__ __launch_bounds__(64 * kMd5Waves) void md5_stage_kernel(
     const uint8_t *__restrict__ base, const uint64_t *__restrict__ offs,
     const uint64_t *__restrict__ sizes, const uint32_t *__restrict__ order, uint32_t n,
-    const DevTables *__restrict__ tabs, uint32_t w1, uint32_t *__restrict__ crc_out,
-    uint8_t *__restrict__ sig_out, int32_t *__restrict__ codes_out)
+    const DevTables *__restrict__ tabs, uint32_t w1, uint32_t *__restrict__ queue,
+    uint32_t *__restrict__ crc_out, uint8_t *__restrict__ sig_out, int32_t *__restrict__ codes_out)
 {
     constexpr int CH = kMd5Chunk;
     constexpr int PIECES = CH / 16;   // 16-byte pieces of one file's chunk
@@ -235,15 +235,31 @@ __global__ __launch_bounds__(64 * kMd5Waves) void md5_stage_kernel(
     // that holds the most bytes: the first `w1` waves (one workgroup per
     // CU) take the largest chunks and the rest take the remaining chunks
     // smallest first, so a CU's second workgroup is a light one.
+    //
+    // With a queue (the default) the grid is one workgroup per CU, one wave
+    // per SIMD, and each wave takes the next chunk from a device counter
+    // until none is left: the first chunks taken are the largest, and the
+    // rest go to the waves whose chunks end first, so small files run in the
+    // time the largest ones take instead of beside them (fewer files stream
+    // at once while the longest chains run).
     const uint32_t nw = (n + 63) / 64;
-    const uint32_t w = blockIdx.x * kMd5Waves + (threadIdx.x >> 6);
-    if (w >= nw)
-        return;
-    const uint32_t chunk = (w < w1) ? w : nw - 1 - (w - w1);
-    const uint32_t wave0 = chunk * 64;
     uint8_t *tile = sbuf[threadIdx.x >> 6];
     const uint8_t *safe = reinterpret_cast<const uint8_t *>(tabs);  // >= 16 readable bytes
     const uint32_t K16 = tabs->t.K16;
+    uint32_t chunk;
+    if (queue) {
+        uint32_t c0 = 0;
+        if (lane == 0)
+            c0 = atomicAdd(queue, 1u);
+        chunk = __shfl(c0, 0);
+    } else {
+        const uint32_t w = blockIdx.x * kMd5Waves + (threadIdx.x >> 6);
+        chunk = (w < w1) ? w : nw - 1 - (w - w1);
+        if (w >= nw)
+            chunk = nw;
+    }
+    for (; chunk < nw;) {
+    const uint32_t wave0 = chunk * 64;
     const uint32_t i = wave0 + lane;
     const bool valid = i < n;
     const uint32_t f = valid ? order[i] : 0;
@@ -330,22 +346,29 @@ __global__ __launch_bounds__(64 * kMd5Waves) void md5_stage_kernel(
             block(load16(q, false), load16(q + 16, false), load16(q + 32, false), load16(q + 48, false));
         }
     }
-    if (!valid)
-        return;
-    for (uint64_t k = nblk << 6; k < L; k++)  // CRC of the L & 63 tail bytes
-        c = crc_byte<SAR>(sT, c, p[k]);
-    md5_finish(st, p, nblk, L);
-    crc_out[f] = c ^ 0xFFFFFFFFu;  // CRC32_FINAL (storage/storage_dio.c:500)
-    if (sig_out)  // memcpy(sig + 8, md5 digest, 16) (storage/storage_service.c:119)
-        store_sig(sig_out + 24ull * f, L, st[0], st[1], st[2], st[3]);
-    if (codes_out)
-        reinterpret_cast<int4 *>(codes_out)[f] =
-            make_int4((int)st[0], (int)st[1], (int)st[2], (int)st[3]);
+    if (valid) {
+        for (uint64_t k = nblk << 6; k < L; k++)  // CRC of the L & 63 tail bytes
+            c = crc_byte<SAR>(sT, c, p[k]);
+        md5_finish(st, p, nblk, L);
+        crc_out[f] = c ^ 0xFFFFFFFFu;  // CRC32_FINAL (storage/storage_dio.c:500)
+        if (sig_out)  // memcpy(sig + 8, md5 digest, 16) (storage/storage_service.c:119)
+            store_sig(sig_out + 24ull * f, L, st[0], st[1], st[2], st[3]);
+        if (codes_out)
+            reinterpret_cast<int4 *>(codes_out)[f] =
+                make_int4((int)st[0], (int)st[1], (int)st[2], (int)st[3]);
+    }
+    if (!queue)
+        break;
+    uint32_t c1 = 0;
+    if (lane == 0)
+        c1 = atomicAdd(queue, 1u);
+    chunk = __shfl(c1, 0);
+    }
 }
 
 hipError_t launch_md5_stage(bool sar, const uint8_t *base, const uint64_t *offs,
                             const uint64_t *sizes, uint32_t n, const uint32_t *order,
-                            const DevTables *tabs, uint32_t *crc_out, uint8_t *sig_out,
+                            const DevTables *tabs, uint32_t *queue, uint32_t *crc_out, uint8_t *sig_out,
                             int32_t *codes_out, hipStream_t st)
 {
     static int ncu[64];
@@ -358,21 +381,27 @@ hipError_t launch_md5_stage(bool sar, const uint8_t *base, const uint64_t *offs,
     if (ncu[dev] == 0 &&
         (e = hipDeviceGetAttribute(&ncu[dev], hipDeviceAttributeMultiprocessorCount, dev)) != hipSuccess)
         return e;
-    static int onewg = -1;
-    if (onewg < 0) {  // A/B: FDFS_GPU_MD5_ONEWG=1 -> one workgroup per CU, plain largest-first
-        const char *ev = getenv("FDFS_GPU_MD5_ONEWG");
-        onewg = ev ? atoi(ev) : 0;
+    static int mode = -1;
+    if (mode < 0) {  // A/B: FDFS_GPU_MD5_QUEUE=0 -> one chunk per wave, all waves resident
+        const char *ev = getenv("FDFS_GPU_MD5_QUEUE");
+        mode = ev ? atoi(ev) : 1;
     }
     constexpr unsigned kBlk = 64 * kMd5Waves;
-    const unsigned grid = (n + kBlk - 1) / kBlk;
-    const uint32_t w1 = onewg ? 0xFFFFFFFFu : (uint32_t)ncu[dev] * kMd5Waves;
-    const size_t dyn = onewg ? 64 * 1024 : 0;  // LDS the kernel does not touch: 1 workgroup per CU
+    const uint32_t nw = (n + 63) / 64;
+    unsigned grid = (n + kBlk - 1) / kBlk;
+    uint32_t *q = nullptr;
+    if (mode && queue) {  // queue zeroed by the caller (launch_sig_lane's workspace memset)
+        q = queue;
+        const unsigned g = (unsigned)ncu[dev];
+        grid = g < (nw + kMd5Waves - 1) / kMd5Waves ? g : (nw + kMd5Waves - 1) / kMd5Waves;
+    }
+    const uint32_t w1 = (uint32_t)ncu[dev] * kMd5Waves;
     if (sar)
-        md5_stage_kernel<true><<<grid, kBlk, dyn, st>>>(base, offs, sizes, order, n, tabs, w1, crc_out,
-                                                        sig_out, codes_out);
+        md5_stage_kernel<true><<<grid, kBlk, 0, st>>>(base, offs, sizes, order, n, tabs, w1, q, crc_out,
+                                                      sig_out, codes_out);
     else
-        md5_stage_kernel<false><<<grid, kBlk, dyn, st>>>(base, offs, sizes, order, n, tabs, w1, crc_out,
-                                                         sig_out, codes_out);
+        md5_stage_kernel<false><<<grid, kBlk, 0, st>>>(base, offs, sizes, order, n, tabs, w1, q, crc_out,
+                                                       sig_out, codes_out);
     return hipGetLastError();
 }
 

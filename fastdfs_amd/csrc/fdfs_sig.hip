@@ -582,7 +582,7 @@ hipError_t launch_sig_lane(bool sar, int method, const uint8_t *base, const uint
                            uint8_t *sig_out, int32_t *codes_out, unsigned seg_grid, hipStream_t st,
                            hipEvent_t ev0, hipEvent_t ev1)
 {
-    hipError_t e = hipMemsetAsync(hist, 0, sizeof(uint32_t) * kSizeBins * 2, st);
+    hipError_t e = hipMemsetAsync(hist, 0, sizeof(uint32_t) * kLaneWsDwords, st);
     if (e != hipSuccess)
         return e;
     uint32_t *cursor = hist + kSizeBins;
@@ -603,8 +603,8 @@ hipError_t launch_sig_lane(bool sar, int method, const uint8_t *base, const uint
     }
     if (ev0)
         (void)hipEventRecord(ev0, st);
-    e = (method == 2) ? launch_md5_stage(sar, base, offs, sizes, n, order, tabs, crc_out, sig_out,
-                                         codes_out, st)
+    e = (method == 2) ? launch_md5_stage(sar, base, offs, sizes, n, order, tabs, hist + 2 * kSizeBins,
+                                         crc_out, sig_out, codes_out, st)
                       : launch_sig_hash(sar, base, offs, sizes, n, order, tabs,
                                         offload ? kBigCrcMin : ~0ull, crc_out, sig_out, codes_out, st);
     if (e != hipSuccess)
