@@ -169,3 +169,32 @@ def test_misaligned_records_rejected(ctx):
     with pytest.raises(FdfsGpuError) as ei:
         ctx.dedup_bucket(buf[4:4 + 24 * 100], None, 2)
     assert ei.value.errno == errno.EINVAL
+
+
+def test_dedup_global_rccl_one_rank(oracle, ctx):
+    """dedup_global over a real RCCL group (one rank on this box): the three
+    all-to-alls run on the HIP kernels' device tensors, with the exact dtypes
+    and split sizes the multi-GPU bench uses, and the answer equals the
+    single-GPU dedup.  Ranks > 1 are covered by the gloo tests."""
+    import socket
+    import torch.distributed as dist
+    from fastdfs_amd.dist import dedup_global
+
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    dist.init_process_group("nccl", init_method=f"tcp://127.0.0.1:{port}", rank=0, world_size=1,
+                            device_id=torch.device("cuda", 0))
+    try:
+        sig = torch.from_numpy(_sigs(100_000, 60_000, 11)).cuda()
+        gidx = torch.arange(sig.shape[0], dtype=torch.int64, device="cuda")
+        stats = {}
+        rep, ref = dedup_global(ctx, sig, gidx, stats=stats)
+        torch.cuda.synchronize()
+        orep, oref = oracle.dedup(sig.cpu().numpy())
+        assert np.array_equal(rep.cpu().numpy(), orep.astype(np.int64))
+        assert np.array_equal(ref.cpu().numpy(), oref.astype(np.int32))
+        assert stats["peer_bytes"] == 0
+    finally:
+        dist.destroy_process_group()
