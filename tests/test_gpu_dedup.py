@@ -198,3 +198,17 @@ def test_dedup_global_rccl_one_rank(oracle, ctx):
         assert stats["peer_bytes"] == 0
     finally:
         dist.destroy_process_group()
+
+
+def test_empty_batch(ctx):
+    """A rank with no files: dedup, bucket and group all return empty results
+    (bucket counts zeroed) without launching a zero-size grid."""
+    sig = torch.empty((0, 24), dtype=torch.uint8, device="cuda")
+    rep, ref = ctx.dedup(sig)
+    assert rep.numel() == 0 and ref.numel() == 0
+    rows, counts, row_of = ctx.dedup_bucket(sig, torch.empty(0, dtype=torch.int64, device="cuda"), 4)
+    assert rows.shape == (0, 32) and row_of.numel() == 0
+    assert counts.cpu().tolist() == [0, 0, 0, 0]
+    rep, ref = ctx.dedup_group(rows)
+    torch.cuda.synchronize()
+    assert rep.numel() == 0 and ref.numel() == 0
