@@ -10,6 +10,12 @@ import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "lib", "libfdfs_gpu.so")
+# Measurement scripts (scripts/) may point this at the probe build
+# (`make -C fastdfs_amd/csrc probes` -> lib/probes/libfdfs_gpu.so, whose
+# FDFS_GPU_* knobs change results); the production library reads no
+# environment.
+if os.environ.get("FDFS_GPU_PROBE_LIB") == "1":
+    LIB_PATH = os.path.join(_HERE, "lib", "probes", "libfdfs_gpu.so")
 HEADER_PATH = os.path.join(os.path.dirname(_HERE), "include", "fdfs_gpu.h")
 
 SIG_CRC_ONLY = 0

@@ -45,6 +45,41 @@ def _check_dev(t: torch.Tensor, name: str, dtype=None):
         raise ValueError(f"{name} must be {dtype}, got {t.dtype}")
 
 
+_U32_MAX = 0xFFFFFFFF
+
+
+def _check_batch(data: torch.Tensor, offsets: torch.Tensor, sizes: torch.Tensor, check_bounds: bool):
+    """Batch shape checks before any device pointer reaches a kernel: n fits
+    the C ABI's uint32 count, offsets/sizes pair up, and (check_bounds, one
+    device reduction + sync) every file lies inside `data`."""
+    _check_dev(data, "data", torch.uint8)
+    _check_dev(offsets, "offsets", torch.int64)
+    _check_dev(sizes, "sizes", torch.int64)
+    n = offsets.numel()
+    if sizes.numel() != n:
+        raise ValueError("offsets and sizes differ in length")
+    if n > _U32_MAX:
+        raise ValueError(f"batch of {n} files exceeds the uint32 count of fdfs_gpu_batch")
+    if check_bounds and n:
+        lo = int(torch.minimum(offsets.min(), sizes.min()).item())
+        hi = int((offsets + sizes).max().item())
+        if lo < 0 or hi > data.numel():
+            raise ValueError(f"file range [{lo}, {hi}) outside data of {data.numel()} bytes")
+    return n
+
+
+def _check_sig(sig: torch.Tensor, gidx: torch.Tensor | None, width: int = 24) -> int:
+    _check_dev(sig, "sig", torch.uint8)
+    if sig.dim() != 2 or sig.shape[1] != width:
+        raise ValueError(f"sig must be uint8[n, {width}], got {tuple(sig.shape)}")
+    n = sig.shape[0]
+    if gidx is not None:
+        _check_dev(gidx, "gidx", torch.int64)
+        if gidx.numel() != n:
+            raise ValueError(f"gidx has {gidx.numel()} entries for {n} records")
+    return n
+
+
 class Context:
     """A libfdfs_gpu context on one HIP device.
 
@@ -98,19 +133,17 @@ class Context:
     def sig_batch(self, data: torch.Tensor, offsets: torch.Tensor, sizes: torch.Tensor,
                   method: int = SIG_HASH, crc_out: torch.Tensor | None = None,
                   sig_out: torch.Tensor | None = None, codes_out: torch.Tensor | None = None,
-                  want_sig: bool = True, want_codes: bool = False, stream=None):
+                  want_sig: bool = True, want_codes: bool = False, stream=None,
+                  check_bounds: bool = True):
         """CRC32 (+ 24-byte signature for SIG_HASH / SIG_MD5) of every file.
 
         data: uint8 device tensor; offsets/sizes: int64 device tensors [n].
         Returns (crc int32[n] holding the uint32 bit pattern, sig uint8[n,24]
-        or None, codes int32[n,4] or None).
+        or None, codes int32[n,4] or None).  check_bounds verifies that every
+        file lies inside `data` (one reduction + sync); callers that build
+        the layout themselves (bench.py) turn it off.
         """
-        _check_dev(data, "data", torch.uint8)
-        _check_dev(offsets, "offsets", torch.int64)
-        _check_dev(sizes, "sizes", torch.int64)
-        n = offsets.numel()
-        if sizes.numel() != n:
-            raise ValueError("offsets and sizes differ in length")
+        n = _check_batch(data, offsets, sizes, check_bounds)
         dev = data.device
         if crc_out is None:
             crc_out = torch.empty(n, dtype=torch.int32, device=dev)
@@ -160,10 +193,7 @@ class Context:
 
     def dedup(self, sig: torch.Tensor, gidx: torch.Tensor | None = None, stream=None):
         """rep int64[n] (first ingest index of the class), ref int32[n] (class size)."""
-        _check_dev(sig, "sig", torch.uint8)
-        n = sig.numel() // 24
-        if gidx is not None:
-            _check_dev(gidx, "gidx", torch.int64)
+        n = _check_sig(sig, gidx)
         rep = torch.empty(n, dtype=torch.int64, device=sig.device)
         ref = torch.empty(n, dtype=torch.int32, device=sig.device)
         self._rc(self._L.fdfs_gpu_dedup(self._h, sig.data_ptr(), _ptr(gidx), n, rep.data_ptr(),
@@ -172,10 +202,9 @@ class Context:
 
     def dedup_bucket(self, sig: torch.Tensor, gidx: torch.Tensor | None, nranks: int, stream=None):
         """Pack {sig, gidx} rows by owner rank: (rows uint8[n,32], counts int64[nranks], row_of int64[n])."""
-        _check_dev(sig, "sig", torch.uint8)
-        n = sig.numel() // 24
-        if gidx is not None:
-            _check_dev(gidx, "gidx", torch.int64)
+        n = _check_sig(sig, gidx)
+        if not 1 <= nranks <= 64:
+            raise ValueError("nranks must be in [1, 64]")
         rows = torch.empty((n, 32), dtype=torch.uint8, device=sig.device)
         counts = torch.empty(nranks, dtype=torch.int64, device=sig.device)
         row_of = torch.empty(n, dtype=torch.int64, device=sig.device)
@@ -186,8 +215,7 @@ class Context:
 
     def dedup_group(self, rows: torch.Tensor, stream=None):
         """Owner-side grouping of 32-byte rows: (rep int64[m], ref int32[m])."""
-        _check_dev(rows, "rows", torch.uint8)
-        m = rows.numel() // 32
+        m = _check_sig(rows, None, 32)
         rep = torch.empty(m, dtype=torch.int64, device=rows.device)
         ref = torch.empty(m, dtype=torch.int32, device=rows.device)
         self._rc(self._L.fdfs_gpu_dedup_group(self._h, rows.data_ptr(), m, rep.data_ptr(),
@@ -310,11 +338,10 @@ class Context:
     def scrub(self, data: torch.Tensor, offsets: torch.Tensor, sizes: torch.Tensor,
               expected_crc: torch.Tensor, stream=None):
         """Recompute every file's CRC32 and compare: (crc int32[n], bad uint8[n], nbad int32[1])."""
-        _check_dev(data, "data", torch.uint8)
-        _check_dev(offsets, "offsets", torch.int64)
-        _check_dev(sizes, "sizes", torch.int64)
+        n = _check_batch(data, offsets, sizes, True)
         _check_dev(expected_crc, "expected_crc", torch.int32)
-        n = offsets.numel()
+        if expected_crc.numel() != n:
+            raise ValueError("one expected CRC per file")
         dev = data.device
         crc = torch.empty(n, dtype=torch.int32, device=dev)
         bad = torch.empty(n, dtype=torch.uint8, device=dev)

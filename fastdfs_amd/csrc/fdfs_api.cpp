@@ -7,6 +7,7 @@
 #include <cerrno>
 #include <cstdio>
 #include <cstring>
+#include <mutex>
 #include <new>
 #include <vector>
 
@@ -33,6 +34,15 @@ struct fdfs_gpu_ctx {
     std::vector<hipEvent_t> pool;
     double acc_ms[4] = {0, 0, 0, 0};
     uint64_t acc_n[4] = {0, 0, 0, 0};
+    // One call at a time per context (host threads serialise here; entry
+    // points that call other entry points re-enter on the same thread).
+    std::recursive_mutex mu;
+    // The workspace is shared by every call: ws_ev is recorded on the stream
+    // of the last call that used it, and a call on another stream waits for
+    // it first, so calls on different streams never overlap on ws.
+    hipEvent_t ws_ev = nullptr;
+    hipStream_t ws_st = nullptr;
+    bool ws_rec = false;
 };
 
 namespace {
@@ -89,20 +99,52 @@ size_t sig_ws_bytes(uint64_t n)
 
 size_t dedup_ws_bytes(uint64_t n) { return fdfs::dedup_ws_bytes(n) + align_up(8 * 64); }
 
+bool capturing(hipStream_t st)
+{
+    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+    return hipStreamIsCapturing(st, &cs) == hipSuccess && cs != hipStreamCaptureStatusNone;
+}
+
+// Workspace ordering across streams (see fdfs_gpu_ctx::ws_ev).  Inside a
+// stream capture nothing is recorded or waited on: a captured sequence must
+// use one stream (include/fdfs_gpu.h).
+void ws_enter(fdfs_gpu_ctx *ctx, hipStream_t st)
+{
+    if (ctx->ws_rec && ctx->ws_st != st && !capturing(st))
+        (void)hipStreamWaitEvent(st, ctx->ws_ev, 0);
+}
+
+void ws_leave(fdfs_gpu_ctx *ctx, hipStream_t st)
+{
+    if (!capturing(st) && hipEventRecord(ctx->ws_ev, st) == hipSuccess) {
+        ctx->ws_st = st;
+        ctx->ws_rec = true;
+    }
+}
+
+struct WsScope {
+    fdfs_gpu_ctx *ctx;
+    hipStream_t st;
+    WsScope(fdfs_gpu_ctx *c, hipStream_t s) : ctx(c), st(s) { ws_enter(c, s); }
+    ~WsScope() { ws_leave(ctx, st); }
+};
+
 int ensure_ws(fdfs_gpu_ctx *ctx, size_t bytes, hipStream_t st)
 {
     if (bytes <= ctx->ws_bytes)
         return 0;
-    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
-    if (hipStreamIsCapturing(st, &cs) == hipSuccess && cs != hipStreamCaptureStatusNone) {
+    if (capturing(st)) {
         std::snprintf(ctx->err, sizeof(ctx->err),
                       "workspace growth needed during stream capture; call fdfs_gpu_reserve first");
         return ENOMEM;
     }
     if (ctx->ws) {
-        hipError_t e = hipStreamSynchronize(st);
+        // the last call that used ws (on any stream) must be done with it
+        hipError_t e = ctx->ws_rec ? hipEventSynchronize(ctx->ws_ev) : hipSuccess;
+        if (e == hipSuccess)
+            e = hipStreamSynchronize(st);
         if (e != hipSuccess)
-            return fail(ctx, e, "hipStreamSynchronize");
+            return fail(ctx, e, "workspace growth sync");
         (void)hipFree(ctx->ws);
         ctx->ws = nullptr;
         ctx->ws_bytes = 0;
@@ -182,13 +224,17 @@ int fdfs_gpu_open(int device, unsigned flags, fdfs_gpu_ctx **out)
         for (int x = 0; x < 256; x++)
             h->Dc[p][x] = h->t.D[p][x ^ 0xFF];
     fdfs::build_poly_mfma_tables(h->pm);
-    hipError_t e = hipMalloc(&ctx->d_tabs, sizeof(fdfs::DevTables));
+    hipError_t e = hipEventCreateWithFlags(&ctx->ws_ev, hipEventDisableTiming);
+    if (e == hipSuccess)
+        e = hipMalloc(&ctx->d_tabs, sizeof(fdfs::DevTables));
     if (e == hipSuccess)
         e = hipMemcpy(ctx->d_tabs, h, sizeof(fdfs::DevTables), hipMemcpyHostToDevice);
     delete h;
     if (e != hipSuccess) {
         if (ctx->d_tabs)
             (void)hipFree(ctx->d_tabs);
+        if (ctx->ws_ev)
+            (void)hipEventDestroy(ctx->ws_ev);
         delete ctx;
         return EIO;
     }
@@ -217,6 +263,8 @@ int fdfs_gpu_close(fdfs_gpu_ctx *ctx)
         (void)hipEventDestroy(e);
     if (ctx->d_tabs)
         (void)hipFree(ctx->d_tabs);
+    if (ctx->ws_ev)
+        (void)hipEventDestroy(ctx->ws_ev);
     delete ctx;
     return 0;
 }
@@ -225,6 +273,7 @@ int fdfs_gpu_reserve(fdfs_gpu_ctx *ctx, uint64_t max_files, uint64_t max_records
 {
     if (!ctx)
         return EINVAL;
+    std::lock_guard<std::recursive_mutex> lk(ctx->mu);
     DeviceGuard g(ctx->device);
     size_t a = sig_ws_bytes(max_files), b = dedup_ws_bytes(max_records);
     return ensure_ws(ctx, a > b ? a : b, nullptr);
@@ -236,6 +285,7 @@ int fdfs_gpu_set_timing(fdfs_gpu_ctx *ctx, int enable)
 {
     if (!ctx)
         return EINVAL;
+    std::lock_guard<std::recursive_mutex> lk(ctx->mu);
     ctx->timing = enable != 0;
     return 0;
 }
@@ -244,6 +294,7 @@ int fdfs_gpu_read_timing(fdfs_gpu_ctx *ctx, int kernel, double *ms_out, uint64_t
 {
     if (!ctx || kernel < 0 || kernel > 3)
         return EINVAL;
+    std::lock_guard<std::recursive_mutex> lk(ctx->mu);
     DeviceGuard g(ctx->device);
     for (auto &r : ctx->recs) {
         float ms = 0.f;
@@ -279,6 +330,7 @@ int fdfs_gpu_sig_batch(fdfs_gpu_ctx *ctx, const fdfs_gpu_batch *batch, int metho
         return 0;
     if (!batch->base || !batch->offset || !batch->size || !crc_out)
         return EINVAL;
+    std::lock_guard<std::recursive_mutex> lk(ctx->mu);
     DeviceGuard g(ctx->device);
     if (!g.ok)
         return ENODEV;
@@ -286,6 +338,7 @@ int fdfs_gpu_sig_batch(fdfs_gpu_ctx *ctx, const fdfs_gpu_batch *batch, int metho
     int rc = ensure_ws(ctx, sig_ws_bytes(n), st);
     if (rc)
         return rc;
+    WsScope wsc(ctx, st);
     Carve cv{static_cast<char *>(ctx->ws)};
     const uint8_t *base = static_cast<const uint8_t *>(batch->base);
     hipError_t e;
@@ -369,6 +422,7 @@ int fdfs_gpu_sig_batch_host(fdfs_gpu_ctx *ctx, const fdfs_gpu_batch *hb, int met
     if (chunk_bytes == 0)
         chunk_bytes = 256ull << 20;
     constexpr uint32_t kMaxChunkFiles = 1u << 20;
+    std::lock_guard<std::recursive_mutex> lk(ctx->mu);
     DeviceGuard g(ctx->device);
     if (!g.ok)
         return ENODEV;
@@ -509,6 +563,7 @@ static int dedup_common(fdfs_gpu_ctx *ctx, const uint8_t *sig, uint32_t stride,
     if ((reinterpret_cast<uintptr_t>(sig) | reinterpret_cast<uintptr_t>(gidx) |
          reinterpret_cast<uintptr_t>(rep_out)) & 7)
         return EINVAL;
+    std::lock_guard<std::recursive_mutex> lk(ctx->mu);
     DeviceGuard g(ctx->device);
     if (!g.ok)
         return ENODEV;
@@ -516,6 +571,7 @@ static int dedup_common(fdfs_gpu_ctx *ctx, const uint8_t *sig, uint32_t stride,
     int rc = ensure_ws(ctx, dedup_ws_bytes(n), st);
     if (rc)
         return rc;
+    WsScope wsc(ctx, st);
     hipEvent_t a, b;
     timing_pair(ctx, FDFS_KERNEL_DEDUP, a, b);
     hipError_t e = fdfs::launch_dedup_group(sig, stride, gidx, gstride, n, ctx->ws, rep_out, ref_out,
@@ -548,6 +604,7 @@ int fdfs_gpu_dedup_bucket(fdfs_gpu_ctx *ctx, const uint8_t *sig, const uint64_t 
     if ((reinterpret_cast<uintptr_t>(sig) | reinterpret_cast<uintptr_t>(gidx) |
          reinterpret_cast<uintptr_t>(records_out) | reinterpret_cast<uintptr_t>(row_of_out)) & 7)
         return EINVAL;  // u64 words
+    std::lock_guard<std::recursive_mutex> lk(ctx->mu);
     DeviceGuard g(ctx->device);
     if (!g.ok)
         return ENODEV;
@@ -555,6 +612,7 @@ int fdfs_gpu_dedup_bucket(fdfs_gpu_ctx *ctx, const uint8_t *sig, const uint64_t 
     int rc = ensure_ws(ctx, align_up(8 * 64), st);
     if (rc)
         return rc;
+    WsScope wsc(ctx, st);
     uint64_t *cursor = static_cast<uint64_t *>(ctx->ws);
     hipEvent_t a, b;
     timing_pair(ctx, FDFS_KERNEL_BUCKET, a, b);
@@ -658,6 +716,7 @@ int fdfs_gpu_fdht_route_keys(fdfs_gpu_ctx *ctx, const uint8_t *keys, uint32_t ke
         return EINVAL;
     if (reinterpret_cast<uintptr_t>(keys) & 3)  // the kernel reads each key as u32 words
         return EINVAL;
+    std::lock_guard<std::recursive_mutex> lk(ctx->mu);
     DeviceGuard g(ctx->device);
     if (!g.ok)
         return ENODEV;
@@ -665,6 +724,7 @@ int fdfs_gpu_fdht_route_keys(fdfs_gpu_ctx *ctx, const uint8_t *keys, uint32_t ke
     int rc = ensure_ws(ctx, align_up(4ull * group_count) + align_up(8ull * group_count), st);
     if (rc)
         return rc;
+    WsScope wsc(ctx, st);
     Carve cv{static_cast<char *>(ctx->ws)};
     uint32_t *gcount = cv.take<uint32_t>(group_count);
     uint64_t *cursor = cv.take<uint64_t>(group_count);
@@ -707,6 +767,7 @@ int fdfs_gpu_recovery_batch(fdfs_gpu_ctx *ctx, const fdfs_gpu_batch *batch, int 
         return EINVAL;
     if ((reinterpret_cast<uintptr_t>(out->sig) | reinterpret_cast<uintptr_t>(out->rep)) & 7)
         return EINVAL;
+    std::lock_guard<std::recursive_mutex> lk(ctx->mu);
     DeviceGuard g(ctx->device);
     if (!g.ok)
         return ENODEV;
@@ -728,6 +789,7 @@ int fdfs_gpu_recovery_batch(fdfs_gpu_ctx *ctx, const fdfs_gpu_batch *batch, int 
     int rc = ensure_ws(ctx, a_bytes + b_bytes, st);
     if (rc)
         return rc;
+    WsScope wsc(ctx, st);
     Carve cv{static_cast<char *>(ctx->ws) + a_bytes};
     uint64_t *flag = cv.take<uint64_t>(n);
     uint64_t *pos = cv.take<uint64_t>(n + 1);
@@ -778,6 +840,7 @@ int fdfs_gpu_scrub(fdfs_gpu_ctx *ctx, const fdfs_gpu_batch *batch, const uint32_
 {
     if (!ctx || !batch || !expected_crc || !crc_out || !bad_out || !nbad_out)
         return EINVAL;
+    std::lock_guard<std::recursive_mutex> lk(ctx->mu);
     int rc = fdfs_gpu_sig_batch(ctx, batch, FDFS_SIG_CRC_ONLY, crc_out, nullptr, nullptr, stream);
     if (rc || batch->n == 0)
         return rc;

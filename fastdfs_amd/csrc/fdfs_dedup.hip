@@ -548,11 +548,15 @@ hipError_t launch_dedup_group(const uint8_t *sig, uint32_t sig_stride, const uin
     dp_scatter_kernel<<<(unsigned)pl.tiles, kDpTileThreads, 0, st>>>(keys, n, pl.d1, pl.tiles, off, ent);
     const uint64_t *parts = ent;
     if (pl.d2) {
+#ifdef FDFS_PROBES
         static int per = -1;
-        if (per < 0) {
+        if (per < 0) {  // A/B (make probes): FDFS_GPU_DEDUP_SPLIT=4 -> 4096-entry chunks
             const char *ev = getenv("FDFS_GPU_DEDUP_SPLIT");
             per = (ev && atoi(ev) == 4) ? 4 : kDpSplitPer;
         }
+#else
+        constexpr int per = kDpSplitPer;
+#endif
         if (per == 4)
             dp_split_kernel<4><<<1u << pl.d1, kDpSplitThreads, 0, st>>>(ent, n, pl.d1, pl.d2, pl.tiles, off,
                                                                      ent2, pstart);

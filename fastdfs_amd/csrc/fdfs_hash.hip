@@ -382,16 +382,23 @@ hipError_t launch_sig_hash(bool sar, const uint8_t *base, const uint64_t *offs,
                            const DevTables *tabs, uint64_t big_min, uint32_t *crc_out, uint8_t *sig_out,
                            int32_t *codes_out, hipStream_t st)
 {
+#ifdef FDFS_PROBES
+    // measurement build only (make probes): FDFS_GPU_HASH_MODE 1 = loads
+    // only, 2 = compute only (wrong results); FDFS_GPU_HASH_TM CRC table form
+    // 0 = slice-by-16 bytes, 2 = rotated rep8
     static int mode = -1;
-    if (mode < 0) {  // FDFS_GPU_HASH_MODE (measurement probes): 1 = loads only, 2 = compute only
+    if (mode < 0) {
         const char *ev = getenv("FDFS_GPU_HASH_MODE");
         mode = ev ? atoi(ev) : 0;
     }
     static int tm = -1;
-    if (tm < 0) {  // FDFS_GPU_HASH_TM: CRC table form, 0 = slice-by-16 bytes, 2 = rotated rep8
+    if (tm < 0) {
         const char *ev = getenv("FDFS_GPU_HASH_TM");
         tm = ev ? atoi(ev) : 0;
     }
+#else
+    constexpr int tm = 0;
+#endif
     const unsigned blk = tm == 2 ? 1024 : kHashBlock;
     const unsigned grid = (n + blk - 1) / blk;
 #define HASH_LAUNCH(S, M)                                                                                \
@@ -403,11 +410,14 @@ hipError_t launch_sig_hash(bool sar, const uint8_t *base, const uint64_t *offs,
             sig_hash_kernel<S, 0, M><<<grid, blk, 0, st>>>(base, offs, sizes, order, n, tabs, big_min, crc_out, \
                                                            sig_out, codes_out);                          \
     } while (0)
+#ifdef FDFS_PROBES
     if (mode == 1)
         HASH_LAUNCH(true, 1);
     else if (mode == 2)
         HASH_LAUNCH(true, 2);
-    else if (sar)
+    else
+#endif
+    if (sar)
         HASH_LAUNCH(true, 0);
     else
         HASH_LAUNCH(false, 0);

@@ -381,11 +381,15 @@ hipError_t launch_md5_stage(bool sar, const uint8_t *base, const uint64_t *offs,
     if (ncu[dev] == 0 &&
         (e = hipDeviceGetAttribute(&ncu[dev], hipDeviceAttributeMultiprocessorCount, dev)) != hipSuccess)
         return e;
+#ifdef FDFS_PROBES
     static int mode = -1;
-    if (mode < 0) {  // A/B: FDFS_GPU_MD5_QUEUE=0 -> one chunk per wave, all waves resident
+    if (mode < 0) {  // A/B (make probes): FDFS_GPU_MD5_QUEUE=0 -> one chunk per wave, all resident
         const char *ev = getenv("FDFS_GPU_MD5_QUEUE");
         mode = ev ? atoi(ev) : 1;
     }
+#else
+    constexpr int mode = 1;
+#endif
     constexpr unsigned kBlk = 64 * kMd5Waves;
     const uint32_t nw = (n + 63) / 64;
     unsigned grid = (n + kBlk - 1) / kBlk;

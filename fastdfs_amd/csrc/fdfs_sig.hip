@@ -658,12 +658,16 @@ hipError_t launch_crc_seg(bool sar, const uint8_t *base, const uint64_t *offs, c
 // plain slice-by-16 (A/B measurement only).
 int crc_table_mode()
 {
+#ifdef FDFS_PROBES
     static int v = -1;
-    if (v < 0) {  // FDFS_GPU_CRC_TABLES=byte: slice-by-16 with bank conflicts (A/B only)
+    if (v < 0) {  // A/B (make probes): FDFS_GPU_CRC_TABLES=byte -> slice-by-16 with bank conflicts
         const char *e = getenv("FDFS_GPU_CRC_TABLES");
         v = (e && e[0] == 'b') ? 0 : 2;
     }
     return v;
+#else
+    return 2;
+#endif
 }
 
 int crc_seg_blocks_per_cu()

@@ -79,7 +79,8 @@ def recovery_records(ctx: Context, data: torch.Tensor, offsets: torch.Tensor, si
         _check_dev(t, nm, dt)
     if servers_per_group is not None:
         _check_dev(servers_per_group, "servers_per_group", torch.int32)
-    n = offsets.numel()
+    from .api import _check_batch
+    n = _check_batch(data, offsets, sizes, True)
     if file_ids.dim() != 2 or file_ids.shape[0] != n or file_id_len.numel() != n:
         raise ValueError("one file id record per file")
     dev = data.device
@@ -100,7 +101,9 @@ def recovery_records(ctx: Context, data: torch.Tensor, offsets: torch.Tensor, si
                                            len(namespace), group_count, _ptr(servers_per_group),
                                            ctypes.byref(out), _stream_handle(stream)),
             "fdfs_gpu_recovery_batch")
-    m = int(nsrc.item())  # synchronises the stream
+    # nsources was written on `stream`, which need not be torch's current one
+    (stream if stream is not None else torch.cuda.current_stream()).synchronize()
+    m = int(nsrc.item())
 
     def routed(st, k):
         return Routed(st[0][:k], st[1][:k], st[2][:k], st[3][:k], st[4][:k], st[5])

@@ -4,7 +4,15 @@
  * duplicate grouping that replaces per-file FastDHT lookups.
  *
  * Plain C types only: device pointers are `const void *` / `void *`, streams
- * are hipStream_t passed as `void *` (NULL = the null stream).  Every call
+ * are hipStream_t passed as `void *` (NULL = the null stream).
+ *
+ * Threading: a context serialises its calls (a mutex; any host thread may
+ * call), and the device workspace it owns is ordered across streams: a call
+ * on stream B starts after the previous call of the context, on stream A,
+ * has finished with it.  Calls stay asynchronous on their stream.  Inside a
+ * hipStream capture this cross-stream ordering is not recorded, so a
+ * captured sequence must use one stream, after fdfs_gpu_reserve.  For
+ * concurrency across dio threads, open one context per thread.  Every call
  * returns 0 or a positive errno value (EINVAL bad arguments, ENOMEM
  * allocation failure, EIO a HIP error), the convention of the reference's
  * storage daemon (e.g. storage/storage_dio.c:443).  Inputs are caller owned
@@ -112,6 +120,60 @@ int fdfs_gpu_sig_batch(fdfs_gpu_ctx *ctx, const fdfs_gpu_batch *batch, int metho
 int fdfs_gpu_sig_batch_host(fdfs_gpu_ctx *ctx, const fdfs_gpu_batch *host_batch, int method,
                             uint32_t *crc_out, uint8_t *sig_out, int32_t *codes_out,
                             uint64_t chunk_bytes);
+
+/* ---- Chunked (state-carrying) form of the same path ---------------------
+ * The storage daemon hashes an upload one received chunk at a time
+ * (<= buff_size, conf/storage.conf:52) and keeps the running values in the
+ * file's StorageFileContext (storage/storage_nio.h:94-96):
+ *     storage_write_to_file   init   (storage/storage_service.c:7147-7161)
+ *     dio_write_file          update (storage/storage_dio.c:465-483)
+ *                             final  (storage/storage_dio.c:498-515)
+ * These three calls are that loop for a batch of uploads at once: each call
+ * advances many files by one chunk each, on the GPU.  The state is a device
+ * array of fdfs_gpu_file_state laid out as StorageFileContext holds it
+ * (int crc32; int file_hash_codes[4]; MD5_CTX {state[4], count[2],
+ * buffer[64]}); it can be saved, moved between calls and streams, and
+ * resumed.  Results equal the one-shot fdfs_gpu_sig_batch over the
+ * concatenated chunks for every chunking. */
+typedef struct {
+    int32_t  crc32;          /* CRC32_ex running value (CRC32_XINIT at init) */
+    int32_t  hash_codes[4];  /* CALC_HASH_CODES4 running values (FDFS_SIG_HASH) */
+    uint32_t md5_state[4];   /* MD5_CTX.state (FDFS_SIG_MD5) */
+    uint32_t md5_count[2];   /* bits hashed so far, low word first (MD5_CTX.count);
+                                kept for every method: the signature's file size */
+    uint8_t  md5_buffer[64]; /* MD5_CTX.buffer: the (count / 8) % 64 pending bytes */
+    uint8_t  reserved[20];
+} fdfs_gpu_file_state;       /* 128 bytes */
+
+/* storage_write_to_file's initialisation of n states (device array):
+ * crc32 = CRC32_XINIT, INIT_HASH_CODES4, my_md5_init, count 0. */
+int fdfs_gpu_state_init(fdfs_gpu_ctx *ctx, fdfs_gpu_file_state *states, uint32_t n, void *stream);
+
+/* dio_write_file's per-chunk update for a batch of chunks (device memory):
+ * chunk i = bytes [base + offset[i], + size[i]) is hashed onto
+ * states[state_idx ? state_idx[i] : i]: CRC32_ex always (as uploads do,
+ * storage/storage_service.c:4533), CALC_HASH_CODES4 for FDFS_SIG_HASH,
+ * my_md5_update for FDFS_SIG_MD5.  A state may appear at most once per call
+ * (the daemon has one chunk of an upload in flight at a time); chunks may
+ * start at any byte and have any length, including 0. */
+int fdfs_gpu_update_batch(fdfs_gpu_ctx *ctx, const fdfs_gpu_batch *chunks, const uint32_t *state_idx,
+                          int method, fdfs_gpu_file_state *states, void *stream);
+
+/* dio_write_file's finalisation for n files: CRC32_FINAL (crc_out[i], the
+ * %u value), FINISH_HASH_CODES4 or my_md5_final, and
+ * STORAGE_GEN_FILE_SIGNATURE with file size = bytes hashed (sig_out[i],
+ * codes_out[i]; either may be NULL) of states[state_idx ? state_idx[i] : i].
+ * The states are not modified. */
+int fdfs_gpu_final_batch(fdfs_gpu_ctx *ctx, const fdfs_gpu_file_state *states,
+                         const uint32_t *state_idx, uint32_t n, int method, uint32_t *crc_out,
+                         uint8_t *sig_out, int32_t *codes_out, void *stream);
+
+/* crc32_combine: out[i] = the CRC32_ex running value of A || B given
+ * crc_a[i] = CRC32_ex(A, init) and crc_b[i] = CRC32_ex(B, 0), with len_b[i] =
+ * |B| (device arrays): M^(8 |B|) crc_a XOR crc_b over GF(2).  Joins the
+ * partial states of one file hashed in pieces on several GPUs. */
+int fdfs_gpu_crc_combine(fdfs_gpu_ctx *ctx, const uint32_t *crc_a, const uint32_t *crc_b,
+                         const uint64_t *len_b, uint32_t n, uint32_t *out, void *stream);
 
 /* Single-GPU duplicate grouping over n records in ingest order.
  *   sig:  device uint8_t[n*24]; gidx: device uint64_t[n] global ingest index

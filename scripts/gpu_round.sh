@@ -37,7 +37,7 @@ done
 step sq_c3 600 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_MFMA GRBM_GUI_ACTIVE -d $O/sq_c3 -o run --output-format csv -- $B --config c3 --steps 1 --warmup 1 || exit $?
 step sq_c2 300 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_MFMA GRBM_GUI_ACTIVE -d $O/sq_c2 -o run --output-format csv -- $B --steps 1 --warmup 1 || exit $?
 for m in 1 2; do
-  FDFS_GPU_HASH_MODE=$m step probe_c2_mode$m 300 $B || exit $?
+  FDFS_GPU_PROBE_LIB=1 FDFS_GPU_HASH_MODE=$m step probe_c2_mode$m 300 $B || exit $?
 done
 fi
 echo done

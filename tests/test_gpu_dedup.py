@@ -164,10 +164,10 @@ def test_misaligned_records_rejected(ctx):
     from fastdfs_amd import FdfsGpuError
     buf = torch.zeros(24 * 100 + 8, dtype=torch.uint8, device="cuda")
     with pytest.raises(FdfsGpuError) as ei:
-        ctx.dedup(buf[1:1 + 24 * 100])
+        ctx.dedup(buf[1:1 + 24 * 100].view(100, 24))
     assert ei.value.errno == errno.EINVAL
     with pytest.raises(FdfsGpuError) as ei:
-        ctx.dedup_bucket(buf[4:4 + 24 * 100], None, 2)
+        ctx.dedup_bucket(buf[4:4 + 24 * 100].view(100, 24), None, 2)
     assert ei.value.errno == errno.EINVAL
 
 
