@@ -46,7 +46,12 @@ EXPORTS = (
     "fdfs_gpu_sig_batch_host",
     "fdfs_gpu_scrub",
     "fdfs_gpu_last_error",
+    "fdfs_gpu_state_init",
+    "fdfs_gpu_update_batch",
+    "fdfs_gpu_final_batch",
+    "fdfs_gpu_crc_combine",
 )
+FILE_STATE_SIZE = 128  # sizeof(fdfs_gpu_file_state)
 KERNEL_SIG_LANE = 0
 KERNEL_CRC_SEG = 1
 KERNEL_DEDUP = 2
@@ -132,5 +137,13 @@ def load() -> ctypes.CDLL:
     L.fdfs_gpu_scrub.argtypes = [vp, ctypes.POINTER(FdfsGpuBatch), vp, vp, vp, vp, vp]
     L.fdfs_gpu_last_error.restype = ctypes.c_char_p
     L.fdfs_gpu_last_error.argtypes = [vp]
+    L.fdfs_gpu_state_init.restype = i32
+    L.fdfs_gpu_state_init.argtypes = [vp, vp, u32, vp]
+    L.fdfs_gpu_update_batch.restype = i32
+    L.fdfs_gpu_update_batch.argtypes = [vp, ctypes.POINTER(FdfsGpuBatch), vp, i32, vp, vp]
+    L.fdfs_gpu_final_batch.restype = i32
+    L.fdfs_gpu_final_batch.argtypes = [vp, vp, vp, u32, i32, vp, vp, vp, vp]
+    L.fdfs_gpu_crc_combine.restype = i32
+    L.fdfs_gpu_crc_combine.argtypes = [vp, vp, vp, vp, u32, vp, vp]
     _lib = L
     return L

@@ -160,6 +160,87 @@ class Context:
                  "fdfs_gpu_sig_batch")
         return crc_out, sig_out, codes_out
 
+    # ------------------------------------------- chunked (state-carrying) form
+    def new_states(self, n: int, device=None, stream=None) -> torch.Tensor:
+        """n fdfs_gpu_file_state records (uint8[n, 128] on the device),
+        initialised as storage_write_to_file does (CRC32_XINIT,
+        INIT_HASH_CODES4, my_md5_init)."""
+        dev = torch.device("cuda", self.device) if device is None else device
+        states = torch.empty((n, _lib.FILE_STATE_SIZE), dtype=torch.uint8, device=dev)
+        if n > _U32_MAX:
+            raise ValueError("too many states for a uint32 count")
+        self._rc(self._L.fdfs_gpu_state_init(self._h, states.data_ptr(), n, _stream_handle(stream)),
+                 "fdfs_gpu_state_init")
+        return states
+
+    @staticmethod
+    def _check_states(states: torch.Tensor) -> int:
+        _check_dev(states, "states", torch.uint8)
+        if states.dim() != 2 or states.shape[1] != _lib.FILE_STATE_SIZE:
+            raise ValueError(f"states must be uint8[n, {_lib.FILE_STATE_SIZE}]")
+        return states.shape[0]
+
+    def update_batch(self, states: torch.Tensor, data: torch.Tensor, offsets: torch.Tensor,
+                     sizes: torch.Tensor, method: int = SIG_HASH,
+                     state_idx: torch.Tensor | None = None, stream=None, check_bounds: bool = True):
+        """dio_write_file's per-chunk update for a batch: chunk i (data
+        [offsets[i], offsets[i] + sizes[i])) is hashed onto
+        states[state_idx[i]] (state_idx int32[n], default i).  A state may
+        appear at most once per call."""
+        ns = self._check_states(states)
+        n = _check_batch(data, offsets, sizes, check_bounds)
+        if state_idx is not None:
+            _check_dev(state_idx, "state_idx", torch.int32)
+            if state_idx.numel() != n:
+                raise ValueError("one state index per chunk")
+            if check_bounds and n:
+                lo, hi = int(state_idx.min().item()), int(state_idx.max().item())
+                if lo < 0 or hi >= ns:
+                    raise ValueError(f"state index range [{lo}, {hi}] outside {ns} states")
+        elif n > ns:
+            raise ValueError(f"{n} chunks for {ns} states")
+        b = _lib.FdfsGpuBatch(data.data_ptr(), offsets.data_ptr(), sizes.data_ptr(), n)
+        self._rc(self._L.fdfs_gpu_update_batch(self._h, ctypes.byref(b), _ptr(state_idx), method,
+                                               states.data_ptr(), _stream_handle(stream)),
+                 "fdfs_gpu_update_batch")
+
+    def final_batch(self, states: torch.Tensor, method: int = SIG_HASH,
+                    state_idx: torch.Tensor | None = None, want_sig: bool = True,
+                    want_codes: bool = False, stream=None):
+        """CRC32_FINAL + FINISH_HASH_CODES4 / my_md5_final + the 24-byte
+        signature of each state (or of states[state_idx]): (crc int32[n],
+        sig uint8[n,24] | None, codes int32[n,4] | None), as sig_batch."""
+        ns = self._check_states(states)
+        n = ns
+        if state_idx is not None:
+            _check_dev(state_idx, "state_idx", torch.int32)
+            n = state_idx.numel()
+        dev = states.device
+        crc = torch.empty(n, dtype=torch.int32, device=dev)
+        sig = torch.empty((n, 24), dtype=torch.uint8, device=dev) \
+            if (want_sig and method != SIG_CRC_ONLY) else None
+        codes = torch.empty((n, 4), dtype=torch.int32, device=dev) \
+            if (want_codes and method != SIG_CRC_ONLY) else None
+        self._rc(self._L.fdfs_gpu_final_batch(self._h, states.data_ptr(), _ptr(state_idx), n, method,
+                                              crc.data_ptr(), _ptr(sig), _ptr(codes),
+                                              _stream_handle(stream)), "fdfs_gpu_final_batch")
+        return crc, sig, codes
+
+    def crc_combine(self, crc_a: torch.Tensor, crc_b: torch.Tensor, len_b: torch.Tensor, stream=None):
+        """crc32_combine over GF(2): the running CRC32_ex value of A||B from
+        crc_a = CRC32_ex(A, init), crc_b = CRC32_ex(B, 0) and |B| (int64)."""
+        _check_dev(crc_a, "crc_a", torch.int32)
+        _check_dev(crc_b, "crc_b", torch.int32)
+        _check_dev(len_b, "len_b", torch.int64)
+        n = crc_a.numel()
+        if crc_b.numel() != n or len_b.numel() != n:
+            raise ValueError("crc_a, crc_b and len_b differ in length")
+        out = torch.empty_like(crc_a)
+        self._rc(self._L.fdfs_gpu_crc_combine(self._h, crc_a.data_ptr(), crc_b.data_ptr(),
+                                              len_b.data_ptr(), n, out.data_ptr(),
+                                              _stream_handle(stream)), "fdfs_gpu_crc_combine")
+        return out
+
     # ----------------------------------------------------------------- dedup
     def sig_batch_host(self, data, offsets, sizes, method: int = SIG_HASH, want_sig: bool = True,
                        want_codes: bool = False, chunk_bytes: int = 0):

@@ -363,10 +363,127 @@ int fdfs_gpu_sig_batch(fdfs_gpu_ctx *ctx, const fdfs_gpu_batch *batch, int metho
         hipEvent_t a, b;
         timing_pair(ctx, FDFS_KERNEL_SIG_LANE, a, b);
         e = fdfs::launch_sig_lane(ctx->sar, method, base, batch->offset, batch->size, n, hist,
-                                  order, &big, ctx->d_tabs, crc_out, sig_out, codes_out, ctx->seg_grid,
-                                  st, a, b);
+                                  order, &big, ctx->d_tabs, crc_out, sig_out, codes_out, nullptr, nullptr,
+                                  ctx->seg_grid, st, a, b);
     }
     return e == hipSuccess ? 0 : fail(ctx, e, "sig_batch launch");
+}
+
+// ---- chunked (state-carrying) form ------------------------------------------
+
+int fdfs_gpu_state_init(fdfs_gpu_ctx *ctx, fdfs_gpu_file_state *states, uint32_t n, void *stream)
+{
+    if (!ctx)
+        return EINVAL;
+    if (n == 0)
+        return 0;
+    if (!states)
+        return EINVAL;
+    std::lock_guard<std::recursive_mutex> lk(ctx->mu);
+    DeviceGuard g(ctx->device);
+    if (!g.ok)
+        return ENODEV;
+    hipError_t e = fdfs::launch_state_init(states, n, reinterpret_cast<hipStream_t>(stream));
+    return e == hipSuccess ? 0 : fail(ctx, e, "state_init launch");
+}
+
+int fdfs_gpu_update_batch(fdfs_gpu_ctx *ctx, const fdfs_gpu_batch *chunks, const uint32_t *state_idx,
+                          int method, fdfs_gpu_file_state *states, void *stream)
+{
+    if (!ctx || !chunks)
+        return EINVAL;
+    if (method != FDFS_SIG_CRC_ONLY && method != FDFS_SIG_HASH && method != FDFS_SIG_MD5)
+        return EINVAL;
+    const uint32_t n = chunks->n;
+    if (n == 0)
+        return 0;
+    if (!chunks->base || !chunks->offset || !chunks->size || !states)
+        return EINVAL;
+    if (reinterpret_cast<uintptr_t>(states) & 15)
+        return EINVAL;
+    std::lock_guard<std::recursive_mutex> lk(ctx->mu);
+    DeviceGuard g(ctx->device);
+    if (!g.ok)
+        return ENODEV;
+    hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+    int rc = ensure_ws(ctx, sig_ws_bytes(n) + align_up(4ull * n), st);
+    if (rc)
+        return rc;
+    WsScope wsc(ctx, st);
+    Carve cv{static_cast<char *>(ctx->ws)};
+    const uint8_t *base = static_cast<const uint8_t *>(chunks->base);
+    hipError_t e;
+    if (method == FDFS_SIG_CRC_ONLY) {
+        // per-chunk CRC by the segmented kernel, then carried onto the state
+        uint32_t *tmp = cv.take<uint32_t>(n);
+        uint64_t *nseg = cv.take<uint64_t>(n);
+        uint64_t *first = cv.take<uint64_t>((size_t)n + 1);
+        uint64_t *bsum = cv.take<uint64_t>(fdfs::scan_workspace_elems(n));
+        hipEvent_t a, b;
+        timing_pair(ctx, FDFS_KERNEL_CRC_SEG, a, b);
+        e = fdfs::launch_crc_seg(ctx->sar, base, chunks->offset, chunks->size, n, nseg, first, bsum,
+                                 ctx->d_tabs, tmp, ctx->seg_grid, st, a, b);
+        if (e == hipSuccess)
+            e = fdfs::launch_crc_carry(tmp, chunks->size, n, state_idx, states, ctx->d_tabs, st);
+    } else {
+        uint32_t *hist = cv.take<uint32_t>(fdfs::kLaneWsDwords);
+        uint32_t *order = cv.take<uint32_t>(n);
+        fdfs::BigCrcWs big;
+        big.nbig = cv.take<uint32_t>(1);
+        big.offs = cv.take<uint64_t>(n);
+        big.sizes = cv.take<uint64_t>(n);
+        big.seg_first = cv.take<uint64_t>((size_t)n + 1);
+        big.crc = cv.take<uint32_t>(n);
+        big.poly = cv.take<uint32_t>(2 * (size_t)n);
+        hipEvent_t a, b;
+        timing_pair(ctx, FDFS_KERNEL_SIG_LANE, a, b);
+        e = fdfs::launch_sig_lane(ctx->sar, method, base, chunks->offset, chunks->size, n, hist, order, &big,
+                                  ctx->d_tabs, nullptr, nullptr, nullptr, states, state_idx, ctx->seg_grid,
+                                  st, a, b);
+    }
+    return e == hipSuccess ? 0 : fail(ctx, e, "update_batch launch");
+}
+
+int fdfs_gpu_final_batch(fdfs_gpu_ctx *ctx, const fdfs_gpu_file_state *states,
+                         const uint32_t *state_idx, uint32_t n, int method, uint32_t *crc_out,
+                         uint8_t *sig_out, int32_t *codes_out, void *stream)
+{
+    if (!ctx)
+        return EINVAL;
+    if (method != FDFS_SIG_CRC_ONLY && method != FDFS_SIG_HASH && method != FDFS_SIG_MD5)
+        return EINVAL;
+    if (n == 0)
+        return 0;
+    if (!states || !crc_out)
+        return EINVAL;
+    if ((reinterpret_cast<uintptr_t>(states) | reinterpret_cast<uintptr_t>(sig_out)) & 3 ||
+        reinterpret_cast<uintptr_t>(codes_out) & 15)
+        return EINVAL;
+    std::lock_guard<std::recursive_mutex> lk(ctx->mu);
+    DeviceGuard g(ctx->device);
+    if (!g.ok)
+        return ENODEV;
+    hipError_t e = fdfs::launch_final(method, states, state_idx, n, crc_out, sig_out, codes_out,
+                                      reinterpret_cast<hipStream_t>(stream));
+    return e == hipSuccess ? 0 : fail(ctx, e, "final_batch launch");
+}
+
+int fdfs_gpu_crc_combine(fdfs_gpu_ctx *ctx, const uint32_t *crc_a, const uint32_t *crc_b,
+                         const uint64_t *len_b, uint32_t n, uint32_t *out, void *stream)
+{
+    if (!ctx)
+        return EINVAL;
+    if (n == 0)
+        return 0;
+    if (!crc_a || !crc_b || !len_b || !out)
+        return EINVAL;
+    std::lock_guard<std::recursive_mutex> lk(ctx->mu);
+    DeviceGuard g(ctx->device);
+    if (!g.ok)
+        return ENODEV;
+    hipError_t e = fdfs::launch_crc_combine(crc_a, crc_b, len_b, n, out, ctx->d_tabs,
+                                            reinterpret_cast<hipStream_t>(stream));
+    return e == hipSuccess ? 0 : fail(ctx, e, "crc_combine launch");
 }
 
 // ---- host-resident batches: chunked, double-buffered H2D / hash / D2H -------

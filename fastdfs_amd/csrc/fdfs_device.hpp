@@ -229,6 +229,42 @@ __device__ __forceinline__ uint32_t poly_word(uint32_t h, uint32_t w)
 
 __device__ __forceinline__ uint32_t bswap32(uint32_t v) { return __builtin_bswap32(v); }
 
+// m^e mod 2^32 (simple_hash / Time33 multipliers raised to a length).
+__device__ __forceinline__ uint32_t pow_dev(uint32_t m, uint64_t e)
+{
+    uint32_t r = 1;
+    for (; e; e >>= 1, m *= m)
+        if (e & 1)
+            r *= m;
+    return r;
+}
+
+// One thread's GF(2) advance of a CRC32_ex state by `nbytes` zero bytes,
+// v -> M^nbytes v, from the matrix powers M^(2^k) (columns in t.MPOW).  Used
+// where a chunk's state must be carried over the chunk: CRC32_ex(d, X) =
+// M^|d| X ^ CRC32_ex(d, 0) for both shift variants (linear over GF(2)).
+__device__ __forceinline__ uint32_t advance_bytes(const CrcTables &t, uint32_t v, uint64_t nbytes)
+{
+    for (int k = 0; nbytes && k < 48; k++, nbytes >>= 1) {
+        if (!(nbytes & 1))
+            continue;
+        uint32_t r = 0;
+#pragma unroll 8
+        for (int c = 0; c < 32; c++)
+            r ^= (0u - ((v >> c) & 1u)) & t.MPOW[k][c];
+        v = r;
+    }
+    return v;
+}
+
+// fdfs_gpu_file_state.md5_count += 8 * nbytes (two u32 words, low first).
+__device__ __forceinline__ void count_add(uint32_t (&cnt)[2], uint64_t nbytes)
+{
+    const uint64_t c = ((uint64_t)cnt[1] << 32 | cnt[0]) + (nbytes << 3);
+    cnt[0] = (uint32_t)c;
+    cnt[1] = (uint32_t)(c >> 32);
+}
+
 // Cooperative global -> LDS copy of `ndw` dwords.
 __device__ __forceinline__ void lds_fill(uint32_t *dst, const uint32_t *__restrict__ src, int ndw)
 {

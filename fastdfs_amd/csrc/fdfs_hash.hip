@@ -45,15 +45,6 @@ constexpr int kHashBlock = 256;
 typedef int i32x4 __attribute__((ext_vector_type(4)));
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 
-__device__ __forceinline__ uint32_t pow_dev(uint32_t m, uint32_t e)
-{
-    uint32_t r = 1;
-    for (; e; e >>= 1, m *= m)
-        if (e & 1)
-            r *= m;
-    return r;
-}
-
 // All four CALC_HASH_CODES4 hashes of one 16-byte vector on the lane.
 template <bool SAR, int TM>
 __device__ __forceinline__ uint32_t crc16(const uint32_t *sD, const Rep8Lane &R8, uint32_t K,
@@ -95,12 +86,18 @@ __device__ __forceinline__ uint32_t and_xor80(uint32_t a, uint32_t m)
     return r;
 }
 
-template <bool SAR, int TM, int MODE>
+// ST (fdfs_gpu_update_batch): the lane continues the chunk's
+// StorageFileContext-shaped state (crc32, file_hash_codes) instead of
+// INIT_HASH_CODES4 and writes it back unfinalised; every step above is a
+// recurrence from whatever state it starts in (the polynomial planes start
+// from the lane's running value), so nothing else changes.
+template <bool SAR, int TM, int MODE, bool ST>
 __global__ __launch_bounds__(TM == 2 ? 1024 : kHashBlock) void sig_hash_kernel(
     const uint8_t *__restrict__ base, const uint64_t *__restrict__ offs,
     const uint64_t *__restrict__ sizes, const uint32_t *__restrict__ order, uint32_t n,
     const DevTables *__restrict__ tabs, uint64_t big_min, uint32_t *__restrict__ crc_out,
-    uint8_t *__restrict__ sig_out, int32_t *__restrict__ codes_out)
+    uint8_t *__restrict__ sig_out, int32_t *__restrict__ codes_out,
+    fdfs_gpu_file_state *__restrict__ states, const uint32_t *__restrict__ sidx)
 {
     __shared__ uint32_t sD[TM == 2 ? kRep8Dwords : 16 * 256];
     __shared__ uint32_t sT[256];
@@ -128,6 +125,16 @@ __global__ __launch_bounds__(TM == 2 ? 1024 : kHashBlock) void sig_hash_kernel(
     const uint8_t *p = valid ? base + offs[f] : safe;
     uint32_t c = 0xFFFFFFFFu;  // CRC32_XINIT (storage/storage_service.c:7149)
     uint32_t e = 0, s = 0, t = 0;  // INIT_HASH_CODES4 (storage/storage_service.c:7156)
+    fdfs_gpu_file_state *fs = nullptr;
+    if constexpr (ST) {
+        if (valid) {
+            fs = states + (sidx ? sidx[f] : f);
+            c = (uint32_t)fs->crc32;
+            e = (uint32_t)fs->hash_codes[1];
+            s = (uint32_t)fs->hash_codes[2];
+            t = (uint32_t)fs->hash_codes[3];
+        }
+    }
     // Files of >= big_min bytes leave their CRC, simple_hash and Time33 to
     // segment-parallel kernels (launch_sig_lane runs them before this one
     // and patches the outputs after) and keep only ELFHash here: their waves
@@ -284,6 +291,22 @@ __global__ __launch_bounds__(TM == 2 ? 1024 : kHashBlock) void sig_hash_kernel(
     }
     if (!valid)
         return;
+    if constexpr (ST) {
+        // big chunks: crc32, codes 0/2/3 come from big_patch_kernel, which
+        // still needs the chunk's starting values there
+        if (small) {
+            fs->crc32 = (int32_t)c;
+            fs->hash_codes[0] = (int32_t)c;
+            fs->hash_codes[2] = (int32_t)s;
+            fs->hash_codes[3] = (int32_t)t;
+        }
+        fs->hash_codes[1] = (int32_t)e;
+        uint32_t cnt[2] = {fs->md5_count[0], fs->md5_count[1]};
+        count_add(cnt, L);
+        fs->md5_count[0] = cnt[0];
+        fs->md5_count[1] = cnt[1];
+        return;
+    }
     c ^= 0xFFFFFFFFu;  // CRC32_FINAL / FINISH_HASH_CODES4 (storage/storage_dio.c:500,508)
     if (small)
         crc_out[f] = c;  // else big_patch_kernel puts the segmented CRC in all three outputs
@@ -380,7 +403,8 @@ hipError_t launch_poly_seg(const uint8_t *base, const uint64_t *boffs, const uin
 hipError_t launch_sig_hash(bool sar, const uint8_t *base, const uint64_t *offs,
                            const uint64_t *sizes, uint32_t n, const uint32_t *order,
                            const DevTables *tabs, uint64_t big_min, uint32_t *crc_out, uint8_t *sig_out,
-                           int32_t *codes_out, hipStream_t st)
+                           int32_t *codes_out, fdfs_gpu_file_state *states, const uint32_t *sidx,
+                           hipStream_t st)
 {
 #ifdef FDFS_PROBES
     // measurement build only (make probes): FDFS_GPU_HASH_MODE 1 = loads
@@ -399,16 +423,19 @@ hipError_t launch_sig_hash(bool sar, const uint8_t *base, const uint64_t *offs,
 #else
     constexpr int tm = 0;
 #endif
-    const unsigned blk = tm == 2 ? 1024 : kHashBlock;
+    const unsigned blk = (tm == 2 && !states) ? 1024 : kHashBlock;
     const unsigned grid = (n + blk - 1) / blk;
 #define HASH_LAUNCH(S, M)                                                                                \
     do {                                                                                                 \
-        if (tm == 2)                                                                                     \
-            sig_hash_kernel<S, 2, M><<<grid, blk, 0, st>>>(base, offs, sizes, order, n, tabs, big_min, crc_out, \
-                                                           sig_out, codes_out);                          \
+        if (states)                                                                                      \
+            sig_hash_kernel<S, 0, M, true><<<grid, blk, 0, st>>>(base, offs, sizes, order, n, tabs, big_min, \
+                                                                 crc_out, sig_out, codes_out, states, sidx); \
+        else if (tm == 2)                                                                                \
+            sig_hash_kernel<S, 2, M, false><<<grid, blk, 0, st>>>(base, offs, sizes, order, n, tabs, big_min, \
+                                                                  crc_out, sig_out, codes_out, nullptr, nullptr); \
         else                                                                                             \
-            sig_hash_kernel<S, 0, M><<<grid, blk, 0, st>>>(base, offs, sizes, order, n, tabs, big_min, crc_out, \
-                                                           sig_out, codes_out);                          \
+            sig_hash_kernel<S, 0, M, false><<<grid, blk, 0, st>>>(base, offs, sizes, order, n, tabs, big_min, \
+                                                                  crc_out, sig_out, codes_out, nullptr, nullptr); \
     } while (0)
 #ifdef FDFS_PROBES
     if (mode == 1)

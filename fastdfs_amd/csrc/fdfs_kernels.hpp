@@ -3,6 +3,8 @@
 #include <hip/hip_runtime.h>
 #include <cstdint>
 
+#include "../../include/fdfs_gpu.h"
+
 namespace fdfs {
 
 struct DevTables;
@@ -29,10 +31,15 @@ struct BigCrcWs {  // device arrays of n entries (seg_first n + 1)
 hipError_t launch_poly_seg(const uint8_t *base, const uint64_t *boffs, const uint64_t *bsizes,
                            const uint64_t *seg_first, const uint32_t *nbig, uint32_t *bpoly,
                            unsigned grid, hipStream_t st);
+// Lane-per-file paths (HASH / MD5).  states == nullptr: one-shot over whole
+// files (outputs crc_out / sig_out / codes_out).  states != nullptr: the
+// chunked update (fdfs_gpu_update_batch): chunk f continues and rewrites
+// states[sidx ? sidx[f] : f], and no output is written.
 hipError_t launch_sig_lane(bool sar, int method, const uint8_t *base, const uint64_t *offs,
                            const uint64_t *sizes, uint32_t n, uint32_t *hist, uint32_t *order,
                            const BigCrcWs *big, const DevTables *tabs, uint32_t *crc_out,
-                           uint8_t *sig_out, int32_t *codes_out, unsigned seg_grid, hipStream_t st,
+                           uint8_t *sig_out, int32_t *codes_out, fdfs_gpu_file_state *states,
+                           const uint32_t *sidx, unsigned seg_grid, hipStream_t st,
                            hipEvent_t ev0, hipEvent_t ev1);
 hipError_t launch_crc_seg(bool sar, const uint8_t *base, const uint64_t *offs, const uint64_t *sizes,
                           uint32_t n, uint64_t *nseg, uint64_t *seg_first, uint64_t *bsum,
@@ -41,11 +48,26 @@ hipError_t launch_crc_seg(bool sar, const uint8_t *base, const uint64_t *offs, c
 hipError_t launch_md5_stage(bool sar, const uint8_t *base, const uint64_t *offs,
                             const uint64_t *sizes, uint32_t n, const uint32_t *order,
                             const DevTables *tabs, uint32_t *queue, uint32_t *crc_out, uint8_t *sig_out,
-                            int32_t *codes_out, hipStream_t st);
+                            int32_t *codes_out, fdfs_gpu_file_state *states, const uint32_t *sidx,
+                            hipStream_t st);
 hipError_t launch_sig_hash(bool sar, const uint8_t *base, const uint64_t *offs,
                            const uint64_t *sizes, uint32_t n, const uint32_t *order,
                            const DevTables *tabs, uint64_t big_min, uint32_t *crc_out, uint8_t *sig_out,
-                           int32_t *codes_out, hipStream_t st);
+                           int32_t *codes_out, fdfs_gpu_file_state *states, const uint32_t *sidx,
+                           hipStream_t st);
+
+// chunked-update helpers (fdfs_stream.hip)
+hipError_t launch_state_init(fdfs_gpu_file_state *states, uint32_t n, hipStream_t st);
+// CRC_ONLY update: crc[f] = CRC32_FINAL(CRC32_ex(chunk f, XINIT)) from
+// crc_seg_kernel, carried onto the chunk's state (and its count advanced).
+hipError_t launch_crc_carry(const uint32_t *crc, const uint64_t *sizes, uint32_t n,
+                            const uint32_t *sidx, fdfs_gpu_file_state *states, const DevTables *tabs,
+                            hipStream_t st);
+hipError_t launch_final(int method, const fdfs_gpu_file_state *states, const uint32_t *sidx,
+                        uint32_t n, uint32_t *crc_out, uint8_t *sig_out, int32_t *codes_out,
+                        hipStream_t st);
+hipError_t launch_crc_combine(const uint32_t *a, const uint32_t *b, const uint64_t *len_b, uint32_t n,
+                              uint32_t *out, const DevTables *tabs, hipStream_t st);
 int crc_seg_blocks_per_cu();
 int crc_table_mode();
 

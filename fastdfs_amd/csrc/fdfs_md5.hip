@@ -6,130 +6,11 @@
 // (storage/storage_service.c:106-120).
 #include "fdfs_device.hpp"
 #include "fdfs_kernels.hpp"
+#include "fdfs_md5.hpp"
 
 #include <cstdlib>
 
-#ifndef MD5_CHAIN_ASM
-#define MD5_CHAIN_ASM 1
-#endif
-
 namespace fdfs {
-
-// ----------------------------------------------------------------- MD5 core
-
-__device__ __forceinline__ uint32_t rotl(uint32_t x, int s)
-{
-    return __builtin_amdgcn_alignbit(x, x, 32 - s);
-}
-
-#define MD5_F(b, c, d) ((d) ^ ((b) & ((c) ^ (d))))
-#define MD5_G(b, c, d) ((c) ^ ((d) & ((b) ^ (c))))
-#define MD5_H(b, c, d) ((b) ^ (c) ^ (d))
-#define MD5_I(b, c, d) ((c) ^ ((b) | ~(d)))
-// The step's critical path is F -> add -> rotate -> add.  a, m and k are
-// known steps ahead, so (a + m + k) is summed off the path and the on-path
-// add is kept a single full-rate v_add_u32 (hipcc would otherwise fold it
-// into a v_add3_u32, a half-rate instruction on the chain).
-__device__ __forceinline__ uint32_t add_chain(uint32_t x, uint32_t y)
-{
-#if MD5_CHAIN_ASM
-    uint32_t r;
-    asm("v_add_u32_e32 %0, %1, %2" : "=v"(r) : "v"(x), "v"(y));
-    return r;
-#else
-    return x + y;
-#endif
-}
-#define MD5_STEP(FN, a, b, c, d, m, k, s) a = (b) + rotl(add_chain((a) + (m) + (k), FN(b, c, d)), s)
-
-__device__ __forceinline__ void md5_compress(uint32_t st[4], const uint32_t m[16])
-{
-    uint32_t a = st[0], b = st[1], c = st[2], d = st[3];
-    MD5_STEP(MD5_F, a, b, c, d, m[0], 0xd76aa478u, 7);
-    MD5_STEP(MD5_F, d, a, b, c, m[1], 0xe8c7b756u, 12);
-    MD5_STEP(MD5_F, c, d, a, b, m[2], 0x242070dbu, 17);
-    MD5_STEP(MD5_F, b, c, d, a, m[3], 0xc1bdceeeu, 22);
-    MD5_STEP(MD5_F, a, b, c, d, m[4], 0xf57c0fafu, 7);
-    MD5_STEP(MD5_F, d, a, b, c, m[5], 0x4787c62au, 12);
-    MD5_STEP(MD5_F, c, d, a, b, m[6], 0xa8304613u, 17);
-    MD5_STEP(MD5_F, b, c, d, a, m[7], 0xfd469501u, 22);
-    MD5_STEP(MD5_F, a, b, c, d, m[8], 0x698098d8u, 7);
-    MD5_STEP(MD5_F, d, a, b, c, m[9], 0x8b44f7afu, 12);
-    MD5_STEP(MD5_F, c, d, a, b, m[10], 0xffff5bb1u, 17);
-    MD5_STEP(MD5_F, b, c, d, a, m[11], 0x895cd7beu, 22);
-    MD5_STEP(MD5_F, a, b, c, d, m[12], 0x6b901122u, 7);
-    MD5_STEP(MD5_F, d, a, b, c, m[13], 0xfd987193u, 12);
-    MD5_STEP(MD5_F, c, d, a, b, m[14], 0xa679438eu, 17);
-    MD5_STEP(MD5_F, b, c, d, a, m[15], 0x49b40821u, 22);
-
-    MD5_STEP(MD5_G, a, b, c, d, m[1], 0xf61e2562u, 5);
-    MD5_STEP(MD5_G, d, a, b, c, m[6], 0xc040b340u, 9);
-    MD5_STEP(MD5_G, c, d, a, b, m[11], 0x265e5a51u, 14);
-    MD5_STEP(MD5_G, b, c, d, a, m[0], 0xe9b6c7aau, 20);
-    MD5_STEP(MD5_G, a, b, c, d, m[5], 0xd62f105du, 5);
-    MD5_STEP(MD5_G, d, a, b, c, m[10], 0x02441453u, 9);
-    MD5_STEP(MD5_G, c, d, a, b, m[15], 0xd8a1e681u, 14);
-    MD5_STEP(MD5_G, b, c, d, a, m[4], 0xe7d3fbc8u, 20);
-    MD5_STEP(MD5_G, a, b, c, d, m[9], 0x21e1cde6u, 5);
-    MD5_STEP(MD5_G, d, a, b, c, m[14], 0xc33707d6u, 9);
-    MD5_STEP(MD5_G, c, d, a, b, m[3], 0xf4d50d87u, 14);
-    MD5_STEP(MD5_G, b, c, d, a, m[8], 0x455a14edu, 20);
-    MD5_STEP(MD5_G, a, b, c, d, m[13], 0xa9e3e905u, 5);
-    MD5_STEP(MD5_G, d, a, b, c, m[2], 0xfcefa3f8u, 9);
-    MD5_STEP(MD5_G, c, d, a, b, m[7], 0x676f02d9u, 14);
-    MD5_STEP(MD5_G, b, c, d, a, m[12], 0x8d2a4c8au, 20);
-
-    MD5_STEP(MD5_H, a, b, c, d, m[5], 0xfffa3942u, 4);
-    MD5_STEP(MD5_H, d, a, b, c, m[8], 0x8771f681u, 11);
-    MD5_STEP(MD5_H, c, d, a, b, m[11], 0x6d9d6122u, 16);
-    MD5_STEP(MD5_H, b, c, d, a, m[14], 0xfde5380cu, 23);
-    MD5_STEP(MD5_H, a, b, c, d, m[1], 0xa4beea44u, 4);
-    MD5_STEP(MD5_H, d, a, b, c, m[4], 0x4bdecfa9u, 11);
-    MD5_STEP(MD5_H, c, d, a, b, m[7], 0xf6bb4b60u, 16);
-    MD5_STEP(MD5_H, b, c, d, a, m[10], 0xbebfbc70u, 23);
-    MD5_STEP(MD5_H, a, b, c, d, m[13], 0x289b7ec6u, 4);
-    MD5_STEP(MD5_H, d, a, b, c, m[0], 0xeaa127fau, 11);
-    MD5_STEP(MD5_H, c, d, a, b, m[3], 0xd4ef3085u, 16);
-    MD5_STEP(MD5_H, b, c, d, a, m[6], 0x04881d05u, 23);
-    MD5_STEP(MD5_H, a, b, c, d, m[9], 0xd9d4d039u, 4);
-    MD5_STEP(MD5_H, d, a, b, c, m[12], 0xe6db99e5u, 11);
-    MD5_STEP(MD5_H, c, d, a, b, m[15], 0x1fa27cf8u, 16);
-    MD5_STEP(MD5_H, b, c, d, a, m[2], 0xc4ac5665u, 23);
-
-    MD5_STEP(MD5_I, a, b, c, d, m[0], 0xf4292244u, 6);
-    MD5_STEP(MD5_I, d, a, b, c, m[7], 0x432aff97u, 10);
-    MD5_STEP(MD5_I, c, d, a, b, m[14], 0xab9423a7u, 15);
-    MD5_STEP(MD5_I, b, c, d, a, m[5], 0xfc93a039u, 21);
-    MD5_STEP(MD5_I, a, b, c, d, m[12], 0x655b59c3u, 6);
-    MD5_STEP(MD5_I, d, a, b, c, m[3], 0x8f0ccc92u, 10);
-    MD5_STEP(MD5_I, c, d, a, b, m[10], 0xffeff47du, 15);
-    MD5_STEP(MD5_I, b, c, d, a, m[1], 0x85845dd1u, 21);
-    MD5_STEP(MD5_I, a, b, c, d, m[8], 0x6fa87e4fu, 6);
-    MD5_STEP(MD5_I, d, a, b, c, m[15], 0xfe2ce6e0u, 10);
-    MD5_STEP(MD5_I, c, d, a, b, m[6], 0xa3014314u, 15);
-    MD5_STEP(MD5_I, b, c, d, a, m[13], 0x4e0811a1u, 21);
-    MD5_STEP(MD5_I, a, b, c, d, m[4], 0xf7537e82u, 6);
-    MD5_STEP(MD5_I, d, a, b, c, m[11], 0xbd3af235u, 10);
-    MD5_STEP(MD5_I, c, d, a, b, m[2], 0x2ad7d2bbu, 15);
-    MD5_STEP(MD5_I, b, c, d, a, m[9], 0xeb86d391u, 21);
-    st[0] += a;
-    st[1] += b;
-    st[2] += c;
-    st[3] += d;
-}
-
-// 16 bytes at p; aligned -> one dwordx4, otherwise byte loads.
-__device__ __forceinline__ uint4 load16(const uint8_t *p, bool aligned)
-{
-    if (aligned)
-        return *reinterpret_cast<const uint4 *>(p);
-    uint32_t w[4];
-#pragma unroll
-    for (int d = 0; d < 4; d++)
-        w[d] = (uint32_t)p[4 * d] | ((uint32_t)p[4 * d + 1] << 8) |
-               ((uint32_t)p[4 * d + 2] << 16) | ((uint32_t)p[4 * d + 3] << 24);
-    return make_uint4(w[0], w[1], w[2], w[3]);
-}
 
 __device__ __forceinline__ void store_sig(uint8_t *sig, uint64_t L, uint32_t w2, uint32_t w3,
                                           uint32_t w4, uint32_t w5)
@@ -141,12 +22,10 @@ __device__ __forceinline__ void store_sig(uint8_t *sig, uint64_t L, uint32_t w2,
 }
 
 // Final block(s) of a file whose first nblk full 64-byte blocks are already
-// folded into st: the L & 63 tail bytes, 0x80, zero pad and the 64-bit bit
-// length (RFC 1321 3.1-3.2; my_md5_final at storage/storage_dio.c:512).
-__device__ __forceinline__ void md5_finish(uint32_t st[4], const uint8_t *p, uint64_t nblk,
-                                           uint64_t L)
+// folded into st: the L & 63 tail bytes at tp, 0x80, zero pad and the 64-bit
+// bit length (RFC 1321 3.1-3.2; my_md5_final at storage/storage_dio.c:512).
+__device__ __forceinline__ void md5_finish(uint32_t st[4], const uint8_t *tp, uint64_t L)
 {
-    const uint8_t *tp = p + (nblk << 6);
     const uint32_t r = (uint32_t)(L & 63u);
     uint32_t m[16];
 #pragma unroll
@@ -155,30 +34,13 @@ __device__ __forceinline__ void md5_finish(uint32_t st[4], const uint8_t *p, uin
 #pragma unroll
         for (int q = 0; q < 4; q++) {
             const uint32_t k = 4 * wd + q;
-            uint32_t b = 0;
-            if (k < r) {
-                b = tp[k];
-            } else if (k == r) {
-                b = 0x80u;
-            }
-            word |= b << (8 * q);
+            if (k < r)
+                word |= (uint32_t)tp[k] << (8 * q);
         }
         m[wd] = word;
     }
     const uint64_t bits = L << 3;
-    if (r < 56) {
-        m[14] = (uint32_t)bits;
-        m[15] = (uint32_t)(bits >> 32);
-        md5_compress(st, m);
-    } else {
-        md5_compress(st, m);
-#pragma unroll
-        for (int wd = 0; wd < 14; wd++)
-            m[wd] = 0;
-        m[14] = (uint32_t)bits;
-        m[15] = (uint32_t)(bits >> 32);
-        md5_compress(st, m);
-    }
+    md5_pad_compress(st, m, r, (uint32_t)bits, (uint32_t)(bits >> 32));
 }
 
 // ------------------------------------------------ MD5 path, staged loads
@@ -187,12 +49,19 @@ __device__ __forceinline__ void md5_finish(uint32_t st[4], const uint8_t *p, uin
 // travel lane-per-file.  A lane-per-file load touches 64 files (64 pages) per
 // wave-instruction; over a batch of 100K 1-4 MiB files that is ~100K
 // concurrently open pages and the address translation, not the MD5 chain or
-// HBM, set the time (DESIGN.md section 4.4).  Here each round the wave loads
+// HBM, set the time (DESIGN.md section 4.3).  Here each round the wave loads
 // CH bytes of each of its 64 files cooperatively: every load instruction
-// reads whole 128-byte lines of 8 files (8 lanes x 16 B each), the data is
+// reads 128 contiguous bytes of 8 files (8 lanes x 16 B each), the data is
 // written to LDS as one padded row per file, and each lane then hashes its
 // own row.  The next round's loads are in flight while this round is hashed
 // (two register sets, asm loads so hipcc cannot sink them to their use).
+//
+// A file's bytes may start at any address: the cooperative loads read each
+// file's stream at its own (byte) offset, so the LDS rows always hold the
+// stream 16-byte aligned.  gfx950 serves byte-misaligned 16-byte global loads
+// (the unaligned memory mode ROCm configures; scripts/probes/unaligned_load
+// checks it on the box): a misaligned file costs a second cache line per
+// 128-byte piece, not a lane-serial byte loop.
 //
 // The file's CRC32 (CRC32_ex over the same bytes, storage/storage_dio.c:467)
 // is computed by the same lane from the same LDS row: one pass over HBM for
@@ -201,18 +70,25 @@ __device__ __forceinline__ void md5_finish(uint32_t st[4], const uint8_t *p, uin
 // tables are shared by the workgroup's waves (waves are otherwise
 // independent: no barrier after the table fill).
 //
+// ST (fdfs_gpu_update_batch): the lane continues a StorageFileContext-shaped
+// state instead of starting one.  The (count / 8) % 64 bytes my_md5_update
+// left pending are completed first from the chunk's head (lane-serial, < 64
+// bytes, assembled in the lane's LDS row), the chunk's full blocks then take
+// the staged path above, and its last bytes become the new pending buffer.
+//
 // LDS row stride CH+16 = 144 B: ds_write_b128 groups (8 lanes = one 128-byte
 // row) and ds_read_b128 groups (16 lanes, rows f at quad 9f + const mod 16)
 // are both conflict-free.
 constexpr int kMd5Chunk = 128;
 constexpr int kMd5Waves = 4;
 
-template <bool SAR>
+template <bool SAR, bool ST>
 __global__ __launch_bounds__(64 * kMd5Waves) void md5_stage_kernel(
     const uint8_t *__restrict__ base, const uint64_t *__restrict__ offs,
     const uint64_t *__restrict__ sizes, const uint32_t *__restrict__ order, uint32_t n,
     const DevTables *__restrict__ tabs, uint32_t w1, uint32_t *__restrict__ queue,
-    uint32_t *__restrict__ crc_out, uint8_t *__restrict__ sig_out, int32_t *__restrict__ codes_out)
+    uint32_t *__restrict__ crc_out, uint8_t *__restrict__ sig_out, int32_t *__restrict__ codes_out,
+    fdfs_gpu_file_state *__restrict__ states, const uint32_t *__restrict__ sidx)
 {
     constexpr int CH = kMd5Chunk;
     constexpr int PIECES = CH / 16;   // 16-byte pieces of one file's chunk
@@ -230,11 +106,12 @@ __global__ __launch_bounds__(64 * kMd5Waves) void md5_stage_kernel(
     typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 
     const int lane = threadIdx.x & 63;
-    // Waves take 64-file chunks of the size-descending order.  Every wave is
-    // resident at once (a few per SIMD), so the kernel ends with the SIMD
-    // that holds the most bytes: the first `w1` waves (one workgroup per
-    // CU) take the largest chunks and the rest take the remaining chunks
-    // smallest first, so a CU's second workgroup is a light one.
+    // Waves take 64-file chunks of the size-descending order.  Without a
+    // queue every wave is resident at once (a few per SIMD), so the kernel
+    // ends with the SIMD that holds the most bytes: the first `w1` waves (one
+    // workgroup per CU) take the largest chunks and the rest take the
+    // remaining chunks smallest first, so a CU's second workgroup is a light
+    // one.
     //
     // With a queue (the default) the grid is one workgroup per CU, one wave
     // per SIMD, and each wave takes the next chunk from a device counter
@@ -244,6 +121,7 @@ __global__ __launch_bounds__(64 * kMd5Waves) void md5_stage_kernel(
     // at once while the longest chains run).
     const uint32_t nw = (n + 63) / 64;
     uint8_t *tile = sbuf[threadIdx.x >> 6];
+    uint8_t *mine = tile + lane * STRIDE;
     const uint8_t *safe = reinterpret_cast<const uint8_t *>(tabs);  // >= 16 readable bytes
     const uint32_t K16 = tabs->t.K16;
     uint32_t chunk;
@@ -265,9 +143,41 @@ __global__ __launch_bounds__(64 * kMd5Waves) void md5_stage_kernel(
     const uint32_t f = valid ? order[i] : 0;
     const uint64_t L = valid ? sizes[f] : 0;
     const uint8_t *p = valid ? base + offs[f] : safe;
-    const uint64_t nblk = L >> 6;
     uint32_t st[4] = {0x67452301u, 0xefcdab89u, 0x98badcfeu, 0x10325476u};  // my_md5_init
     uint32_t c = 0xFFFFFFFFu;  // CRC32_XINIT (storage/storage_service.c:7149)
+    fdfs_gpu_file_state *fs = nullptr;
+    uint32_t have = 0;  // bytes pending in the state's MD5 buffer
+    uint64_t pre = 0;   // chunk bytes that complete them
+    if constexpr (ST) {
+        if (valid) {
+            fs = states + (sidx ? sidx[f] : f);
+            c = (uint32_t)fs->crc32;
+#pragma unroll
+            for (int k = 0; k < 4; k++)
+                st[k] = fs->md5_state[k];
+            have = (fs->md5_count[0] >> 3) & 63u;
+        }
+        if (have) {  // my_md5_update's partial block: buffer || chunk head
+            pre = 64 - have < L ? 64 - have : L;
+            for (uint32_t k = 0; k < have; k++)
+                mine[k] = fs->md5_buffer[k];
+            for (uint32_t k = 0; k < (uint32_t)pre; k++) {
+                const uint32_t b = p[k];
+                mine[have + k] = (uint8_t)b;
+                c = crc_byte<SAR>(sT, c, b);
+            }
+            if (have + pre == 64) {
+                const uint4 *q = reinterpret_cast<const uint4 *>(mine);
+                const uint4 a0 = q[0], a1 = q[1], a2 = q[2], a3 = q[3];
+                const uint32_t m[16] = {a0.x, a0.y, a0.z, a0.w, a1.x, a1.y, a1.z, a1.w,
+                                        a2.x, a2.y, a2.z, a2.w, a3.x, a3.y, a3.z, a3.w};
+                md5_compress(st, m);
+            }
+        }
+        __builtin_amdgcn_wave_barrier();
+    }
+    const uint8_t *s0 = p + pre;  // the stream of whole blocks
+    const uint64_t nblk = (L - pre) >> 6;
 
     auto block = [&](uint4 a0, uint4 a1, uint4 a2, uint4 a3) {
         const uint32_t m[16] = {a0.x, a0.y, a0.z, a0.w, a1.x, a1.y, a1.z, a1.w,
@@ -279,7 +189,7 @@ __global__ __launch_bounds__(64 * kMd5Waves) void md5_stage_kernel(
         c = chain16<SAR>(sD, c, a3, K16);
     };
 
-    if (__all((((uintptr_t)p) & 15u) == 0)) {
+    {
         uint64_t mx = nblk;
 #pragma unroll
         for (int o = 32; o; o >>= 1) {
@@ -293,7 +203,7 @@ __global__ __launch_bounds__(64 * kMd5Waves) void md5_stage_kernel(
 #pragma unroll
         for (int k = 0; k < NLD; k++) {
             const int src = k * FPI + fsub;
-            lp[k] = reinterpret_cast<const uint8_t *>(__shfl((uintptr_t)p, src)) + piece * 16;
+            lp[k] = reinterpret_cast<const uint8_t *>(__shfl((uintptr_t)s0, src)) + piece * 16;
             lim[k] = __shfl(nblk, src) * 4;
         }
         u32x4 RA[NLD], RB[NLD];
@@ -314,7 +224,6 @@ __global__ __launch_bounds__(64 * kMd5Waves) void md5_stage_kernel(
                 *reinterpret_cast<u32x4 *>(tile + (k * FPI + fsub) * STRIDE + piece * 16) = R[k];
             __builtin_amdgcn_wave_barrier();
         };
-        const uint8_t *mine = tile + lane * STRIDE;
         auto hash_round = [&](uint64_t r) {
 #pragma unroll
             for (int b = 0; b < BPR; b++) {
@@ -338,24 +247,39 @@ __global__ __launch_bounds__(64 * kMd5Waves) void md5_stage_kernel(
         asm volatile("s_waitcnt vmcnt(0)"
                      : "+v"(RA[0]), "+v"(RA[1]), "+v"(RA[2]), "+v"(RA[3]), "+v"(RA[4]), "+v"(RA[5]),
                        "+v"(RA[6]), "+v"(RA[7]) :: "memory");
-    } else {
-        // some file of this wave starts off a 16-byte boundary: lane-serial
-        // byte-assembled loads (rare; bulk-ingest batches are aligned)
-        for (uint64_t j = 0; j < nblk; j++) {
-            const uint8_t *q = p + j * 64;
-            block(load16(q, false), load16(q + 16, false), load16(q + 32, false), load16(q + 48, false));
-        }
     }
     if (valid) {
-        for (uint64_t k = nblk << 6; k < L; k++)  // CRC of the L & 63 tail bytes
-            c = crc_byte<SAR>(sT, c, p[k]);
-        md5_finish(st, p, nblk, L);
-        crc_out[f] = c ^ 0xFFFFFFFFu;  // CRC32_FINAL (storage/storage_dio.c:500)
-        if (sig_out)  // memcpy(sig + 8, md5 digest, 16) (storage/storage_service.c:119)
-            store_sig(sig_out + 24ull * f, L, st[0], st[1], st[2], st[3]);
-        if (codes_out)
-            reinterpret_cast<int4 *>(codes_out)[f] =
-                make_int4((int)st[0], (int)st[1], (int)st[2], (int)st[3]);
+        const uint8_t *tp = s0 + (nblk << 6);
+        const uint32_t r = (uint32_t)((L - pre) & 63u);
+        for (uint32_t k = 0; k < r; k++)  // CRC of the tail bytes
+            c = crc_byte<SAR>(sT, c, tp[k]);
+        if constexpr (ST) {
+            // the new pending bytes: the chunk appended to a still-partial
+            // buffer, or the chunk's last (L - pre) & 63 bytes
+            if (have && have + L < 64) {
+                for (uint32_t k = 0; k < (uint32_t)L; k++)
+                    fs->md5_buffer[have + k] = p[k];
+            } else {
+                for (uint32_t k = 0; k < r; k++)
+                    fs->md5_buffer[k] = tp[k];
+            }
+            fs->crc32 = (int32_t)c;
+#pragma unroll
+            for (int k = 0; k < 4; k++)
+                fs->md5_state[k] = st[k];
+            uint32_t cnt[2] = {fs->md5_count[0], fs->md5_count[1]};
+            count_add(cnt, L);
+            fs->md5_count[0] = cnt[0];
+            fs->md5_count[1] = cnt[1];
+        } else {
+            md5_finish(st, tp, L);
+            crc_out[f] = c ^ 0xFFFFFFFFu;  // CRC32_FINAL (storage/storage_dio.c:500)
+            if (sig_out)  // memcpy(sig + 8, md5 digest, 16) (storage/storage_service.c:119)
+                store_sig(sig_out + 24ull * f, L, st[0], st[1], st[2], st[3]);
+            if (codes_out)
+                reinterpret_cast<int4 *>(codes_out)[f] =
+                    make_int4((int)st[0], (int)st[1], (int)st[2], (int)st[3]);
+        }
     }
     if (!queue)
         break;
@@ -369,7 +293,8 @@ __global__ __launch_bounds__(64 * kMd5Waves) void md5_stage_kernel(
 hipError_t launch_md5_stage(bool sar, const uint8_t *base, const uint64_t *offs,
                             const uint64_t *sizes, uint32_t n, const uint32_t *order,
                             const DevTables *tabs, uint32_t *queue, uint32_t *crc_out, uint8_t *sig_out,
-                            int32_t *codes_out, hipStream_t st)
+                            int32_t *codes_out, fdfs_gpu_file_state *states, const uint32_t *sidx,
+                            hipStream_t st)
 {
     static int ncu[64];
     int dev = 0;
@@ -400,12 +325,14 @@ hipError_t launch_md5_stage(bool sar, const uint8_t *base, const uint64_t *offs,
         grid = g < (nw + kMd5Waves - 1) / kMd5Waves ? g : (nw + kMd5Waves - 1) / kMd5Waves;
     }
     const uint32_t w1 = (uint32_t)ncu[dev] * kMd5Waves;
-    if (sar)
-        md5_stage_kernel<true><<<grid, kBlk, 0, st>>>(base, offs, sizes, order, n, tabs, w1, q, crc_out,
-                                                      sig_out, codes_out);
+#define MD5_LAUNCH(S, T)                                                                              \
+    md5_stage_kernel<S, T><<<grid, kBlk, 0, st>>>(base, offs, sizes, order, n, tabs, w1, q, crc_out, \
+                                                  sig_out, codes_out, states, sidx)
+    if (states)
+        sar ? MD5_LAUNCH(true, true) : MD5_LAUNCH(false, true);
     else
-        md5_stage_kernel<false><<<grid, kBlk, 0, st>>>(base, offs, sizes, order, n, tabs, w1, q, crc_out,
-                                                       sig_out, codes_out);
+        sar ? MD5_LAUNCH(true, false) : MD5_LAUNCH(false, false);
+#undef MD5_LAUNCH
     return hipGetLastError();
 }
 

@@ -556,6 +556,33 @@ __global__ void big_patch_kernel(const uint32_t *__restrict__ nbig, const uint32
     }
 }
 
+// The same for the chunked update (fdfs_gpu_update_batch): the segmented
+// kernels hashed each big chunk from the one-shot start (XINIT for the CRC,
+// 0 for the polynomials), so the chunk's state is carried over it here:
+// CRC32_ex(d, X) = FINAL-form crc ^ ~0 ^ M^|d| (X ^ ~0) and
+// h(d, X) = M^|d| X + h(d, 0) for simple_hash / Time33 (orders divide 2^30).
+__global__ void big_patch_state_kernel(const uint32_t *__restrict__ nbig, const uint32_t *__restrict__ order,
+                                       const uint32_t *__restrict__ bcrc, const uint32_t *__restrict__ bpoly,
+                                       const uint64_t *__restrict__ sizes, const uint32_t *__restrict__ sidx,
+                                       fdfs_gpu_file_state *__restrict__ states,
+                                       const DevTables *__restrict__ tabs)
+{
+    const uint32_t nb = *nbig;
+    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < nb; i += gridDim.x * blockDim.x) {
+        const uint32_t f = order[i];
+        const uint64_t L = sizes[f];
+        fdfs_gpu_file_state *fs = states + (sidx ? sidx[f] : f);
+        const uint32_t c = bcrc[i] ^ 0xFFFFFFFFu ^ advance_bytes(tabs->t, ~(uint32_t)fs->crc32, L);
+        const uint32_t e = (uint32_t)(L & 0x3FFFFFFFull);
+        const uint32_t s = pow_dev(31u, e) * (uint32_t)fs->hash_codes[2] + bpoly[2ull * i];
+        const uint32_t t = pow_dev(33u, e) * (uint32_t)fs->hash_codes[3] + bpoly[2ull * i + 1];
+        fs->crc32 = (int32_t)c;
+        fs->hash_codes[0] = (int32_t)c;
+        fs->hash_codes[2] = (int32_t)s;
+        fs->hash_codes[3] = (int32_t)t;
+    }
+}
+
 // ------------------------------------------------------------------ launchers
 
 hipError_t launch_exclusive_scan(const uint64_t *in, uint64_t n, uint64_t *out, uint64_t *bsum,
@@ -579,7 +606,8 @@ static hipError_t crc_seg_run(bool sar, const uint8_t *base, const uint64_t *off
 hipError_t launch_sig_lane(bool sar, int method, const uint8_t *base, const uint64_t *offs,
                            const uint64_t *sizes, uint32_t n, uint32_t *hist, uint32_t *order,
                            const BigCrcWs *big, const DevTables *tabs, uint32_t *crc_out,
-                           uint8_t *sig_out, int32_t *codes_out, unsigned seg_grid, hipStream_t st,
+                           uint8_t *sig_out, int32_t *codes_out, fdfs_gpu_file_state *states,
+                           const uint32_t *sidx, unsigned seg_grid, hipStream_t st,
                            hipEvent_t ev0, hipEvent_t ev1)
 {
     hipError_t e = hipMemsetAsync(hist, 0, sizeof(uint32_t) * kLaneWsDwords, st);
@@ -604,14 +632,18 @@ hipError_t launch_sig_lane(bool sar, int method, const uint8_t *base, const uint
     if (ev0)
         (void)hipEventRecord(ev0, st);
     e = (method == 2) ? launch_md5_stage(sar, base, offs, sizes, n, order, tabs, hist + 2 * kSizeBins,
-                                         crc_out, sig_out, codes_out, st)
+                                         crc_out, sig_out, codes_out, states, sidx, st)
                       : launch_sig_hash(sar, base, offs, sizes, n, order, tabs,
-                                        offload ? kBigCrcMin : ~0ull, crc_out, sig_out, codes_out, st);
+                                        offload ? kBigCrcMin : ~0ull, crc_out, sig_out, codes_out, states,
+                                        sidx, st);
     if (e != hipSuccess)
         return e;
     if (ev1)
         (void)hipEventRecord(ev1, st);
-    if (offload)
+    if (offload && states)
+        big_patch_state_kernel<<<256, 256, 0, st>>>(big->nbig, order, big->crc, big->poly, sizes, sidx, states,
+                                                    tabs);
+    else if (offload)
         big_patch_kernel<<<256, 256, 0, st>>>(big->nbig, order, big->crc, big->poly, crc_out, sig_out,
                                               codes_out);
     return hipGetLastError();

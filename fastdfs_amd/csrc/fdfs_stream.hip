@@ -1,0 +1,143 @@
+// Chunked (state-carrying) form of the upload path: the per-file
+// StorageFileContext state (storage/storage_nio.h:94-96) that
+// storage_write_to_file initialises (storage/storage_service.c:7147-7161),
+// dio_write_file advances one received chunk at a time
+// (storage/storage_dio.c:465-483) and finalises after the last chunk
+// (storage/storage_dio.c:498-515), for a batch of uploads per call.
+//
+// The heavy per-chunk work is the one-shot kernels run in their state mode
+// (sig_hash_kernel / md5_stage_kernel, fdfs_hash.hip / fdfs_md5.hip) or, for
+// CRC only, the segmented kernel followed by crc_carry_kernel below.  This
+// file holds the small per-file kernels around them.
+#include "fdfs_device.hpp"
+#include "fdfs_kernels.hpp"
+#include "fdfs_md5.hpp"
+
+namespace fdfs {
+
+static_assert(sizeof(fdfs_gpu_file_state) == 128, "fdfs_gpu_file_state is 128 bytes");
+
+__global__ void state_init_kernel(fdfs_gpu_file_state *__restrict__ states, uint32_t n)
+{
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n)
+        return;
+    fdfs_gpu_file_state *fs = states + i;
+    fs->crc32 = (int32_t)0xFFFFFFFFu;  // CRC32_XINIT (storage/storage_service.c:7149)
+    fs->hash_codes[0] = (int32_t)0xFFFFFFFFu;  // INIT_HASH_CODES4 (:7156)
+    fs->hash_codes[1] = 0;
+    fs->hash_codes[2] = 0;
+    fs->hash_codes[3] = 0;
+    fs->md5_state[0] = 0x67452301u;  // my_md5_init (:7160)
+    fs->md5_state[1] = 0xefcdab89u;
+    fs->md5_state[2] = 0x98badcfeu;
+    fs->md5_state[3] = 0x10325476u;
+    fs->md5_count[0] = 0;
+    fs->md5_count[1] = 0;
+}
+
+// CRC_ONLY update: crc[f] = CRC32_FINAL(CRC32_ex(chunk f, XINIT)) as the
+// segmented kernel leaves it; the chunk's own running value X carries over
+// as CRC32_ex(d, X) = crc ^ ~0 ^ M^|d| (X ^ ~0) (linear over GF(2)).
+__global__ void crc_carry_kernel(const uint32_t *__restrict__ crc, const uint64_t *__restrict__ sizes,
+                                 uint32_t n, const uint32_t *__restrict__ sidx,
+                                 fdfs_gpu_file_state *__restrict__ states, const DevTables *__restrict__ tabs)
+{
+    const uint32_t f = blockIdx.x * blockDim.x + threadIdx.x;
+    if (f >= n)
+        return;
+    const uint64_t L = sizes[f];
+    fdfs_gpu_file_state *fs = states + (sidx ? sidx[f] : f);
+    fs->crc32 = (int32_t)(crc[f] ^ 0xFFFFFFFFu ^ advance_bytes(tabs->t, ~(uint32_t)fs->crc32, L));
+    uint32_t cnt[2] = {fs->md5_count[0], fs->md5_count[1]};
+    count_add(cnt, L);
+    fs->md5_count[0] = cnt[0];
+    fs->md5_count[1] = cnt[1];
+}
+
+// CRC32_FINAL, FINISH_HASH_CODES4 / my_md5_final and
+// STORAGE_GEN_FILE_SIGNATURE (storage/storage_service.c:106-120) of state
+// sidx[i]; the state itself is left as it is.
+__global__ void final_kernel(int method, const fdfs_gpu_file_state *__restrict__ states,
+                             const uint32_t *__restrict__ sidx, uint32_t n, uint32_t *__restrict__ crc_out,
+                             uint8_t *__restrict__ sig_out, int32_t *__restrict__ codes_out)
+{
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n)
+        return;
+    const fdfs_gpu_file_state *fs = states + (sidx ? sidx[i] : i);
+    const uint32_t crc = (uint32_t)fs->crc32 ^ 0xFFFFFFFFu;  // CRC32_FINAL (storage/storage_dio.c:500)
+    crc_out[i] = crc;
+    if (method == FDFS_SIG_CRC_ONLY)
+        return;
+    const uint32_t lo = fs->md5_count[0], hi = fs->md5_count[1];
+    const uint64_t L = ((uint64_t)hi << 32 | lo) >> 3;
+    uint32_t w[4];
+    if (method == FDFS_SIG_HASH) {  // FINISH_HASH_CODES4 (:508): only h[0] is finalised
+        w[0] = (uint32_t)fs->hash_codes[0] ^ 0xFFFFFFFFu;
+        w[1] = (uint32_t)fs->hash_codes[1];
+        w[2] = (uint32_t)fs->hash_codes[2];
+        w[3] = (uint32_t)fs->hash_codes[3];
+    } else {  // my_md5_final (:512) over the pending (count / 8) % 64 bytes
+        uint32_t st[4] = {fs->md5_state[0], fs->md5_state[1], fs->md5_state[2], fs->md5_state[3]};
+        uint32_t m[16];
+        const uint32_t *b = reinterpret_cast<const uint32_t *>(fs->md5_buffer);
+#pragma unroll
+        for (int k = 0; k < 16; k++)
+            m[k] = b[k];
+        md5_pad_compress(st, m, (lo >> 3) & 63u, lo, hi);
+#pragma unroll
+        for (int k = 0; k < 4; k++)
+            w[k] = st[k];
+    }
+    if (codes_out)
+        reinterpret_cast<int4 *>(codes_out)[i] = make_int4((int)w[0], (int)w[1], (int)w[2], (int)w[3]);
+    if (sig_out) {  // long2buff(size), then int2buff x4 (hash) or the raw digest (MD5)
+        uint32_t *sp = reinterpret_cast<uint32_t *>(sig_out + 24ull * i);
+        sp[0] = bswap32((uint32_t)(L >> 32));
+        sp[1] = bswap32((uint32_t)L);
+#pragma unroll
+        for (int k = 0; k < 4; k++)
+            sp[2 + k] = method == FDFS_SIG_HASH ? bswap32(w[k]) : w[k];
+    }
+}
+
+__global__ void crc_combine_kernel(const uint32_t *__restrict__ a, const uint32_t *__restrict__ b,
+                                   const uint64_t *__restrict__ len_b, uint32_t n, uint32_t *__restrict__ out,
+                                   const DevTables *__restrict__ tabs)
+{
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n)
+        out[i] = advance_bytes(tabs->t, a[i], len_b[i]) ^ b[i];
+}
+
+static unsigned blocks(uint32_t n) { return (n + 255) / 256; }
+
+hipError_t launch_state_init(fdfs_gpu_file_state *states, uint32_t n, hipStream_t st)
+{
+    state_init_kernel<<<blocks(n), 256, 0, st>>>(states, n);
+    return hipGetLastError();
+}
+
+hipError_t launch_crc_carry(const uint32_t *crc, const uint64_t *sizes, uint32_t n, const uint32_t *sidx,
+                            fdfs_gpu_file_state *states, const DevTables *tabs, hipStream_t st)
+{
+    crc_carry_kernel<<<blocks(n), 256, 0, st>>>(crc, sizes, n, sidx, states, tabs);
+    return hipGetLastError();
+}
+
+hipError_t launch_final(int method, const fdfs_gpu_file_state *states, const uint32_t *sidx, uint32_t n,
+                        uint32_t *crc_out, uint8_t *sig_out, int32_t *codes_out, hipStream_t st)
+{
+    final_kernel<<<blocks(n), 256, 0, st>>>(method, states, sidx, n, crc_out, sig_out, codes_out);
+    return hipGetLastError();
+}
+
+hipError_t launch_crc_combine(const uint32_t *a, const uint32_t *b, const uint64_t *len_b, uint32_t n,
+                              uint32_t *out, const DevTables *tabs, hipStream_t st)
+{
+    crc_combine_kernel<<<blocks(n), 256, 0, st>>>(a, b, len_b, n, out, tabs);
+    return hipGetLastError();
+}
+
+}  // namespace fdfs

@@ -70,3 +70,47 @@ def test_context_refuses_cpu_tensors():
     from fastdfs_amd.api import _check_dev
     with pytest.raises(ValueError, match="no CPU path"):
         _check_dev(torch.zeros(4, dtype=torch.uint8), "data", torch.uint8)
+
+
+def test_production_library_reads_no_environment():
+    """No environment variable can change a result: the production .so does
+    not import getenv/secure_getenv (the probe knobs live in `make probes`)."""
+    out = subprocess.run(["nm", "-D", "--undefined-only", _lib.LIB_PATH], capture_output=True,
+                         text=True, check=True).stdout
+    assert not re.search(r"\b(secure_)?getenv\b", out)
+
+
+def test_file_state_layout_matches_storage_file_context():
+    """fdfs_gpu_file_state mirrors StorageFileContext's hash fields
+    (storage/storage_nio.h:94-96: int crc32; int file_hash_codes[4];
+    MD5_CTX {UINT4 state[4]; UINT4 count[2]; unsigned char buffer[64]}),
+    compiled by the host C compiler from the public header."""
+    import tempfile
+    src = r'''
+#include <stddef.h>
+#include <stdio.h>
+#include "fdfs_gpu.h"
+int main(void) {
+    printf("%zu %zu %zu %zu %zu %zu\n", sizeof(fdfs_gpu_file_state),
+           offsetof(fdfs_gpu_file_state, crc32), offsetof(fdfs_gpu_file_state, hash_codes),
+           offsetof(fdfs_gpu_file_state, md5_state), offsetof(fdfs_gpu_file_state, md5_count),
+           offsetof(fdfs_gpu_file_state, md5_buffer));
+    return 0;
+}
+'''
+    with tempfile.TemporaryDirectory() as d:
+        c = os.path.join(d, "t.c")
+        open(c, "w").write(src)
+        exe = os.path.join(d, "t")
+        subprocess.run(["gcc", "-std=c99", "-I", os.path.dirname(_lib.HEADER_PATH), "-o", exe, c],
+                       check=True)
+        got = subprocess.run([exe], capture_output=True, text=True, check=True).stdout.split()
+    assert [int(x) for x in got] == [_lib.FILE_STATE_SIZE, 0, 4, 20, 36, 44]
+
+
+def test_stream_api_argument_errors():
+    L = _lib.load()
+    assert L.fdfs_gpu_state_init(None, None, 1, None) == errno.EINVAL
+    assert L.fdfs_gpu_update_batch(None, None, None, 0, None, None) == errno.EINVAL
+    assert L.fdfs_gpu_final_batch(None, None, None, 1, 0, None, None, None, None) == errno.EINVAL
+    assert L.fdfs_gpu_crc_combine(None, None, None, None, 1, None, None) == errno.EINVAL

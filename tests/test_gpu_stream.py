@@ -1,0 +1,238 @@
+"""GPU parity of the chunked (state-carrying) path: fdfs_gpu_state_init /
+update_batch / final_batch, i.e. the per-chunk loop of dio_write_file
+(storage/storage_dio.c:465-515) on the GPU, against the oracle's one-shot
+result (chunking never changes the reference's values: every primitive is a
+streaming recurrence) and against the GPU one-shot path.
+"""
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def ctxs():
+    import fastdfs_amd as F
+    if not torch.cuda.is_available():
+        pytest.fail("gpu test collected without a GPU")
+    return {0: F.Context(0, unsigned_hash=False), 1: F.Context(0, unsigned_hash=True)}
+
+
+def _splits(rng, size, small_frac=0.3, max_chunk=70_000):
+    """Random cut points of one file: chunk sizes mix tiny (<= 63, MD5 tail
+    fills), zero-length and 1..max_chunk byte chunks."""
+    cuts, pos = [], 0
+    while pos < size:
+        u = rng.random()
+        if u < small_frac:
+            step = int(rng.integers(0, 64))
+        else:
+            step = int(rng.integers(1, max_chunk))
+        step = min(step, size - pos)
+        cuts.append(step)
+        pos += step
+    if not cuts or rng.random() < 0.2:
+        cuts.append(0)  # an empty chunk (a zero-length update)
+    return cuts
+
+
+def _stream(ctx, method, files, rng, order_shuffle=True, dev="cuda:0"):
+    """Feed every file chunk by chunk: call k carries chunk k of each file
+    that has one, the chunks placed at random byte alignment in a fresh
+    device buffer, in a random order, addressed by state_idx."""
+    n = len(files)
+    cuts = [_splits(rng, len(f)) for f in files]
+    states = ctx.new_states(n)
+    starts = [0] * n
+    k = 0
+    while True:
+        live = [i for i in range(n) if k < len(cuts[i])]
+        if not live:
+            break
+        if order_shuffle:
+            rng.shuffle(live)
+        offs, sizes, parts, pos = [], [], [], 0
+        for i in live:
+            pos += int(rng.integers(0, 16))
+            c = cuts[i][k]
+            offs.append(pos)
+            sizes.append(c)
+            parts.append((pos, files[i][starts[i]: starts[i] + c]))
+            starts[i] += c
+            pos += c
+        buf = np.zeros(pos + 16, np.uint8)
+        for p0, b in parts:
+            buf[p0: p0 + len(b)] = b
+        ctx.update_batch(states, torch.from_numpy(buf).to(dev),
+                         torch.tensor(offs, dtype=torch.int64, device=dev),
+                         torch.tensor(sizes, dtype=torch.int64, device=dev), method=method,
+                         state_idx=torch.tensor(live, dtype=torch.int32, device=dev))
+        k += 1
+    assert all(starts[i] == len(files[i]) for i in range(n))
+    return states, k
+
+
+def _final(ctx, states, method):
+    crc, sig, codes = ctx.final_batch(states, method=method, want_codes=True)
+    torch.cuda.synchronize()
+    crc = crc.cpu().numpy().view(np.uint32)
+    if method == 0:
+        return crc, None, None
+    return crc, sig.cpu().numpy(), codes.cpu().numpy()
+
+
+def _files(rng, sizes):
+    return [rng.integers(0, 256, size=int(s), dtype=np.uint8) for s in sizes]
+
+
+@pytest.mark.parametrize("variant", [0, 1])
+@pytest.mark.parametrize("method", [0, 1, 2])
+def test_random_chunking_vs_oracle(oracle, ctxs, variant, method):
+    """Random files cut at random chunk boundaries (tiny, empty and large
+    chunks, any alignment), fed over many calls: the final CRC / signature /
+    codes equal the oracle's one-shot values and the GPU one-shot path's."""
+    rng = np.random.default_rng(500 + 10 * method + variant)
+    sizes = np.concatenate([[0, 1, 63, 64, 65, 127, 128, 129], rng.integers(0, 300_000, 150)])
+    files = _files(rng, sizes)
+    states, calls = _stream(ctxs[variant], method, files, rng)
+    assert calls > 5
+    crc, sig, codes = _final(ctxs[variant], states, method)
+    for i, f in enumerate(files):
+        oc, os_, ocodes = oracle.dio_file(f, method, variant)
+        assert crc[i] == oc, (i, len(f))
+        if method:
+            assert sig[i].tobytes() == os_, (i, len(f))
+            assert [int(x) for x in codes[i]] == ocodes, (i, len(f))
+    # the one-shot GPU path over the same files agrees
+    offs = np.zeros(len(files), np.int64)
+    offs[1:] = np.cumsum([len(f) for f in files])[:-1]
+    data = torch.from_numpy(np.concatenate(files + [np.zeros(16, np.uint8)])).cuda()
+    c1, s1, _ = ctxs[variant].sig_batch(data, torch.from_numpy(offs).cuda(),
+                                        torch.from_numpy(sizes.astype(np.int64)).cuda(), method=method)
+    assert np.array_equal(c1.cpu().numpy().view(np.uint32), crc)
+    if method:
+        assert np.array_equal(s1.cpu().numpy(), sig)
+
+
+@pytest.mark.parametrize("method", [1, 2])
+def test_state_matches_oracle_mid_stream(oracle, ctxs, method):
+    """The state after each chunk is the reference's running state: crc32 =
+    CRC32_ex(prefix, XINIT), hash codes = CALC_HASH_CODES4 over the prefix,
+    MD5 count and pending-buffer bytes as my_md5_update leaves them."""
+    rng = np.random.default_rng(77 + method)
+    f = rng.integers(0, 256, size=200_003, dtype=np.uint8)
+    ctx = ctxs[0]
+    states = ctx.new_states(1)
+    pos = 0
+    for c in [5, 59, 0, 64, 1000, 63, 70_000, 1, 128_811]:
+        d = torch.from_numpy(f[pos: pos + c].copy() if c else np.zeros(1, np.uint8)).cuda()
+        ctx.update_batch(states, d, torch.zeros(1, dtype=torch.int64, device="cuda"),
+                         torch.tensor([c], dtype=torch.int64, device="cuda"), method=method)
+        pos += c
+        st = states.cpu().numpy()[0]
+        crc32 = int(st[0:4].view(np.int32)[0])
+        assert crc32 == oracle.crc32_ex(f[:pos], -1, 0), pos
+        bits = int(st[36:44].view(np.uint64)[0])
+        assert bits == 8 * pos
+        if method == 1:
+            h = st[4:20].view(np.int32)
+            assert int(h[0]) == crc32
+            assert int(h[1]) == oracle.elf_ex(f[:pos], 0, 0)
+            assert int(h[2]) == oracle.simple_ex(f[:pos], 0)
+            assert int(h[3]) == oracle.time33_ex(f[:pos], 0)
+        else:
+            r = pos % 64
+            assert st[44: 44 + r].tobytes() == f[pos - r: pos].tobytes()
+    assert pos == f.size
+
+
+@pytest.mark.parametrize("variant", [0, 1])
+def test_big_chunks_hash(oracle, ctxs, variant):
+    """HASH updates with chunks >= 4 MiB take the segment-parallel CRC and
+    polynomial kernels; the state they start from is carried over them
+    (GF(2) advance for the CRC, M^len for simple_hash / Time33)."""
+    rng = np.random.default_rng(91 + variant)
+    files = _files(rng, [(9 << 20) + 12345, (5 << 20) + 7, 300_000])
+    cuts = [[1234, (4 << 20) + 5, (9 << 20) + 12345 - 1234 - (4 << 20) - 5],
+            [17, (5 << 20) - 10],
+            [150_000, 150_000]]
+    cuts[1].append(len(files[1]) - sum(cuts[1]))
+    ctx = ctxs[variant]
+    states = ctx.new_states(3)
+    pos = [0, 0, 0]
+    for k in range(3):
+        live = [i for i in range(3) if k < len(cuts[i])]
+        offs, sizes, chunks, p = [], [], [], 0
+        for i in live:
+            c = cuts[i][k]
+            offs.append(p + 3)
+            sizes.append(c)
+            chunks.append(np.zeros(3, np.uint8))
+            chunks.append(files[i][pos[i]: pos[i] + c])
+            pos[i] += c
+            p += 3 + c
+        ctx.update_batch(states, torch.from_numpy(np.concatenate(chunks)).cuda(),
+                         torch.tensor(offs, dtype=torch.int64, device="cuda"),
+                         torch.tensor(sizes, dtype=torch.int64, device="cuda"), method=1,
+                         state_idx=torch.tensor(live, dtype=torch.int32, device="cuda"))
+    assert pos == [len(f) for f in files]
+    crc, sig, codes = _final(ctx, states, 1)
+    for i, f in enumerate(files):
+        oc, os_, ocodes = oracle.dio_file(f, 1, variant)
+        assert crc[i] == oc and sig[i].tobytes() == os_ and [int(x) for x in codes[i]] == ocodes, i
+
+
+@pytest.mark.parametrize("variant", [0, 1])
+def test_crc_combine(oracle, ctxs, variant):
+    """crc32_combine: CRC32_ex(A||B, X) from CRC32_ex(A, X), CRC32_ex(B, 0), |B|."""
+    rng = np.random.default_rng(3 + variant)
+    a_list, b_list, want = [], [], []
+    for la, lb in [(0, 0), (0, 5), (7, 0), (100, 1), (4096, 65536), (12345, 1 << 20), (3, (1 << 22) + 9)]:
+        a = rng.integers(0, 256, la, dtype=np.uint8)
+        b = rng.integers(0, 256, lb, dtype=np.uint8)
+        a_list.append(oracle.crc32_ex(a, -1, variant))
+        b_list.append(oracle.crc32_ex(b, 0, variant))
+        want.append((oracle.crc32_ex(np.concatenate([a, b]), -1, variant) & 0xFFFFFFFF, lb))
+    out = ctxs[variant].crc_combine(torch.tensor(a_list, dtype=torch.int32).cuda(),
+                                    torch.tensor(b_list, dtype=torch.int32).cuda(),
+                                    torch.tensor([w[1] for w in want], dtype=torch.int64).cuda())
+    got = out.cpu().numpy().view(np.uint32)
+    assert [int(x) for x in got] == [w[0] for w in want]
+
+
+def test_many_uploads_one_chunk_each(oracle, ctxs):
+    """The daemon's shape: 20K concurrent uploads, each call advances every
+    one by one 256 KiB-or-less chunk (the first shorter by a header), MD5."""
+    rng = np.random.default_rng(12)
+    sizes = rng.integers(0, 1_200_000, 2000)
+    files = _files(rng, sizes)
+    ctx = ctxs[0]
+    n = len(files)
+    states = ctx.new_states(n)
+    pos = np.zeros(n, np.int64)
+    first = rng.integers(200_000, 262_144, n)
+    k = 0
+    while True:
+        live = [i for i in range(n) if pos[i] < len(files[i]) or (k == 0)]
+        if not live:
+            break
+        offs, szs, parts, p = [], [], [], 0
+        for i in live:
+            c = int(min(first[i] if k == 0 else 262_144, len(files[i]) - pos[i]))
+            offs.append(p)
+            szs.append(c)
+            parts.append(files[i][pos[i]: pos[i] + c])
+            pos[i] += c
+            p += c
+        ctx.update_batch(states, torch.from_numpy(np.concatenate(parts + [np.zeros(1, np.uint8)])).cuda(),
+                         torch.tensor(offs, dtype=torch.int64, device="cuda"),
+                         torch.tensor(szs, dtype=torch.int64, device="cuda"), method=2,
+                         state_idx=torch.tensor(live, dtype=torch.int32, device="cuda"))
+        k += 1
+    crc, sig, _ = _final(ctx, states, 2)
+    offs = np.zeros(n, np.uint64)
+    offs[1:] = np.cumsum(sizes)[:-1]
+    ocrc, osig = oracle.dio_batch(np.concatenate(files), offs, sizes.astype(np.uint64), 2, 0, nthreads=8)
+    assert np.array_equal(crc, ocrc)
+    assert np.array_equal(sig, osig)
