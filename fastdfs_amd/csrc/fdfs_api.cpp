@@ -486,38 +486,59 @@ int fdfs_gpu_crc_combine(fdfs_gpu_ctx *ctx, const uint32_t *crc_a, const uint32_
     return e == hipSuccess ? 0 : fail(ctx, e, "crc_combine launch");
 }
 
-// ---- host-resident batches: chunked, double-buffered H2D / hash / D2H -------
+// ---- host-resident batches: windows of chunks through the chunked path -----
 
 extern "C++" {
 namespace {
 
-struct HostChunk {
-    uint32_t i0, i1;   // files [i0, i1)
-    uint64_t lo, hi;   // host byte window copied for them
+struct HostPiece {
+    uint32_t file;
+    uint64_t at, len;  // host byte range of this piece of the file
 };
 
-// Consecutive files whose byte ranges fit one window of <= chunk bytes (a
-// file larger than that is a chunk alone).  Packed batches (increasing
-// offsets) copy each byte once.
-std::vector<HostChunk> plan_host_chunks(const uint64_t *off, const uint64_t *sz, uint32_t n,
-                                        uint64_t chunk, uint32_t max_files)
+struct HostWindow {
+    uint64_t lo, hi;   // host bytes copied for the window
+    size_t p0, p1;     // its pieces
+};
+
+// Windows of at most `chunk` host bytes, each holding at most one piece of
+// any file (the update contract): files are taken in order, a file larger
+// than the space left is cut and continues in the next window, so every
+// window fits its slot whatever the file sizes.  Packed batches (increasing
+// offsets) copy each byte once; a file that starts before the window does
+// opens a new one.  Empty files get no piece (init + final is their result).
+void plan_host_windows(const uint64_t *off, const uint64_t *sz, uint32_t n, uint64_t chunk,
+                       uint32_t max_pieces, std::vector<HostPiece> &pieces, std::vector<HostWindow> &wins)
 {
-    std::vector<HostChunk> out;
     uint32_t i = 0;
+    uint64_t a = 0;  // bytes of file i already placed
     while (i < n) {
-        HostChunk c{i, i + 1, off[i], off[i] + sz[i]};
-        for (uint32_t j = i + 1; j < n && j - i < max_files; j++) {
-            const uint64_t lo = std::min(c.lo, off[j]), hi = std::max(c.hi, off[j] + sz[j]);
-            if (hi - lo > chunk)
-                break;
-            c.lo = lo;
-            c.hi = hi;
-            c.i1 = j + 1;
+        if (sz[i] == 0) {
+            i++;
+            continue;
         }
-        out.push_back(c);
-        i = c.i1;
+        HostWindow w{off[i] + a, off[i] + a, pieces.size(), pieces.size()};
+        while (i < n && w.p1 - w.p0 < max_pieces) {
+            if (sz[i] == 0) {
+                i++;
+                a = 0;
+                continue;
+            }
+            const uint64_t s = off[i] + a;
+            if (s < w.lo || s >= w.lo + chunk)
+                break;
+            const uint64_t take = std::min(sz[i] - a, w.lo + chunk - s);
+            pieces.push_back({i, s, take});
+            w.p1++;
+            w.hi = std::max(w.hi, s + take);
+            a += take;
+            if (a < sz[i])
+                break;  // the window is full: the file continues in the next one
+            i++;
+            a = 0;
+        }
+        wins.push_back(w);
     }
-    return out;
 }
 
 }  // namespace
@@ -538,49 +559,36 @@ int fdfs_gpu_sig_batch_host(fdfs_gpu_ctx *ctx, const fdfs_gpu_batch *hb, int met
         return EINVAL;
     if (chunk_bytes == 0)
         chunk_bytes = 256ull << 20;
-    constexpr uint32_t kMaxChunkFiles = 1u << 20;
+    constexpr uint32_t kMaxPieces = 1u << 20;
     std::lock_guard<std::recursive_mutex> lk(ctx->mu);
     DeviceGuard g(ctx->device);
     if (!g.ok)
         return ENODEV;
-    const auto chunks = plan_host_chunks(hb->offset, hb->size, n, chunk_bytes, kMaxChunkFiles);
-    uint64_t win = 0;
-    uint32_t maxf = 0;
-    for (const auto &c : chunks) {
-        win = std::max(win, c.hi - c.lo);
-        maxf = std::max(maxf, c.i1 - c.i0);
+    std::vector<HostPiece> pieces;
+    std::vector<HostWindow> wins;
+    plan_host_windows(hb->offset, hb->size, n, chunk_bytes, kMaxPieces, pieces, wins);
+    uint64_t win = 16;
+    uint32_t maxp = 1;
+    for (const auto &w : wins) {
+        win = std::max(win, w.hi - w.lo);
+        maxp = std::max(maxp, (uint32_t)(w.p1 - w.p0));
     }
     const bool want_sig = method != FDFS_SIG_CRC_ONLY && sig_out;
     const bool want_codes = method != FDFS_SIG_CRC_ONLY && codes_out;
-    // two device slots: window bytes (16 B slack), offsets, sizes, outputs
-    const size_t slot = align_up(win + 16) + 2 * align_up(8ull * maxf) + align_up(4ull * maxf) +
-                        align_up(24ull * maxf) + align_up(16ull * maxf);
-    int rc = ensure_ws(ctx, sig_ws_bytes(maxf), nullptr);
+    // device: the n file states and results, and two window slots (bytes,
+    // then offsets / sizes / state indices of its pieces)
+    const size_t meta = 2 * align_up(8ull * maxp) + align_up(4ull * maxp);
+    const size_t slot = align_up(win + 16) + meta;
+    const size_t res = align_up(128ull * n) + align_up(4ull * n) + align_up(24ull * n) + align_up(16ull * n);
+    int rc = ensure_ws(ctx, sig_ws_bytes(maxp) + align_up(4ull * maxp), nullptr);
     if (rc)
         return rc;
-    char *dmem = nullptr;
-    uint64_t *hmeta = nullptr;  // pinned offsets/sizes of the two slots
-    char *hres = nullptr;       // pinned results of the two slots (async D2H)
-    const size_t rslot = align_up(4ull * maxf) + align_up(24ull * maxf) + align_up(16ull * maxf);
+    char *dmem = nullptr, *hmeta = nullptr;
     hipStream_t cp = nullptr, cs = nullptr;
     hipEvent_t copied[2] = {nullptr, nullptr}, done[2] = {nullptr, nullptr};
-    hipError_t e = hipMalloc(&dmem, 2 * slot);
+    hipError_t e = hipMalloc(&dmem, res + 2 * slot);
     if (e == hipSuccess)
-        e = hipHostMalloc(reinterpret_cast<void **>(&hmeta), 2 * 2 * 8ull * maxf, 0);
-    if (e == hipSuccess)
-        e = hipHostMalloc(reinterpret_cast<void **>(&hres), 2 * rslot, 0);
-    // chunk k's results: pinned slot -> the caller's arrays, once it is done
-    auto deliver = [&](size_t k) {
-        const HostChunk &c = chunks[k];
-        const uint32_t m = c.i1 - c.i0;
-        const char *r = hres + (k & 1) * rslot;
-        std::memcpy(crc_out + c.i0, r, 4ull * m);
-        if (want_sig)
-            std::memcpy(sig_out + 24ull * c.i0, r + align_up(4ull * maxf), 24ull * m);
-        if (want_codes)
-            std::memcpy(codes_out + 4ull * c.i0, r + align_up(4ull * maxf) + align_up(24ull * maxf),
-                        16ull * m);
-    };
+        e = hipHostMalloc(reinterpret_cast<void **>(&hmeta), 2 * meta, 0);
     if (e == hipSuccess)
         e = hipStreamCreateWithFlags(&cp, hipStreamNonBlocking);
     if (e == hipSuccess)
@@ -590,59 +598,58 @@ int fdfs_gpu_sig_batch_host(fdfs_gpu_ctx *ctx, const fdfs_gpu_batch *hb, int met
         if (e == hipSuccess)
             e = hipEventCreateWithFlags(&done[k], hipEventDisableTiming);
     }
+    auto *states = reinterpret_cast<fdfs_gpu_file_state *>(dmem);
+    uint32_t *d_crc = reinterpret_cast<uint32_t *>(dmem + align_up(128ull * n));
+    uint8_t *d_sig = reinterpret_cast<uint8_t *>(d_crc) + align_up(4ull * n);
+    int32_t *d_codes = reinterpret_cast<int32_t *>(d_sig + align_up(24ull * n));
+    if (e == hipSuccess)
+        rc = fdfs_gpu_state_init(ctx, states, n, cs);
     const uint8_t *hbase = static_cast<const uint8_t *>(hb->base);
-    for (size_t k = 0; k < chunks.size() && e == hipSuccess; k++) {
-        const HostChunk &c = chunks[k];
-        const uint32_t m = c.i1 - c.i0;
-        char *sl = dmem + (k & 1) * slot;
+    for (size_t k = 0; k < wins.size() && e == hipSuccess && rc == 0; k++) {
+        const HostWindow &w = wins[k];
+        const uint32_t m = (uint32_t)(w.p1 - w.p0);
+        char *sl = dmem + res + (k & 1) * slot;
         uint8_t *d_data = reinterpret_cast<uint8_t *>(sl);
-        uint64_t *d_off = reinterpret_cast<uint64_t *>(sl + align_up(win + 16));
-        uint64_t *d_sz = d_off + align_up(8ull * maxf) / 8;
-        uint32_t *d_crc = reinterpret_cast<uint32_t *>(reinterpret_cast<char *>(d_sz) + align_up(8ull * maxf));
-        uint8_t *d_sig = reinterpret_cast<uint8_t *>(d_crc) + align_up(4ull * maxf);
-        int32_t *d_codes = reinterpret_cast<int32_t *>(d_sig + align_up(24ull * maxf));
-        uint64_t *h_off = hmeta + (k & 1) * 2 * maxf, *h_sz = h_off + maxf;
-        // the slot is free once chunk k - 2 is hashed and its results are home
-        if (k >= 2) {
-            if ((e = hipEventSynchronize(done[k & 1])) != hipSuccess)
-                break;
-            deliver(k - 2);
+        char *d_meta = sl + align_up(win + 16);
+        char *h = hmeta + (k & 1) * meta;
+        // the slot (and its pinned metadata) is free once window k - 2 is hashed
+        if (k >= 2 && (e = hipEventSynchronize(done[k & 1])) != hipSuccess)
+            break;
+        auto *h_off = reinterpret_cast<uint64_t *>(h);
+        auto *h_sz = reinterpret_cast<uint64_t *>(h + align_up(8ull * maxp));
+        auto *h_idx = reinterpret_cast<uint32_t *>(h + 2 * align_up(8ull * maxp));
+        for (uint32_t j = 0; j < m; j++) {
+            const HostPiece &pc = pieces[w.p0 + j];
+            h_off[j] = pc.at - w.lo;
+            h_sz[j] = pc.len;
+            h_idx[j] = pc.file;
         }
-        char *hr = hres + (k & 1) * rslot;
-        for (uint32_t i = 0; i < m; i++) {  // rebased to the window, which lands 16-aligned
-            h_off[i] = hb->offset[c.i0 + i] - c.lo;
-            h_sz[i] = hb->size[c.i0 + i];
-        }
-        if ((e = hipMemcpyAsync(d_data, hbase + c.lo, c.hi - c.lo, hipMemcpyHostToDevice, cp)) != hipSuccess ||
-            (e = hipMemcpyAsync(d_off, h_off, 8ull * m, hipMemcpyHostToDevice, cp)) != hipSuccess ||
-            (e = hipMemcpyAsync(d_sz, h_sz, 8ull * m, hipMemcpyHostToDevice, cp)) != hipSuccess ||
+        if ((e = hipMemcpyAsync(d_data, hbase + w.lo, w.hi - w.lo, hipMemcpyHostToDevice, cp)) != hipSuccess ||
+            (e = hipMemcpyAsync(d_meta, h, meta, hipMemcpyHostToDevice, cp)) != hipSuccess ||
             (e = hipEventRecord(copied[k & 1], cp)) != hipSuccess ||
             (e = hipStreamWaitEvent(cs, copied[k & 1], 0)) != hipSuccess)
             break;
-        fdfs_gpu_batch b{d_data, d_off, d_sz, m};
-        rc = fdfs_gpu_sig_batch(ctx, &b, method, d_crc, want_sig ? d_sig : nullptr,
-                                want_codes ? d_codes : nullptr, cs);
-        if (rc)
-            break;
-        if ((e = hipMemcpyAsync(hr, d_crc, 4ull * m, hipMemcpyDeviceToHost, cs)) != hipSuccess)
-            break;
-        if (want_sig && (e = hipMemcpyAsync(hr + align_up(4ull * maxf), d_sig, 24ull * m,
-                                            hipMemcpyDeviceToHost, cs)) != hipSuccess)
-            break;
-        if (want_codes && (e = hipMemcpyAsync(hr + align_up(4ull * maxf) + align_up(24ull * maxf),
-                                              d_codes, 16ull * m, hipMemcpyDeviceToHost, cs)) != hipSuccess)
-            break;
-        if ((e = hipEventRecord(done[k & 1], cs)) != hipSuccess)
-            break;
+        fdfs_gpu_batch b{d_data, reinterpret_cast<const uint64_t *>(d_meta),
+                         reinterpret_cast<const uint64_t *>(d_meta + align_up(8ull * maxp)), m};
+        rc = fdfs_gpu_update_batch(ctx, &b, reinterpret_cast<const uint32_t *>(d_meta + 2 * align_up(8ull * maxp)),
+                                   method, states, cs);
+        if (rc == 0)
+            e = hipEventRecord(done[k & 1], cs);
+    }
+    if (e == hipSuccess && rc == 0)
+        rc = fdfs_gpu_final_batch(ctx, states, nullptr, n, method, d_crc, want_sig ? d_sig : nullptr,
+                                  want_codes ? d_codes : nullptr, cs);
+    if (e == hipSuccess && rc == 0) {
+        if ((e = hipMemcpyAsync(crc_out, d_crc, 4ull * n, hipMemcpyDeviceToHost, cs)) == hipSuccess && want_sig)
+            e = hipMemcpyAsync(sig_out, d_sig, 24ull * n, hipMemcpyDeviceToHost, cs);
+        if (e == hipSuccess && want_codes)
+            e = hipMemcpyAsync(codes_out, d_codes, 16ull * n, hipMemcpyDeviceToHost, cs);
     }
     if (cs) {
         const hipError_t e2 = hipStreamSynchronize(cs);
         if (e == hipSuccess)
             e = e2;
     }
-    if (e == hipSuccess && rc == 0)  // the last two chunks
-        for (size_t k = chunks.size() >= 2 ? chunks.size() - 2 : 0; k < chunks.size(); k++)
-            deliver(k);
     if (cp)
         (void)hipStreamSynchronize(cp);
     for (int k = 0; k < 2; k++) {
@@ -657,8 +664,6 @@ int fdfs_gpu_sig_batch_host(fdfs_gpu_ctx *ctx, const fdfs_gpu_batch *hb, int met
         (void)hipStreamDestroy(cp);
     if (hmeta)
         (void)hipHostFree(hmeta);
-    if (hres)
-        (void)hipHostFree(hres);
     if (dmem)
         (void)hipFree(dmem);
     if (rc)

@@ -90,3 +90,22 @@ def test_many_small_files(tmp_path, oracle):
     offs[1:] = np.cumsum(sizes)[:-1]
     ocrc, _ = oracle.dio_batch(np.concatenate(bufs), offs, sizes, 0, 0, nthreads=4)
     assert np.array_equal(got, ocrc)
+
+
+@pytest.mark.gpu
+def test_streamed_windows(tmp_path, oracle):
+    """Files larger than the tool's 64 MiB window continue in the next ones
+    (their CRC32_ex state carried on the device), small files around them."""
+    rng = np.random.default_rng(8)
+    sizes = [3, (130 << 20) + 17, 0, 70_000, (64 << 20), 5]
+    paths, bufs = [], []
+    for i, n in enumerate(sizes):
+        b = rng.integers(0, 256, size=n, dtype=np.uint8)
+        p = tmp_path / f"w{i}"
+        p.write_bytes(b.tobytes())
+        paths.append(str(p))
+        bufs.append(b)
+    r = _run(paths)
+    assert r.returncode == 0, r.stdout
+    got = [int(x) for x in r.stdout.split()]
+    assert got == [oracle.crc32(b) for b in bufs]
