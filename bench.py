@@ -51,8 +51,13 @@ def parse():
     p.add_argument("--warmup", type=int, default=3)
     p.add_argument("--config", default="c2", choices=["c1", "c2", "c3", "c4", "c5"])
     p.add_argument("--files", type=int, default=0, help="override files per GPU")
+    p.add_argument("--method", default="", choices=["", "crc", "hash", "md5"],
+                   help="override the config's signature method (crc = check_file_duplicate=0)")
+    p.add_argument("--align", type=int, default=16,
+                   help="file start alignment in the batch buffer (1 = packed back to back)")
     p.add_argument("--cpu-seconds", type=float, default=10.0)
-    p.add_argument("--cpu-threads", type=int, default=16)
+    p.add_argument("--cpu-threads", type=int, default=0,
+                   help="CPU baseline threads (0 = every core this process may run on)")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--unsigned-hash", action="store_true")
     return p.parse_args()
@@ -114,9 +119,14 @@ def dedup_step(ctx, sig, gidx, world, stats=None):
     return ctx.dedup(sig)
 
 
+def host_threads(args) -> int:
+    return args.cpu_threads or len(os.sched_getaffinity(0))
+
+
 def cpu_baseline(data, offs_np, sizes_np, method, variant, seconds, threads):
     """The C oracle (restated reference loops, 256 KiB chunks as dio_write_file
-    gets them) on a bounded prefix of the same batch, `threads` host threads."""
+    gets them) on a bounded prefix of the same batch, `threads` host threads,
+    one file per thread at a time."""
     from oracle import oracle as O
     O.lib()
 
@@ -147,24 +157,49 @@ def cpu_baseline(data, offs_np, sizes_np, method, variant, seconds, threads):
                       f"{dt:.1f} s", "cpu_model": cpu_model()}
 
 
-def cpu_dedup_baseline(sig: torch.Tensor, seconds: float):
-    """The oracle's grouping (sort by signature + run detection, the CPU
-    form of the FastDHT semantics) on one host core, over prefixes of the
-    bench's signatures that double until ~`seconds` of CPU work."""
+# The reference's own dedup decision costs at least one synchronous FastDHT
+# GET per uploaded file (storage/storage_service.c:2652, fdht_get_ex1), plus
+# two SETs on a miss (:2714, :2734) and an INC per link (:2984): MODELLED
+# here, not measured (no FastDHT server exists in this pipeline), at a
+# same-rack TCP round trip.
+FDHT_RTT_US = 100.0
+
+
+def fdht_model():
+    return {"kind": "modelled", "rtt_us": FDHT_RTT_US,
+            "files_per_s_per_connection": round(1e6 / FDHT_RTT_US, 1),
+            "note": "one synchronous FastDHT GET per file (storage/storage_service.c:2652) per "
+                    "dio thread; a miss adds 2 SETs, a link 1 INC (:2714,:2734,:2984)"}
+
+
+def cpu_dedup_baseline(sig: torch.Tensor, seconds: float, threads: int):
+    """The oracle's grouping (hash partition, sort by signature + run
+    detection per partition: the CPU form of the FastDHT semantics,
+    oracle/fdfs_oracle.c orc_dedup_mt) on `threads` host cores and on one,
+    over prefixes of the bench's signatures that double until ~`seconds` of
+    CPU work."""
     from oracle import oracle as O
-    n, spent, m = 1 << 20, 0.0, 0
-    while True:
-        m = min(n, sig.shape[0])
-        host = sig[:m].cpu().numpy()
-        t0 = time.perf_counter()
-        O.dedup(host)
-        spent = time.perf_counter() - t0
-        if spent * 2.5 > seconds or m == sig.shape[0]:
-            break
-        n *= 2
-    return {"value": round(m / spent, 1), "unit": "files/s", "cores": 1, "kind": "port",
-            "sample": f"first {m} of the bench's signatures, oracle/fdfs_oracle.c orc_dedup "
-                      f"({cpu_model()})"}
+
+    def rate(nt, budget):
+        n, spent, m = 1 << 20, 0.0, 0
+        while True:
+            m = min(n, sig.shape[0])
+            host = sig[:m].cpu().numpy()
+            t0 = time.perf_counter()
+            O.dedup(host, nt, partitioned=True)
+            spent = time.perf_counter() - t0
+            if spent * 2.5 > budget or m == sig.shape[0]:
+                break
+            n *= 2
+        return m / spent, m
+    r_all, m_all = rate(threads, seconds / 2)
+    r_one, m_one = rate(1, seconds / 2)
+    return {"value": round(r_all, 1), "unit": "files/s", "cores": threads, "kind": "port",
+            "sample": f"first {m_all} of the bench's signatures, oracle/fdfs_oracle.c orc_dedup_mt, "
+                      f"{threads} threads ({cpu_model()})",
+            "single_thread": {"value": round(r_one, 1), "unit": "files/s",
+                              "sample": f"first {m_one} signatures, orc_dedup_mt, 1 thread"},
+            "reference_fdht_model": fdht_model()}
 
 
 def cpu_model() -> str:
@@ -213,29 +248,6 @@ def load_valu(config: str, avg_ms: float):
     return None
 
 
-def c5_signatures(total, world, rank, dev):
-    """Config 5's signature set: `total` records, 10% duplicates drawn
-    uniformly from the 90% unique ones (seed 5); every rank derives the same
-    global set and takes its contiguous share.  Returns (sig, gidx)."""
-    per = total // world
-    g = torch.Generator(device=dev)
-    g.manual_seed(5)
-    nu = total - total // 10
-    uniq_idx = torch.randint(0, nu, (total - nu,), generator=g, device=dev)
-    lo, hi = rank * per, (rank + 1) * per if rank < world - 1 else total
-    idx = torch.arange(lo, hi, device=dev, dtype=torch.int64)
-    src = torch.where(idx < nu, idx, uniq_idx[(idx - nu).clamp(min=0, max=max(total - nu - 1, 0))])
-    # signature bytes = fixed mix of the unique id (deterministic, 16 random-looking bytes)
-    sig = torch.zeros((hi - lo, 24), dtype=torch.uint8, device=dev)
-    x = (src * (0x9E3779B97F4A7C15 - (1 << 64))) ^ 0x5DEECE66D
-    for k in range(2):
-        x = x ^ (x >> 31)
-        x = x * 0x7FB5D329728EA185
-        sig[:, 8 + 8 * k: 16 + 8 * k] = x.contiguous().view(torch.uint8).view(-1, 8)
-    sig[:, 5:8] = (src % 251).to(torch.uint8).view(-1, 1)
-    return sig, idx
-
-
 def dedup_strong(ctx, sig, gidx, world, steps, warmup):
     """Timed dedup steps over one signature set (all ranks): (seconds for
     `steps`, mean ms of the rank's dedup_group kernels, bytes all ranks sent
@@ -251,12 +263,37 @@ def dedup_strong(ctx, sig, gidx, world, steps, warmup):
     return dt, kms / max(launches, 1), peer
 
 
+METHODS = {"crc": F.SIG_CRC_ONLY, "hash": F.SIG_HASH, "md5": F.SIG_MD5}
+KERNEL_OF = {F.SIG_CRC_ONLY: (_lib.KERNEL_CRC_SEG, "crc_seg_kernel<SAR,2>"),
+             F.SIG_HASH: (_lib.KERNEL_SIG_LANE, "sig_hash_kernel<SAR>"),
+             F.SIG_MD5: (_lib.KERNEL_SIG_LANE, "md5_stage_kernel<SAR>")}
+
+
+def chain_floor_ms(ctx, data, offs_t, sizes_t, sizes, method, kernel):
+    """The lane-serial floor of a lane-per-file batch: the same kernel over
+    a batch of the batch's largest file alone (one lane, one dependent
+    chain: MD5 / ELFHash have no intra-file parallel form), timed by the
+    library's HIP events on the launch stream."""
+    k = int(np.argmax(sizes))
+    o1, s1 = offs_t[k:k + 1].contiguous(), sizes_t[k:k + 1].contiguous()
+    ctx.sig_batch(data, o1, s1, method=method, check_bounds=False)
+    torch.cuda.synchronize()
+    ctx.set_timing(True)
+    ctx.read_timing(kernel)
+    for _ in range(2):
+        ctx.sig_batch(data, o1, s1, method=method, check_bounds=False)
+    ms, cnt = ctx.read_timing(kernel)
+    ctx.set_timing(False)
+    return ms / max(cnt, 1), int(sizes[k])
+
+
 def main():
     args = parse()
     world, rank, local = setup_dist(args)
     dev = torch.device("cuda", local)
     ctx = F.Context(local, unsigned_hash=args.unsigned_hash)
     variant = 1 if args.unsigned_hash else 0
+    threads = host_threads(args)
     res = {"metric": METRIC, "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
            "higher_is_better": True, "vs_baseline": None, "dtype": "u8",
            "data": "synthetic (seeded sizes, random bytes generated in HBM)"}
@@ -270,32 +307,38 @@ def main():
             sizes = np.concatenate([np.full(c, sz, np.int64) for sz, c in mix])
             sizes = sizes[np.random.default_rng(1 + 1000 * rank).permutation(sizes.size)]
             n = sizes.size
-            method, kernel, kname = F.SIG_HASH, _lib.KERNEL_SIG_LANE, "sig_hash_kernel<SAR>"
-            workload = ("config 1: test_upload DEBUG mix (gen_files sizes 5K..100M, 65,560 files), "
-                        "CRC32 + HASH_CODES4 signature + dedup per step")
+            method = F.SIG_HASH
+            workload = "config 1: test_upload DEBUG mix (gen_files sizes 5K..100M, 65,560 files)"
         elif args.config == "c2":
             n = args.files or 1_000_000
             sizes = C.small_files_sizes(n, seed=1 + 1000 * rank)
-            method, kernel, kname = F.SIG_HASH, _lib.KERNEL_SIG_LANE, "sig_hash_kernel<SAR>"
-            workload = ("config 2: 1M files/GPU of U[4,64] KiB, CRC32 + HASH_CODES4 signature "
-                        "+ bulk dedup per step")
+            method = F.SIG_HASH
+            workload = "config 2: 1M files/GPU of U[4,64] KiB"
         elif args.config == "c3":
             n = args.files or 100_000  # the full config (~262 GB resident in HBM)
             sizes = C.photo_sizes(n, seed=3 + 1000 * rank)
-            method, kernel, kname = F.SIG_MD5, _lib.KERNEL_SIG_LANE, "md5_stage_kernel<SAR>"
-            workload = f"config 3: {n} files/GPU of U[1,4] MiB, CRC32 + MD5 signature + dedup"
+            method = F.SIG_MD5
+            workload = f"config 3: {n} files/GPU of U[1,4] MiB"
         else:
             n = args.files or 8
             sizes = np.full(n, 1 << 30, dtype=np.int64)
-            method, kernel, kname = F.SIG_CRC_ONLY, _lib.KERNEL_CRC_SEG, "crc_seg_kernel<SAR,2>"
+            method = F.SIG_CRC_ONLY
             workload = f"config 4: {n} x 1 GiB files/GPU, segmented CRC32 (64 KiB) + GF(2) combine"
-        data, offs_t, sizes_t = C.device_batch(sizes, seed=2 + 1000 * rank, device=dev)
+        if args.method:
+            method = METHODS[args.method]
+        kernel, kname = KERNEL_OF[method]
+        workload += {F.SIG_CRC_ONLY: ", CRC32 only (check_file_duplicate=0)",
+                     F.SIG_HASH: ", CRC32 + HASH_CODES4 signature + bulk dedup per step",
+                     F.SIG_MD5: ", CRC32 + MD5 signature + bulk dedup per step"}[method]
+        if args.config == "c4":
+            workload = workload.split(", CRC32 only")[0]
+        data, offs_t, sizes_t = C.device_batch(sizes, seed=2 + 1000 * rank, device=dev, align=args.align)
         nbytes = int(sizes.sum())
         gidx = (torch.arange(n, device=dev, dtype=torch.int64) + rank * n)
         ctx.reserve(n, n)
 
         def step():
-            crc, sig, _ = ctx.sig_batch(data, offs_t, sizes_t, method=method)
+            crc, sig, _ = ctx.sig_batch(data, offs_t, sizes_t, method=method, check_bounds=False)
             if sig is not None:
                 dedup_step(ctx, sig, gidx, world)
 
@@ -314,36 +357,45 @@ def main():
         avg_ms = kms / max(launches, 1)
         per_launch = float(nbytes)  # each file byte read once; 28 B/file of outputs on top
         achieved = per_launch / (avg_ms * 1e-3) / 1e9
-        traffic, tsrc = load_traffic(args.config, kname)
-        res["roofline"] = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
-                           "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
-                           "traffic": traffic, "kernel": kname,
-                           "kernel_ms_avg": round(avg_ms, 4), "launches": launches,
-                           "algorithmic_bytes_per_launch": nbytes}
+        traffic, tsrc = load_traffic(args.config, kname) if (args.align == 16 and not args.method) \
+            else (None, None)
+        roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
+                "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
+                "traffic": traffic, "kernel": kname,
+                "kernel_ms_avg": round(avg_ms, 4), "launches": launches,
+                "algorithmic_bytes_per_launch": nbytes}
         if tsrc:
-            res["roofline"]["traffic_source"] = tsrc
-        if args.config == "c1":
-            res["roofline"]["note"] = ("bound by the lane-serial ELFHash of the ten 100 MB files (one wave "
-                                       "issues ~1 VALU instruction per 8.5 cycles), not by HBM; DESIGN.md §7")
-        valu = load_valu(args.config, avg_ms)
+            roof["traffic_source"] = tsrc
+        if args.config in ("c1", "c3") and method != F.SIG_CRC_ONLY:
+            # lane-per-file batches whose largest file's dependent chain (MD5
+            # / ELFHash) outlasts the HBM stream: the roof is that chain
+            fms, fbytes = chain_floor_ms(ctx, data, offs_t, sizes_t, sizes, method, kernel)
+            roof.update({"bound": "md5_chain" if method == F.SIG_MD5 else "elf_chain",
+                         "peak": round(per_launch / (fms * 1e-3) / 1e9, 1),
+                         "frac": round(fms / avg_ms, 4), "hbm_frac": round(achieved / HBM_PEAK_GBS, 4),
+                         "chain_floor_ms": round(fms, 3), "chain_floor_file_bytes": fbytes,
+                         "note": "peak = batch bytes over the time the same kernel takes for the "
+                                 "largest file alone (one lane's serial chain)"})
+        res["roofline"] = roof
+        valu = load_valu(args.config, avg_ms) if not args.method else None
         if valu:
             res["valu"] = valu
         if method != F.SIG_CRC_ONLY:
             # dedup-only throughput of the same signatures (files/s, all ranks)
-            _, sig, _ = ctx.sig_batch(data, offs_t, sizes_t, method=method)
+            _, sig, _ = ctx.sig_batch(data, offs_t, sizes_t, method=method, check_bounds=False)
             ddt = timed(lambda: dedup_step(ctx, sig, gidx, world), args.steps, 1, world)
             res["dedup_files_per_s"] = round(sum_over_ranks(float(n), world) * args.steps / ddt, 1)
         cfg = {"workload": workload, "files_per_gpu": n, "bytes_per_gpu": nbytes,
                "method": {0: "crc_only", 1: "hash", 2: "md5"}[method],
-               "crc_variant": "unsigned" if variant else "signed", "align": 16,
+               "crc_variant": "unsigned" if variant else "signed", "align": args.align,
                "parallelism": f"dp{world} (files sharded, dedup all-to-all)"}
         res["config"] = cfg
-        if args.config == "c2" and not args.files:
+        if args.config == "c2" and not args.files and not args.method and args.align == 16:
             # config 5's 100M-record dedup, strong-scaled over the ranks of
             # this run: the driver's 1/2/4/8-GPU runs of the default bench
             # give its scaling curve
             total = 100_000_000
-            sig5, gidx5 = c5_signatures(total, world, rank, dev)
+            sig5, gidx5 = C.c5_signatures(total, world, rank, dev)
             st5 = min(args.steps, 5)
             ddt, dms, peer = dedup_strong(ctx, sig5, gidx5, world, st5, 1)
             res["dedup_100m"] = {"files_per_s": round(total * st5 / ddt, 1),
@@ -355,17 +407,16 @@ def main():
                 res["dedup_100m"]["xgmi_gbs"] = round(peer / (ddt / st5) / 1e9, 1)
             del sig5, gidx5
         if rank == 0 and world == 1 and not args.no_cpu_baseline:
-            res["cpu_baseline"] = cpu_baseline(data, C.layout(sizes)[0], sizes, method, variant,
-                                               args.cpu_seconds, args.cpu_threads)
-            if args.config == "c1":  # one core as well as all of them
-                one = cpu_baseline(data, C.layout(sizes)[0], sizes, method, variant,
-                                   args.cpu_seconds / 2, 1)
-                res["cpu_baseline"]["single_thread"] = {k: one[k] for k in ("value", "unit", "sample")}
+            offs_np = C.layout(sizes, args.align)[0]
+            res["cpu_baseline"] = cpu_baseline(data, offs_np, sizes, method, variant,
+                                               args.cpu_seconds, threads)
+            one = cpu_baseline(data, offs_np, sizes, method, variant, args.cpu_seconds / 2, 1)
+            res["cpu_baseline"]["single_thread"] = {k: one[k] for k in ("value", "unit", "sample")}
         else:
             res["cpu_baseline"] = None
     else:  # c5: dedup only, strong scaling over a fixed 100M-signature set
         total = args.files or 100_000_000
-        sig, gidx = c5_signatures(total, world, rank, dev)
+        sig, gidx = C.c5_signatures(total, world, rank, dev)
         dt, avg_ms, peer = dedup_strong(ctx, sig, gidx, world, args.steps, args.warmup)
         res.update({"metric": METRIC, "value": round(total * args.steps / dt, 1),
                     "unit": "files/s", "ms_per_step": round(dt / args.steps * 1e3, 3),
@@ -376,23 +427,26 @@ def main():
         if world > 1:  # all ranks' bytes to peers per step, over the step time
             res["xgmi"] = {"bytes_per_step": round(peer), "gbs": round(peer / (dt / args.steps) / 1e9, 1),
                            "links_peak_gbs": 7 * 153.0 * world}
-        # algorithmic bytes per record: the 32-byte row {sig, gidx} read once,
-        # rep (8 B) + ref (4 B) written once
+        # algorithmic bytes per record: one GPU reads the 24-byte signature
+        # and writes rep (8 B) + ref (4 B); N GPUs group the 32-byte exchange
+        # rows {sig, gidx} instead
         m = float(total) / world
-        nb = m * 44.0
+        per_rec = 36.0 if world == 1 else 44.0
+        nb = m * per_rec
         res["roofline"] = {"bound": "hbm", "achieved": round(nb / (avg_ms * 1e-3) / 1e9, 1),
                            "peak": HBM_PEAK_GBS, "unit": "GB/s",
                            "frac": round(nb / (avg_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
                            "traffic": None,
                            "kernel": "dedup_group (dp_keys + scan + dp_scatter + dp_split + dp_group)",
-                           "kernel_ms_avg": round(avg_ms, 4), "algorithmic_bytes_per_launch": nb}
+                           "kernel_ms_avg": round(avg_ms, 4), "algorithmic_bytes_per_launch": nb,
+                           "algorithmic_bytes_per_record": per_rec}
         if world == 1:
             traffic, tsrc = load_traffic("c5", res["roofline"]["kernel"])
             if traffic:
                 res["roofline"]["traffic"] = traffic
                 res["roofline"]["traffic_source"] = tsrc
         if rank == 0 and world == 1 and not args.no_cpu_baseline:
-            res["cpu_baseline"] = cpu_dedup_baseline(sig, args.cpu_seconds)
+            res["cpu_baseline"] = cpu_dedup_baseline(sig, args.cpu_seconds, threads)
         else:
             res["cpu_baseline"] = None
     if rank == 0:

@@ -64,3 +64,26 @@ def dup_signatures(n: int, dup_frac: float = 0.1, seed: int = 5, device="cpu") -
     pick = np.concatenate([np.arange(nu), rng.integers(0, nu, size=n - nu)])
     rng.shuffle(pick)
     return torch.from_numpy(uniq[pick]).to(device)
+
+
+def c5_signatures(total: int, world: int = 1, rank: int = 0, dev="cuda"):
+    """Config 5's signature set: `total` records, 10% duplicates drawn
+    uniformly from the 90% unique ones (seed 5); every rank derives the same
+    global set and takes its contiguous share.  Returns (sig, gidx)."""
+    per = total // world
+    g = torch.Generator(device=dev)
+    g.manual_seed(5)
+    nu = total - total // 10
+    uniq_idx = torch.randint(0, nu, (total - nu,), generator=g, device=dev)
+    lo, hi = rank * per, (rank + 1) * per if rank < world - 1 else total
+    idx = torch.arange(lo, hi, device=dev, dtype=torch.int64)
+    src = torch.where(idx < nu, idx, uniq_idx[(idx - nu).clamp(min=0, max=max(total - nu - 1, 0))])
+    # signature bytes = fixed mix of the unique id (deterministic, 16 random-looking bytes)
+    sig = torch.zeros((hi - lo, 24), dtype=torch.uint8, device=dev)
+    x = (src * (0x9E3779B97F4A7C15 - (1 << 64))) ^ 0x5DEECE66D
+    for k in range(2):
+        x = x ^ (x >> 31)
+        x = x * 0x7FB5D329728EA185
+        sig[:, 8 + 8 * k: 16 + 8 * k] = x.contiguous().view(torch.uint8).view(-1, 8)
+    sig[:, 5:8] = (src % 251).to(torch.uint8).view(-1, 1)
+    return sig, idx

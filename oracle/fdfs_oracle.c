@@ -448,6 +448,140 @@ int orc_dedup(const uint8_t *sig, uint64_t n, uint64_t *rep_out,
     return 0;
 }
 
+/* The same answers on `nthreads` host threads (the multi-core CPU
+ * baseline of bench.py): records are partitioned by a hash of
+ * their 24 bytes (equal signatures share a partition, indices stay
+ * ascending inside it), each partition is sorted by (signature, index) and
+ * its runs are the classes.  Same output as orc_dedup. */
+typedef struct {
+    const uint8_t *sig;
+    uint64_t n, *idx, *start, *tcount;
+    uint32_t nb, nt;
+    uint64_t *rep;
+    uint32_t *ref;
+    uint32_t next;  /* partition work counter */
+    int phase;
+    int tid_next;
+} dd_job;
+
+static inline uint32_t dd_bucket(const uint8_t *r, uint32_t nb)
+{
+    uint64_t a, b, c;
+    memcpy(&a, r, 8);
+    memcpy(&b, r + 8, 8);
+    memcpy(&c, r + 16, 8);
+    uint64_t h = (a * 0x9E3779B97F4A7C15ull) ^ (b * 0xC2B2AE3D27D4EB4Full) ^ (c * 0x165667B19E3779F9ull);
+    h ^= h >> 29;
+    return (uint32_t)((h * 0xBF58476D1CE4E5B9ull) >> 32) % nb;
+}
+
+static int dd_cmp(const void *x, const void *y, void *arg)
+{
+    const uint8_t *sig = (const uint8_t *)arg;
+    const uint64_t ia = *(const uint64_t *)x, ib = *(const uint64_t *)y;
+    const int c = memcmp(sig + 24 * ia, sig + 24 * ib, 24);
+    return c ? c : (ia > ib) - (ia < ib);
+}
+
+static void *dd_worker(void *arg)
+{
+    dd_job *j = (dd_job *)arg;
+    const uint32_t t = (uint32_t)__atomic_fetch_add(&j->tid_next, 1, __ATOMIC_RELAXED);
+    const uint64_t lo = j->n * t / j->nt, hi = j->n * (t + 1) / j->nt;
+    uint64_t *cnt = j->tcount + (uint64_t)t * j->nb;
+    if (j->phase == 0) {  /* count this thread's slice per partition */
+        for (uint64_t i = lo; i < hi; i++)
+            cnt[dd_bucket(j->sig + 24 * i, j->nb)]++;
+    } else if (j->phase == 1) {  /* scatter (cnt holds this slice's write cursors) */
+        for (uint64_t i = lo; i < hi; i++)
+            j->idx[cnt[dd_bucket(j->sig + 24 * i, j->nb)]++] = i;
+    } else {  /* sort + group partitions */
+        for (;;) {
+            const uint32_t b = __atomic_fetch_add(&j->next, 1, __ATOMIC_RELAXED);
+            if (b >= j->nb)
+                break;
+            uint64_t *o = j->idx + j->start[b];
+            const uint64_t m = j->start[b + 1] - j->start[b];
+            qsort_r(o, (size_t)m, sizeof(uint64_t), dd_cmp, (void *)j->sig);
+            uint64_t s = 0;
+            while (s < m) {
+                uint64_t e = s + 1;
+                while (e < m && memcmp(j->sig + 24 * o[s], j->sig + 24 * o[e], 24) == 0)
+                    e++;
+                for (uint64_t k = s; k < e; k++) {
+                    j->rep[o[k]] = o[s];
+                    j->ref[o[k]] = (uint32_t)(e - s);
+                }
+                s = e;
+            }
+        }
+    }
+    return NULL;
+}
+
+static void dd_run(dd_job *j)
+{
+    pthread_t th[256];
+    j->tid_next = 0;
+    for (uint32_t t = 0; t < j->nt; t++)
+        pthread_create(&th[t], NULL, dd_worker, j);
+    for (uint32_t t = 0; t < j->nt; t++)
+        pthread_join(th[t], NULL);
+}
+
+int orc_dedup_mt(const uint8_t *sig, uint64_t n, uint64_t *rep_out, uint32_t *ref_out, int nthreads)
+{
+    if (nthreads < 1)
+        nthreads = 1;
+    if (nthreads > 256)
+        nthreads = 256;
+    dd_job j;
+    memset(&j, 0, sizeof(j));
+    j.sig = sig;
+    j.n = n;
+    j.nt = (uint32_t)nthreads;
+    /* partitions of ~2K records: each one's random signature reads stay in cache */
+    uint64_t nb = n / 2048;
+    if (nb < 64u * (uint64_t)nthreads)
+        nb = 64u * (uint64_t)nthreads;
+    if (nb > (1u << 20))
+        nb = 1u << 20;
+    j.nb = (uint32_t)nb;
+    j.rep = rep_out;
+    j.ref = ref_out;
+    j.idx = (uint64_t *)malloc(sizeof(uint64_t) * (n ? n : 1));
+    j.start = (uint64_t *)calloc(j.nb + 1, sizeof(uint64_t));
+    j.tcount = (uint64_t *)calloc((size_t)j.nb * j.nt, sizeof(uint64_t));
+    if (!j.idx || !j.start || !j.tcount) {
+        free(j.idx);
+        free(j.start);
+        free(j.tcount);
+        return 12;
+    }
+    j.phase = 0;
+    dd_run(&j);
+    /* partition starts, and each slice's cursor inside each partition
+     * (slices in order, so indices stay ascending in a partition) */
+    uint64_t run = 0;
+    for (uint32_t b = 0; b < j.nb; b++) {
+        j.start[b] = run;
+        for (uint32_t t = 0; t < j.nt; t++) {
+            const uint64_t c = j.tcount[(uint64_t)t * j.nb + b];
+            j.tcount[(uint64_t)t * j.nb + b] = run;
+            run += c;
+        }
+    }
+    j.start[j.nb] = run;
+    j.phase = 1;
+    dd_run(&j);
+    j.phase = 2;
+    dd_run(&j);
+    free(j.idx);
+    free(j.start);
+    free(j.tcount);
+    return 0;
+}
+
 /* ---- formats that consume the CRC, FastDHT routing -------------------- */
 
 int32_t orc_pjw_hash(const void *buf, size_t len, int variant)

@@ -137,6 +137,10 @@ void orc_fdht_route_key(const char *ns, int ns_len, const uint8_t *obj, int obj_
                         uint32_t group_count, uint32_t servers, int variant, int32_t *key_hash,
                         uint32_t *group, uint32_t *server);
 
+/* orc_dedup's answers on nthreads host threads (hash partition, sort per
+ * partition); the CPU dedup baseline. */
+int orc_dedup_mt(const uint8_t *sig, uint64_t n, uint64_t *rep_out, uint32_t *ref_out, int nthreads);
+
 #ifdef __cplusplus
 }
 #endif

@@ -65,6 +65,8 @@ def lib():
         L.orc_gen_files.argtypes = [u8p]
         L.orc_dedup.restype = ctypes.c_int
         L.orc_dedup.argtypes = [u8p, ctypes.c_uint64, u8p, u8p]
+        L.orc_dedup_mt.restype = ctypes.c_int
+        L.orc_dedup_mt.argtypes = [u8p, ctypes.c_uint64, u8p, u8p, ctypes.c_int]
         L.orc_md5_init.argtypes = [u8p]
         L.orc_md5_update.argtypes = [u8p, u8p, ctypes.c_size_t]
         L.orc_md5_final.argtypes = [u8p, u8p]
@@ -159,13 +161,17 @@ def gen_files() -> tuple[np.ndarray, np.ndarray, np.ndarray]:
     return buf, offs, sizes
 
 
-def dedup(sig: np.ndarray) -> tuple[np.ndarray, np.ndarray]:
-    """(rep uint64[n], ref uint32[n]) with the sequential FastDHT semantics."""
+def dedup(sig: np.ndarray, nthreads: int = 1, partitioned: bool = False) -> tuple[np.ndarray, np.ndarray]:
+    """(rep uint64[n], ref uint32[n]) with the sequential FastDHT semantics
+    (nthreads > 1 or partitioned: the hash-partitioned form, same answers)."""
     sig = np.ascontiguousarray(sig, dtype=np.uint8).reshape(-1, 24)
     n = sig.shape[0]
     rep = np.zeros(n, np.uint64)
     ref = np.zeros(n, np.uint32)
-    assert lib().orc_dedup(_ptr(sig), n, _ptr(rep), _ptr(ref)) == 0
+    if nthreads > 1 or partitioned:
+        assert lib().orc_dedup_mt(_ptr(sig), n, _ptr(rep), _ptr(ref), nthreads) == 0
+    else:
+        assert lib().orc_dedup(_ptr(sig), n, _ptr(rep), _ptr(ref)) == 0
     return rep, ref
 
 

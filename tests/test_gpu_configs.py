@@ -1,0 +1,93 @@
+"""GPU parity at BASELINE.json's full configuration sizes:
+
+* config 4: 1 GiB files and a file past 4 GiB (64-bit offsets, GF(2) powers
+  up to 2^32), CRC only, both shift variants, 16-byte and byte alignment;
+* config 3: the bench's 100K photo files (~262 GB resident), a sample from
+  every size decile against the oracle and hashlib;
+* config 5: the bench's own 100M-signature set on one GPU against the
+  oracle's sequential-semantics dedup.
+"""
+import hashlib
+
+import numpy as np
+import pytest
+import torch
+
+from fastdfs_amd import corpus as C
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def ctxs():
+    import fastdfs_amd as F
+    return {0: F.Context(0, unsigned_hash=False), 1: F.Context(0, unsigned_hash=True)}
+
+
+def test_config4_gib_files(oracle, ctxs):
+    """Two 1 GiB files and one of 4 GiB + 17 B (CRC only), at 16-byte and at
+    odd byte alignment (the same bytes shifted), both variants."""
+    torch.cuda.empty_cache()
+    sizes = np.array([1 << 30, 1 << 30, (4 << 30) + 17], np.int64)
+    offs16, total = C.layout(sizes, 16)
+    data = torch.empty(total + 64, dtype=torch.uint8, device="cuda")
+    C.fill_random(data, 44)
+    host = data.cpu().numpy()
+    want = {}
+    for v in (0, 1):
+        want[v], _ = oracle.dio_batch(host, offs16.astype(np.uint64), sizes.astype(np.uint64), 0, v,
+                                      nthreads=3)
+    del host
+    shifted = torch.empty_like(data)
+    shifted[7:] = data[:-7]  # every file at offset + 7: odd alignment, same bytes
+    for v in (0, 1):
+        for buf, offs in ((data, offs16), (shifted, offs16 + 7)):
+            crc, _, _ = ctxs[v].sig_batch(buf, torch.from_numpy(offs).cuda(), torch.from_numpy(sizes).cuda(),
+                                          method=0)
+            torch.cuda.synchronize()
+            assert np.array_equal(crc.cpu().numpy().view(np.uint32), want[v]), (v, offs[0] & 15)
+    del data, shifted
+    torch.cuda.empty_cache()
+
+
+def test_config3_full_batch(oracle, ctxs):
+    """Config 3 at its bench size: 100K files of U[1, 4] MiB (~262 GB in
+    HBM), CRC + MD5 signature; 15 files from every size decile match the
+    oracle bit for bit and hashlib's MD5."""
+    torch.cuda.empty_cache()
+    n = 100_000
+    sizes = C.photo_sizes(n, seed=3)
+    data, offs_t, sizes_t = C.device_batch(sizes, seed=2, device="cuda:0")
+    crc, sig, _ = ctxs[0].sig_batch(data, offs_t, sizes_t, method=2, check_bounds=False)
+    torch.cuda.synchronize()
+    crc_np, sig_np = crc.cpu().numpy().view(np.uint32), sig.cpu().numpy()
+    offs = offs_t.cpu().numpy()
+    order = np.argsort(sizes, kind="stable")
+    rng = np.random.default_rng(33)
+    picks = np.concatenate([rng.choice(d, 15, replace=False) for d in np.array_split(order, 10)]
+                           + [order[:1], order[-1:]])
+    for i in picks:
+        d = data[int(offs[i]): int(offs[i] + sizes[i])].cpu().numpy()
+        c, s, _ = oracle.dio_file(d, 2, 0)
+        assert c == crc_np[i] and s == sig_np[i].tobytes(), i
+        assert sig_np[i, 8:].tobytes() == hashlib.md5(d.tobytes()).digest(), i
+        assert int.from_bytes(sig_np[i, :8].tobytes(), "big") == sizes[i]
+    del data, crc, sig
+    torch.cuda.empty_cache()
+
+
+def test_config5_bench_set(oracle, ctxs):
+    """The bench's config-5 set (100M signatures, 10 % duplicates) on one
+    GPU: every record's class source and class size equal the oracle's."""
+    torch.cuda.empty_cache()
+    total = 100_000_000
+    sig, gidx = C.c5_signatures(total, 1, 0, "cuda")
+    rep, ref = ctxs[0].dedup(sig)
+    torch.cuda.synchronize()
+    sig_np = sig.cpu().numpy()
+    del sig, gidx
+    orep, oref = oracle.dedup(sig_np, nthreads=16)
+    assert np.array_equal(rep.cpu().numpy(), orep.astype(np.int64))
+    assert np.array_equal(ref.cpu().numpy(), oref.astype(np.int32))
+    assert int(oref.max()) > 1 and (oref > 1).sum() > total // 20
+    torch.cuda.empty_cache()
