@@ -116,13 +116,13 @@ def test_shard_lpt_huge_file_alone():
 
 @pytest.mark.parametrize("world", [2, 3, 8])
 def test_c5_signature_shares(world):
-    """bench.py's config-5 set: the ranks' contiguous shares concatenate to
-    the one-rank set (what the strong-scaled dedup line relies on), with
-    10% of the records duplicating earlier unique ones."""
-    import bench
+    """bench.py's config-5 set (corpus.c5_signatures): the ranks' contiguous
+    shares concatenate to the one-rank set (what the strong-scaled dedup line
+    relies on), with 10% of the records duplicating earlier unique ones."""
+    from fastdfs_amd import corpus as C
     total = 10_000
-    one, gidx1 = bench.c5_signatures(total, 1, 0, torch.device("cpu"))
-    parts = [bench.c5_signatures(total, world, r, torch.device("cpu")) for r in range(world)]
+    one, gidx1 = C.c5_signatures(total, 1, 0, torch.device("cpu"))
+    parts = [C.c5_signatures(total, world, r, torch.device("cpu")) for r in range(world)]
     assert torch.equal(torch.cat([p[0] for p in parts]), one)
     assert torch.equal(torch.cat([p[1] for p in parts]), gidx1)
     assert torch.equal(gidx1, torch.arange(total))
