@@ -119,8 +119,28 @@ def dedup_step(ctx, sig, gidx, world, stats=None):
     return ctx.dedup(sig)
 
 
+def cgroup_cpus() -> float | None:
+    """CPUs granted by the cgroup v2 quota (cpu.max), or None if unlimited."""
+    try:
+        quota, period = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if quota != "max":
+            return int(quota) / int(period)
+    except (OSError, ValueError):
+        pass
+    return None
+
+
 def host_threads(args) -> int:
-    return args.cpu_threads or len(os.sched_getaffinity(0))
+    """Every CPU this process may run on: the affinity set, capped by the
+    cgroup quota (a GPU box's share of a larger host shows the whole host in
+    its affinity mask)."""
+    if args.cpu_threads:
+        return args.cpu_threads
+    n = len(os.sched_getaffinity(0))
+    q = cgroup_cpus()
+    if q is None and os.environ.get("OMP_NUM_THREADS", "").isdigit():
+        q = int(os.environ["OMP_NUM_THREADS"])  # the share a pool box advertises
+    return max(1, min(n, int(q))) if q else n
 
 
 def cpu_baseline(data, offs_np, sizes_np, method, variant, seconds, threads):
@@ -152,6 +172,7 @@ def cpu_baseline(data, offs_np, sizes_np, method, variant, seconds, threads):
         dt, nb = run(k2)
         k = k2
     return {"value": round(nb / dt / 1e9, 4), "unit": "GB/s", "cores": threads, "kind": "port",
+            "host_cpus": len(os.sched_getaffinity(0)), "cgroup_cpus": cgroup_cpus(),
             "sample": f"first {k} files of the rank-0 batch ({nb / 1e9:.2f} GB), "
                       f"oracle/fdfs_oracle.c orc_dio_batch, 256 KiB chunks, {threads} threads, "
                       f"{dt:.1f} s", "cpu_model": cpu_model()}
