@@ -60,6 +60,9 @@ def parse():
                    help="CPU baseline threads (0 = every core this process may run on)")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--unsigned-hash", action="store_true")
+    p.add_argument("--exchange", default="rccl", choices=["rccl", "torch"],
+                   help="N>1 dedup exchange: libfdfs_gpu's fdfs_gpu_dedup_global over its own RCCL "
+                        "communicator, or the same steps over torch.distributed")
     return p.parse_args()
 
 
@@ -111,9 +114,12 @@ def timed(fn, steps, warmup, world):
     return max_over_ranks(time.perf_counter() - t0, world)
 
 
+COMM = None  # fastdfs_amd.api.Comm of the run (N > 1, --exchange rccl)
+
+
 def dedup_step(ctx, sig, gidx, world, stats=None):
     if world > 1:
-        return dedup_global(ctx, sig, gidx, stats=stats)
+        return dedup_global(ctx, sig, gidx, stats=stats, comm=COMM)
     # one GPU holds the whole ingest in order: the ingest index is the
     # position (gidx NULL in fdfs_gpu_dedup, the same answers as arange)
     return ctx.dedup(sig)
@@ -269,6 +275,20 @@ def load_valu(config: str, avg_ms: float):
     return None
 
 
+def peer_bytes(ctx, sig, gidx, world):
+    """Bytes this rank sends to other ranks in one global dedup: its rows
+    for other owners (32 B each) and the answers it returns for theirs
+    (16 B each), from one bucket pass and a count exchange (untimed)."""
+    if world == 1:
+        return 0.0
+    _, counts, _ = ctx.dedup_bucket(sig, gidx, world)
+    recv = torch.empty_like(counts)
+    dist.all_to_all_single(recv, counts)
+    me = dist.get_rank()
+    send, recv = counts.cpu().tolist(), recv.cpu().tolist()
+    return float(32 * (sum(send) - send[me]) + 16 * (sum(recv) - recv[me]))
+
+
 def dedup_strong(ctx, sig, gidx, world, steps, warmup):
     """Timed dedup steps over one signature set (all ranks): (seconds for
     `steps`, mean ms of the rank's dedup_group kernels, bytes all ranks sent
@@ -276,11 +296,10 @@ def dedup_strong(ctx, sig, gidx, world, steps, warmup):
     ctx.reserve(0, 2 * sig.shape[0])
     ctx.set_timing(True)
     ctx.read_timing(_lib.KERNEL_DEDUP)
-    stats = {}
-    dt = timed(lambda: dedup_step(ctx, sig, gidx, world, stats), steps, warmup, world)
+    dt = timed(lambda: dedup_step(ctx, sig, gidx, world), steps, warmup, world)
     kms, launches = ctx.read_timing(_lib.KERNEL_DEDUP)
     ctx.set_timing(False)
-    peer = sum_over_ranks(float(stats.get("peer_bytes", 0)), world) / max(steps + warmup, 1)
+    peer = sum_over_ranks(peer_bytes(ctx, sig, gidx, world), world)
     return dt, kms / max(launches, 1), peer
 
 
@@ -313,6 +332,10 @@ def main():
     world, rank, local = setup_dist(args)
     dev = torch.device("cuda", local)
     ctx = F.Context(local, unsigned_hash=args.unsigned_hash)
+    global COMM
+    if world > 1 and args.exchange == "rccl":
+        from fastdfs_amd.api import Comm
+        COMM = Comm(ctx)
     variant = 1 if args.unsigned_hash else 0
     threads = host_threads(args)
     res = {"metric": METRIC, "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
@@ -470,8 +493,14 @@ def main():
             res["cpu_baseline"] = cpu_dedup_baseline(sig, args.cpu_seconds, threads)
         else:
             res["cpu_baseline"] = None
+    if world > 1:
+        res.setdefault("config", {})["dedup_exchange"] = (
+            "fdfs_gpu_dedup_global (libfdfs_gpu, RCCL send/recv)" if COMM is not None
+            else "torch.distributed all_to_all_single")
     if rank == 0:
         print(json.dumps(res), flush=True)
+    if COMM is not None:
+        COMM.close()
     ctx.close()
     if world > 1:
         dist.destroy_process_group()

@@ -50,7 +50,12 @@ EXPORTS = (
     "fdfs_gpu_update_batch",
     "fdfs_gpu_final_batch",
     "fdfs_gpu_crc_combine",
+    "fdfs_gpu_dedup_global",
+    "fdfs_gpu_comm_unique_id",
+    "fdfs_gpu_comm_init",
+    "fdfs_gpu_comm_destroy",
 )
+COMM_ID_BYTES = 128
 FILE_STATE_SIZE = 128  # sizeof(fdfs_gpu_file_state)
 KERNEL_SIG_LANE = 0
 KERNEL_CRC_SEG = 1
@@ -145,5 +150,13 @@ def load() -> ctypes.CDLL:
     L.fdfs_gpu_final_batch.argtypes = [vp, vp, vp, u32, i32, vp, vp, vp, vp]
     L.fdfs_gpu_crc_combine.restype = i32
     L.fdfs_gpu_crc_combine.argtypes = [vp, vp, vp, vp, u32, vp, vp]
+    L.fdfs_gpu_dedup_global.restype = i32
+    L.fdfs_gpu_dedup_global.argtypes = [vp, vp, vp, vp, u64, vp, vp, vp]
+    L.fdfs_gpu_comm_unique_id.restype = i32
+    L.fdfs_gpu_comm_unique_id.argtypes = [ctypes.c_char_p]
+    L.fdfs_gpu_comm_init.restype = i32
+    L.fdfs_gpu_comm_init.argtypes = [vp, ctypes.c_char_p, i32, i32, ctypes.POINTER(vp)]
+    L.fdfs_gpu_comm_destroy.restype = i32
+    L.fdfs_gpu_comm_destroy.argtypes = [vp]
     _lib = L
     return L

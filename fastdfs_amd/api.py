@@ -281,6 +281,18 @@ class Context:
                                         ref.data_ptr(), _stream_handle(stream)), "fdfs_gpu_dedup")
         return rep, ref
 
+    def dedup_global(self, comm: "Comm", sig: torch.Tensor, gidx: torch.Tensor | None, stream=None):
+        """fdfs_gpu_dedup_global: this rank's share of a multi-GPU ingest
+        grouped across every rank of `comm` over RCCL; (rep int64[n], ref
+        int32[n]) for this rank's records (collective: all ranks call)."""
+        n = _check_sig(sig, gidx)
+        rep = torch.empty(n, dtype=torch.int64, device=sig.device)
+        ref = torch.empty(n, dtype=torch.int32, device=sig.device)
+        self._rc(self._L.fdfs_gpu_dedup_global(self._h, comm.handle, sig.data_ptr(), _ptr(gidx), n,
+                                               rep.data_ptr(), ref.data_ptr(), _stream_handle(stream)),
+                 "fdfs_gpu_dedup_global")
+        return rep, ref
+
     def dedup_bucket(self, sig: torch.Tensor, gidx: torch.Tensor | None, nranks: int, stream=None):
         """Pack {sig, gidx} rows by owner rank: (rows uint8[n,32], counts int64[nranks], row_of int64[n])."""
         n = _check_sig(sig, gidx)
@@ -432,3 +444,36 @@ class Context:
                                         crc.data_ptr(), bad.data_ptr(), nbad.data_ptr(),
                                         _stream_handle(stream)), "fdfs_gpu_scrub")
         return crc, bad, nbad
+
+
+class Comm:
+    """An RCCL communicator for fdfs_gpu_dedup_global, set up through
+    torch.distributed (which carries rank 0's 128-byte id to the others).
+    Collective: every rank of `group` constructs it together."""
+
+    def __init__(self, ctx: Context, group=None):
+        import torch.distributed as dist
+        L = ctx._L
+        rank, world = dist.get_rank(group), dist.get_world_size(group)
+        buf = ctypes.create_string_buffer(_lib.COMM_ID_BYTES)
+        if rank == 0 and L.fdfs_gpu_comm_unique_id(buf):
+            raise FdfsGpuError(errno.EIO, "fdfs_gpu_comm_unique_id")
+        backend = dist.get_backend(group)
+        dev = torch.device("cuda", ctx.device) if backend == "nccl" else torch.device("cpu")
+        t = torch.frombuffer(bytearray(buf.raw), dtype=torch.uint8).to(dev)
+        dist.broadcast(t, src=dist.get_global_rank(group, 0) if group is not None else 0, group=group)
+        uid = bytes(t.cpu().numpy().tobytes())
+        h = ctypes.c_void_p()
+        ctx._rc(L.fdfs_gpu_comm_init(ctx._h, uid, world, rank, ctypes.byref(h)), "fdfs_gpu_comm_init")
+        self._L, self.handle, self.rank, self.world = L, h, rank, world
+
+    def close(self):
+        if getattr(self, "handle", None):
+            self._L.fdfs_gpu_comm_destroy(self.handle)
+            self.handle = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass

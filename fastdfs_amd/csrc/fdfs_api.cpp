@@ -2,6 +2,7 @@
 // checking around the kernels.  No CPU compute path exists: every result
 // comes from a gfx950 kernel, and a missing/failed device is an error.
 #include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
 
 #include <algorithm>
 #include <cerrno>
@@ -43,6 +44,11 @@ struct fdfs_gpu_ctx {
     hipEvent_t ws_ev = nullptr;
     hipStream_t ws_st = nullptr;
     bool ws_rec = false;
+    // fdfs_gpu_dedup_global: exchange buffers (ordered like ws) and the
+    // pinned per-peer row counts {send[64], recv[64]}
+    void *xa = nullptr, *xb = nullptr;
+    size_t xa_bytes = 0, xb_bytes = 0;
+    uint64_t *hcounts = nullptr;
 };
 
 namespace {
@@ -128,6 +134,36 @@ struct WsScope {
     WsScope(fdfs_gpu_ctx *c, hipStream_t s) : ctx(c), st(s) { ws_enter(c, s); }
     ~WsScope() { ws_leave(ctx, st); }
 };
+
+// Grow a context-owned device buffer (like ensure_ws: the last call that
+// used the context's buffers must be done before the old one is freed).
+int ensure_buf(fdfs_gpu_ctx *ctx, void **buf, size_t *have, size_t bytes, hipStream_t st)
+{
+    if (bytes <= *have)
+        return 0;
+    if (capturing(st)) {
+        std::snprintf(ctx->err, sizeof(ctx->err), "exchange buffer growth during stream capture");
+        return ENOMEM;
+    }
+    if (*buf) {
+        hipError_t e = ctx->ws_rec ? hipEventSynchronize(ctx->ws_ev) : hipSuccess;
+        if (e == hipSuccess)
+            e = hipStreamSynchronize(st);
+        if (e != hipSuccess)
+            return fail(ctx, e, "buffer growth sync");
+        (void)hipFree(*buf);
+        *buf = nullptr;
+        *have = 0;
+    }
+    const size_t sz = bytes + bytes / 4;
+    hipError_t e = hipMalloc(buf, sz);
+    if (e != hipSuccess) {
+        std::snprintf(ctx->err, sizeof(ctx->err), "hipMalloc(%zu): %s", sz, hipGetErrorString(e));
+        return ENOMEM;
+    }
+    *have = sz;
+    return 0;
+}
 
 int ensure_ws(fdfs_gpu_ctx *ctx, size_t bytes, hipStream_t st)
 {
@@ -255,6 +291,12 @@ int fdfs_gpu_close(fdfs_gpu_ctx *ctx)
     (void)hipDeviceSynchronize();
     if (ctx->ws)
         (void)hipFree(ctx->ws);
+    if (ctx->xa)
+        (void)hipFree(ctx->xa);
+    if (ctx->xb)
+        (void)hipFree(ctx->xb);
+    if (ctx->hcounts)
+        (void)hipHostFree(ctx->hcounts);
     for (auto &r : ctx->recs) {
         (void)hipEventDestroy(r.a);
         (void)hipEventDestroy(r.b);
@@ -741,6 +783,168 @@ int fdfs_gpu_dedup_bucket(fdfs_gpu_ctx *ctx, const uint8_t *sig, const uint64_t 
     hipError_t e = fdfs::launch_dedup_bucket(sig, gidx, n, nranks, records_out, counts_out, cursor,
                                              row_of_out, st, a, b);
     return e == hipSuccess ? 0 : fail(ctx, e, "dedup_bucket launch");
+}
+
+// ---- multi-GPU dedup over RCCL ---------------------------------------------
+
+static int nccl_fail(fdfs_gpu_ctx *ctx, ncclResult_t r, const char *where)
+{
+    if (ctx)
+        std::snprintf(ctx->err, sizeof(ctx->err), "%s: %s", where, ncclGetErrorString(r));
+    return EIO;
+}
+
+int fdfs_gpu_comm_unique_id(uint8_t *id_out)
+{
+    if (!id_out)
+        return EINVAL;
+    ncclUniqueId id;
+    if (ncclGetUniqueId(&id) != ncclSuccess)
+        return EIO;
+    std::memcpy(id_out, id.internal, NCCL_UNIQUE_ID_BYTES);
+    return 0;
+}
+
+int fdfs_gpu_comm_init(fdfs_gpu_ctx *ctx, const uint8_t *id, int nranks, int rank, void **comm_out)
+{
+    if (!ctx || !id || !comm_out || nranks < 1 || nranks > 64 || rank < 0 || rank >= nranks)
+        return EINVAL;
+    *comm_out = nullptr;
+    std::lock_guard<std::recursive_mutex> lk(ctx->mu);
+    DeviceGuard g(ctx->device);
+    if (!g.ok)
+        return ENODEV;
+    ncclUniqueId uid;
+    std::memcpy(uid.internal, id, NCCL_UNIQUE_ID_BYTES);
+    ncclComm_t c = nullptr;
+    const ncclResult_t r = ncclCommInitRank(&c, nranks, uid, rank);
+    if (r != ncclSuccess)
+        return nccl_fail(ctx, r, "ncclCommInitRank");
+    *comm_out = c;
+    return 0;
+}
+
+int fdfs_gpu_comm_destroy(void *comm)
+{
+    if (!comm)
+        return EINVAL;
+    return ncclCommDestroy(static_cast<ncclComm_t>(comm)) == ncclSuccess ? 0 : EIO;
+}
+
+// One exchange: rank p receives from every rank the rows addressed to it.
+// send/recv: per-peer element counts (elements of `elem` bytes) whose
+// prefix sums place the peers' segments in sbuf / rbuf.
+static int exchange(fdfs_gpu_ctx *ctx, ncclComm_t c, int nranks, int me, const char *sbuf, const uint64_t *send,
+                    char *rbuf, const uint64_t *recv, size_t elem, hipStream_t st)
+{
+    uint64_t so = 0, ro = 0;
+    uint64_t soff[64], roff[64];
+    for (int p = 0; p < nranks; p++) {
+        soff[p] = so;
+        roff[p] = ro;
+        so += send[p];
+        ro += recv[p];
+    }
+    if (send[me] && hipMemcpyAsync(rbuf + roff[me] * elem, sbuf + soff[me] * elem, send[me] * elem,
+                                   hipMemcpyDeviceToDevice, st) != hipSuccess)
+        return fail(ctx, hipGetLastError(), "exchange self copy");
+    if (nranks == 1)
+        return 0;
+    ncclResult_t r = ncclGroupStart();
+    for (int p = 0; p < nranks && r == ncclSuccess; p++) {
+        if (p == me)
+            continue;
+        if (send[p])
+            r = ncclSend(sbuf + soff[p] * elem, send[p] * elem, ncclUint8, p, c, st);
+        if (r == ncclSuccess && recv[p])
+            r = ncclRecv(rbuf + roff[p] * elem, recv[p] * elem, ncclUint8, p, c, st);
+    }
+    const ncclResult_t r2 = ncclGroupEnd();
+    if (r != ncclSuccess || r2 != ncclSuccess)
+        return nccl_fail(ctx, r != ncclSuccess ? r : r2, "exchange");
+    return 0;
+}
+
+int fdfs_gpu_dedup_global(fdfs_gpu_ctx *ctx, void *comm, const uint8_t *sig, const uint64_t *gidx,
+                          uint64_t n, uint64_t *rep_out, uint32_t *ref_out, void *stream)
+{
+    if (!ctx || !comm || n >= 0xFFFFFFFFull)
+        return EINVAL;
+    if (n && (!sig || !rep_out || !ref_out))
+        return EINVAL;
+    if ((reinterpret_cast<uintptr_t>(sig) | reinterpret_cast<uintptr_t>(gidx) |
+         reinterpret_cast<uintptr_t>(rep_out)) & 7)
+        return EINVAL;
+    ncclComm_t c = static_cast<ncclComm_t>(comm);
+    int nranks = 0, me = 0;
+    if (ncclCommCount(c, &nranks) != ncclSuccess || ncclCommUserRank(c, &me) != ncclSuccess ||
+        nranks < 1 || nranks > 64)
+        return EINVAL;
+    std::lock_guard<std::recursive_mutex> lk(ctx->mu);
+    DeviceGuard g(ctx->device);
+    if (!g.ok)
+        return ENODEV;
+    hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+    if (!ctx->hcounts && hipHostMalloc(reinterpret_cast<void **>(&ctx->hcounts), 2 * 64 * 8, 0) != hipSuccess)
+        return ENOMEM;
+    // this rank's side: rows by owner, their positions, the answers coming back
+    const size_t a_bytes = align_up(32 * n) + align_up(8 * n) + align_up(16 * n) + 3 * align_up(8 * 64);
+    int rc = ensure_buf(ctx, &ctx->xa, &ctx->xa_bytes, a_bytes, st);
+    if (rc)
+        return rc;
+    WsScope wsc(ctx, st);
+    Carve ca{static_cast<char *>(ctx->xa)};
+    uint8_t *rows = ca.take<uint8_t>(32 * n);
+    uint64_t *row_of = ca.take<uint64_t>(n);
+    uint64_t *back = ca.take<uint64_t>(2 * n);
+    uint64_t *counts = ca.take<uint64_t>(64);  // send counts; recv counts follow
+    uint64_t *rcounts = ca.take<uint64_t>(64);
+    uint64_t *cursor = ca.take<uint64_t>(64);
+    hipEvent_t a, b;
+    timing_pair(ctx, FDFS_KERNEL_BUCKET, a, b);
+    hipError_t e = fdfs::launch_dedup_bucket(sig, gidx, n, (uint32_t)nranks, rows, counts, cursor, row_of, st, a, b);
+    if (e != hipSuccess)
+        return fail(ctx, e, "dedup_global bucket");
+    // 1. row counts to their owners (one u64 per peer), then to the host:
+    //    the only host synchronisation (the row exchange needs the sizes)
+    ncclResult_t r = ncclAllToAll(counts, rcounts, 1, ncclUint64, c, st);
+    if (r != ncclSuccess)
+        return nccl_fail(ctx, r, "ncclAllToAll counts");
+    if ((e = hipMemcpyAsync(ctx->hcounts, counts, 2 * 64 * 8, hipMemcpyDeviceToHost, st)) != hipSuccess ||
+        (e = hipStreamSynchronize(st)) != hipSuccess)
+        return fail(ctx, e, "dedup_global counts");
+    uint64_t send[64], recv[64], m = 0;
+    for (int p = 0; p < nranks; p++) {
+        send[p] = ctx->hcounts[p];
+        recv[p] = ctx->hcounts[64 + p];
+        m += recv[p];
+    }
+    if (m >= 0xFFFFFFFFull)
+        return EINVAL;
+    // the owner's side: received rows, their answers (packed for the way back)
+    const size_t b_bytes = align_up(32 * m) + align_up(8 * m) + align_up(4 * m) + align_up(16 * m);
+    if ((rc = ensure_buf(ctx, &ctx->xb, &ctx->xb_bytes, b_bytes, st)) ||
+        (rc = ensure_ws(ctx, dedup_ws_bytes(m), st)))
+        return rc;
+    Carve cb{static_cast<char *>(ctx->xb)};
+    uint8_t *rows_in = cb.take<uint8_t>(32 * m);
+    uint64_t *rep_in = cb.take<uint64_t>(m);
+    uint32_t *ref_in = cb.take<uint32_t>(m);
+    uint64_t *ans = cb.take<uint64_t>(2 * m);
+    // 2. rows to their owners over xGMI, 3. group, 4. answers back
+    if ((rc = exchange(ctx, c, nranks, me, reinterpret_cast<const char *>(rows), send,
+                       reinterpret_cast<char *>(rows_in), recv, 32, st)))
+        return rc;
+    timing_pair(ctx, FDFS_KERNEL_DEDUP, a, b);
+    if ((e = fdfs::launch_dedup_group(rows_in, 32, reinterpret_cast<const uint64_t *>(rows_in + 24), 4, m, ctx->ws,
+                                      rep_in, ref_in, st, a, b)) != hipSuccess ||
+        (e = fdfs::launch_answer_pack(rep_in, ref_in, m, ans, st)) != hipSuccess)
+        return fail(ctx, e, "dedup_global group");
+    if ((rc = exchange(ctx, c, nranks, me, reinterpret_cast<const char *>(ans), recv,
+                       reinterpret_cast<char *>(back), send, 16, st)))
+        return rc;
+    e = fdfs::launch_answer_gather(back, row_of, n, rep_out, ref_out, st);
+    return e == hipSuccess ? 0 : fail(ctx, e, "dedup_global gather");
 }
 
 // ---- formats that consume the CRC, FastDHT routing, scrub ----

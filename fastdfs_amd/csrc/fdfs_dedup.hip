@@ -649,6 +649,44 @@ __global__ void bucket_scatter_kernel(const uint8_t *__restrict__ sig, const uin
     }
 }
 
+// Multi-GPU dedup (fdfs_gpu_dedup_global): the owner's per-row answers
+// packed as {rep, ref} pairs for the return exchange, and the exchanged
+// answers mapped back to the rank's records through row_of.
+__global__ void answer_pack_kernel(const uint64_t *__restrict__ rep, const uint32_t *__restrict__ ref,
+                                   uint64_t m, uint64_t *__restrict__ ans)
+{
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < m;
+         i += (uint64_t)gridDim.x * blockDim.x)
+        reinterpret_cast<ulonglong2 *>(ans)[i] = make_ulonglong2(rep[i], ref[i]);
+}
+
+__global__ void answer_gather_kernel(const uint64_t *__restrict__ back, const uint64_t *__restrict__ row_of,
+                                     uint64_t n, uint64_t *__restrict__ rep_out, uint32_t *__restrict__ ref_out)
+{
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+         i += (uint64_t)gridDim.x * blockDim.x) {
+        const ulonglong2 a = reinterpret_cast<const ulonglong2 *>(back)[row_of[i]];
+        rep_out[i] = a.x;
+        ref_out[i] = (uint32_t)a.y;
+    }
+}
+
+hipError_t launch_answer_pack(const uint64_t *rep, const uint32_t *ref, uint64_t m, uint64_t *ans,
+                              hipStream_t st)
+{
+    if (m)
+        answer_pack_kernel<<<grid_for(m, 256), 256, 0, st>>>(rep, ref, m, ans);
+    return hipGetLastError();
+}
+
+hipError_t launch_answer_gather(const uint64_t *back, const uint64_t *row_of, uint64_t n, uint64_t *rep_out,
+                                uint32_t *ref_out, hipStream_t st)
+{
+    if (n)
+        answer_gather_kernel<<<grid_for(n, 256), 256, 0, st>>>(back, row_of, n, rep_out, ref_out);
+    return hipGetLastError();
+}
+
 hipError_t launch_dedup_bucket(const uint8_t *sig, const uint64_t *gidx, uint64_t n,
                                uint32_t nranks, uint8_t *records_out, uint64_t *counts_out,
                                uint64_t *cursor, uint64_t *row_of_out, hipStream_t st,

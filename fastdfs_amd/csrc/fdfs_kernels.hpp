@@ -106,4 +106,9 @@ hipError_t launch_dedup_bucket(const uint8_t *sig, const uint64_t *gidx, uint64_
                                uint64_t *cursor, uint64_t *row_of_out, hipStream_t st,
                                hipEvent_t ev0, hipEvent_t ev1);
 
+hipError_t launch_answer_pack(const uint64_t *rep, const uint32_t *ref, uint64_t m, uint64_t *ans,
+                              hipStream_t st);
+hipError_t launch_answer_gather(const uint64_t *back, const uint64_t *row_of, uint64_t n, uint64_t *rep_out,
+                                uint32_t *ref_out, hipStream_t st);
+
 }  // namespace fdfs

@@ -33,8 +33,14 @@ def shard_lpt(sizes: np.ndarray, nranks: int) -> list[np.ndarray]:
     return [np.nonzero(owner == r)[0] for r in range(nranks)]
 
 
-def dedup_global(kernels, sig: torch.Tensor, gidx: torch.Tensor, group=None, stats=None):
+def dedup_global(kernels, sig: torch.Tensor, gidx: torch.Tensor, group=None, stats=None, comm=None):
     """Dedup across all ranks of `group`.
+
+    comm: a fastdfs_amd.api.Comm -> the whole exchange runs inside
+    libfdfs_gpu (fdfs_gpu_dedup_global over RCCL, the C daemon's path); this
+    function is then a thin caller.  Without it the same steps run here over
+    torch.distributed collectives (the gloo tests use that form with a CPU
+    double of the kernels).
 
     kernels: a fastdfs_amd.Context (the HIP kernels); tests substitute a
     CPU double to exercise the exchange over gloo.
@@ -42,8 +48,10 @@ def dedup_global(kernels, sig: torch.Tensor, gidx: torch.Tensor, group=None, sta
     ingest indices.  Returns (rep int64[n], ref int32[n]) for this rank's
     files, identical to single-process dedup over the concatenated input.
     stats: optional dict; "peer_bytes" accumulates the bytes this rank sent
-    to other ranks (32-byte rows out, 16-byte answers back).
+    to other ranks (32-byte rows out, 16-byte answers back; torch form only).
     """
+    if comm is not None:
+        return kernels.dedup_global(comm, sig, gidx)
     world = dist.get_world_size(group)
     dev = sig.device
     rows, counts, row_of = kernels.dedup_bucket(sig, gidx, world)

@@ -28,8 +28,13 @@
  *   my_md5_init/update/final + STORAGE_GEN_FILE_SIGNATURE
  *       storage/storage_service.c:7160, storage/storage_dio.c:480,512  -> fdfs_gpu_sig_batch(.., FDFS_SIG_MD5, ..)
  *   fdht_get_ex1 "fid" / fdht_set_ex / fdht_inc_ex "ref" dedup decision
- *       storage/storage_service.c:2652,2714,2734,2984 -> fdfs_gpu_dedup (1 GPU)
- *       or fdfs_gpu_dedup_bucket + exchange + fdfs_gpu_dedup_group (N GPUs)
+ *       storage/storage_service.c:2652,2714,2734,2984 -> fdfs_gpu_dedup (1 GPU),
+ *       fdfs_gpu_dedup_global (N GPUs over RCCL), or fdfs_gpu_dedup_bucket +
+ *       the caller's exchange + fdfs_gpu_dedup_group
+ *   the per-chunk loop itself (StorageFileContext state across chunks)
+ *       storage/storage_service.c:7147-7161, storage/storage_dio.c:465-515,
+ *       client/fdfs_crc32.c:67-99 -> fdfs_gpu_state_init / fdfs_gpu_update_batch /
+ *       fdfs_gpu_final_batch (+ fdfs_gpu_crc_combine for pieces hashed apart)
  *   storage_gen_filename + storage_get_store_path (random mode)
  *       storage/storage_service.c:2080-2202      -> fdfs_gpu_file_ids
  *   fdfs_get_file_info_ex's name decode
@@ -74,8 +79,8 @@ typedef struct fdfs_gpu_ctx fdfs_gpu_ctx;
 
 /* A batch of files in device memory: file i is bytes
  * [base + offset[i], base + offset[i] + size[i]).  offset/size are device
- * arrays of n entries.  Any alignment is correct; 16-byte aligned file
- * starts take the fast load path. */
+ * arrays of n entries.  Files may start at any byte (measured: byte-packed
+ * batches hash at the rate of 16-byte aligned ones). */
 typedef struct {
     const void     *base;
     const uint64_t *offset;
@@ -111,12 +116,14 @@ int fdfs_gpu_sig_batch(fdfs_gpu_ctx *ctx, const fdfs_gpu_batch *batch, int metho
 /* The same for a batch in HOST memory (the daemon's receive buffers, the
  * CLI's files): base/offset/size are host pointers, crc_out / sig_out /
  * codes_out host arrays.  Files are streamed to the device in windows of at
- * most chunk_bytes (0 = 256 MiB; a larger file goes alone), double-buffered
- * on two internal streams: window k+1 crosses PCIe while window k is hashed,
- * and each window's results come back as soon as they are ready.
- * Synchronous: returns when every result is in host memory.  A pinned base
- * (hipHostMalloc / hipHostRegister) copies at the full PCIe rate; batches
- * with increasing offsets copy each byte once. */
+ * most chunk_bytes (0 = 256 MiB), double-buffered on two internal streams
+ * (window k+1 crosses PCIe while window k is hashed); a file larger than the
+ * space left in a window continues in the next one, its state carried on the
+ * device (the chunked path below), so device memory is two windows plus
+ * 172 bytes per file whatever the file sizes.  Synchronous: returns when
+ * every result is in host memory.  A pinned base (hipHostMalloc /
+ * hipHostRegister) copies at the full PCIe rate; batches with increasing
+ * offsets copy each byte once. */
 int fdfs_gpu_sig_batch_host(fdfs_gpu_ctx *ctx, const fdfs_gpu_batch *host_batch, int method,
                             uint32_t *crc_out, uint8_t *sig_out, int32_t *codes_out,
                             uint64_t chunk_bytes);
@@ -200,6 +207,31 @@ int fdfs_gpu_dedup_bucket(fdfs_gpu_ctx *ctx, const uint8_t *sig, const uint64_t 
  * of its class) and ref (class size), in row order. */
 int fdfs_gpu_dedup_group(fdfs_gpu_ctx *ctx, const uint8_t *records, uint64_t n,
                          uint64_t *rep_out, uint32_t *ref_out, void *stream);
+
+/* Multi-GPU dedup in one call, over RCCL (xGMI between the GPUs of a node):
+ * one process per GPU, each holding its share of the ingest (sig, gidx: the
+ * files' global ingest indices); every rank calls it with its share and gets
+ * rep_out / ref_out for its own records, identical to fdfs_gpu_dedup over
+ * the concatenated ingest.  Inside: bucket by owner rank (the FastDHT key
+ * partition, storage/fdht_client/fdht_client.c:301-305, as a GPU bucket),
+ * ncclAllToAll of the per-peer row counts, grouped ncclSend/ncclRecv of the
+ * 32-byte rows, the owner's group, and the {rep, ref} answers sent back the
+ * same way.  The one host synchronisation is the count exchange (the row
+ * exchange is sized by it).  comm: an ncclComm_t (RCCL) of the ranks taking
+ * part, each rank's communicator on this context's device.  Replaces the
+ * per-file fdht_get_ex1 / fdht_set_ex / fdht_inc_ex round trips
+ * (storage/storage_service.c:2652,2714,2734,2984) for bulk ingest. */
+int fdfs_gpu_dedup_global(fdfs_gpu_ctx *ctx, void *comm, const uint8_t *sig, const uint64_t *gidx,
+                          uint64_t n, uint64_t *rep_out, uint32_t *ref_out, void *stream);
+
+/* Convenience RCCL communicator setup for callers without one: rank 0 gets
+ * a 128-byte id (ncclGetUniqueId) and sends it to the others by any means;
+ * every rank then calls fdfs_gpu_comm_init (ncclCommInitRank on ctx's
+ * device; collective: all ranks at once). */
+#define FDFS_GPU_COMM_ID_BYTES 128
+int fdfs_gpu_comm_unique_id(uint8_t *id_out);
+int fdfs_gpu_comm_init(fdfs_gpu_ctx *ctx, const uint8_t *id, int nranks, int rank, void **comm_out);
+int fdfs_gpu_comm_destroy(void *comm);
 
 /* Kernel timing (for benchmarks and profiling).  When enabled, every call
  * records a HIP event pair on its stream around its main kernel:

@@ -212,3 +212,39 @@ def test_empty_batch(ctx):
     rep, ref = ctx.dedup_group(rows)
     torch.cuda.synchronize()
     assert rep.numel() == 0 and ref.numel() == 0
+
+
+def test_dedup_global_c_abi_one_rank(oracle, ctx):
+    """fdfs_gpu_dedup_global (the C daemon's multi-GPU entry) over its own
+    RCCL communicator, set up with fdfs_gpu_comm_unique_id / comm_init (the
+    id carried by torch.distributed): one rank on this box, so every RCCL
+    call runs (count all-to-all, grouped exchanges) with one peer.  The
+    answer equals the single-GPU dedup; an empty share works too.  Ranks > 1
+    are not measurable on a one-GPU box."""
+    import socket
+    import torch.distributed as dist
+    from fastdfs_amd.api import Comm
+    from fastdfs_amd.dist import dedup_global
+
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    dist.init_process_group("nccl", init_method=f"tcp://127.0.0.1:{port}", rank=0, world_size=1,
+                            device_id=torch.device("cuda", 0))
+    comm = None
+    try:
+        comm = Comm(ctx)
+        assert comm.world == 1 and comm.rank == 0
+        for n, nu in [(120_000, 70_000), (0, 1), (5, 2)]:
+            sig = torch.from_numpy(_sigs(n, nu, 13 + n)).cuda().view(n, 24)
+            gidx = torch.arange(n, dtype=torch.int64, device="cuda") + 1000
+            rep, ref = dedup_global(ctx, sig, gidx, comm=comm)
+            torch.cuda.synchronize()
+            orep, oref = oracle.dedup(sig.cpu().numpy())
+            assert np.array_equal(rep.cpu().numpy(), orep.astype(np.int64) + 1000)
+            assert np.array_equal(ref.cpu().numpy(), oref.astype(np.int32))
+    finally:
+        if comm is not None:
+            comm.close()
+        dist.destroy_process_group()
