@@ -54,6 +54,10 @@ EXPORTS = (
     "fdfs_gpu_comm_unique_id",
     "fdfs_gpu_comm_init",
     "fdfs_gpu_comm_destroy",
+    "fdfs_gpu_index_create",
+    "fdfs_gpu_index_destroy",
+    "fdfs_gpu_index_ingest",
+    "fdfs_gpu_index_stats",
 )
 COMM_ID_BYTES = 128
 FILE_STATE_SIZE = 128  # sizeof(fdfs_gpu_file_state)
@@ -158,5 +162,13 @@ def load() -> ctypes.CDLL:
     L.fdfs_gpu_comm_init.argtypes = [vp, ctypes.c_char_p, i32, i32, ctypes.POINTER(vp)]
     L.fdfs_gpu_comm_destroy.restype = i32
     L.fdfs_gpu_comm_destroy.argtypes = [vp]
+    L.fdfs_gpu_index_create.restype = i32
+    L.fdfs_gpu_index_create.argtypes = [vp, u64, ctypes.POINTER(vp)]
+    L.fdfs_gpu_index_destroy.restype = i32
+    L.fdfs_gpu_index_destroy.argtypes = [vp]
+    L.fdfs_gpu_index_ingest.restype = i32
+    L.fdfs_gpu_index_ingest.argtypes = [vp, vp, vp, vp, u64, vp, vp, vp]
+    L.fdfs_gpu_index_stats.restype = i32
+    L.fdfs_gpu_index_stats.argtypes = [vp, ctypes.POINTER(u64), ctypes.POINTER(u64), ctypes.POINTER(u64)]
     _lib = L
     return L

@@ -477,3 +477,41 @@ class Comm:
             self.close()
         except Exception:
             pass
+
+
+class DedupIndex:
+    """fdfs_gpu_index: the FastDHT "fid" / "ref" state of an ingest stream,
+    kept in HBM across batches (include/fdfs_gpu.h)."""
+
+    def __init__(self, ctx: Context, max_classes: int):
+        h = ctypes.c_void_p()
+        ctx._rc(ctx._L.fdfs_gpu_index_create(ctx._h, max_classes, ctypes.byref(h)), "fdfs_gpu_index_create")
+        self.ctx, self._h = ctx, h
+
+    def ingest(self, sig: torch.Tensor, gidx: torch.Tensor | None = None, stream=None):
+        """Next batch of the stream: (rep int64[n], ref int32[n])."""
+        n = _check_sig(sig, gidx)
+        rep = torch.empty(n, dtype=torch.int64, device=sig.device)
+        ref = torch.empty(n, dtype=torch.int32, device=sig.device)
+        c = self.ctx
+        c._rc(c._L.fdfs_gpu_index_ingest(c._h, self._h, sig.data_ptr(), _ptr(gidx), n, rep.data_ptr(),
+                                         ref.data_ptr(), _stream_handle(stream)), "fdfs_gpu_index_ingest")
+        return rep, ref
+
+    def stats(self) -> dict:
+        cl, rec, un = ctypes.c_uint64(), ctypes.c_uint64(), ctypes.c_uint64()
+        rc = self.ctx._L.fdfs_gpu_index_stats(self._h, ctypes.byref(cl), ctypes.byref(rec), ctypes.byref(un))
+        if rc:
+            raise FdfsGpuError(rc, "fdfs_gpu_index_stats")
+        return {"classes": cl.value, "records": rec.value, "unplaced": un.value}
+
+    def close(self):
+        if getattr(self, "_h", None):
+            self.ctx._L.fdfs_gpu_index_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass

@@ -785,6 +785,141 @@ int fdfs_gpu_dedup_bucket(fdfs_gpu_ctx *ctx, const uint8_t *sig, const uint64_t 
     return e == hipSuccess ? 0 : fail(ctx, e, "dedup_bucket launch");
 }
 
+// ---- incremental dedup index ------------------------------------------------
+
+struct fdfs_gpu_index {
+    int device = 0;
+    fdfs::IndexTable t{};
+    void *mem = nullptr;
+    uint64_t records = 0;  // records ingested so far (the implicit ingest index base)
+    hipEvent_t ev = nullptr;
+    bool used = false;
+};
+
+int fdfs_gpu_index_create(fdfs_gpu_ctx *ctx, uint64_t max_classes, fdfs_gpu_index **out)
+{
+    if (!ctx || !out || max_classes > (1ull << 40))
+        return EINVAL;
+    *out = nullptr;
+    std::lock_guard<std::recursive_mutex> lk(ctx->mu);
+    DeviceGuard g(ctx->device);
+    if (!g.ok)
+        return ENODEV;
+    uint64_t slots = 1024;
+    while (slots * 3 / 4 < max_classes)  // load factor <= 0.75
+        slots <<= 1;
+    auto *ix = new (std::nothrow) fdfs_gpu_index;
+    if (!ix)
+        return ENOMEM;
+    ix->device = ctx->device;
+    const size_t bytes = align_up(24 * slots) + align_up(8 * slots) + align_up(4 * slots) + align_up(4 * slots) +
+                         align_up(8 * 4);
+    hipError_t e = hipMalloc(&ix->mem, bytes);
+    if (e != hipSuccess) {
+        delete ix;
+        std::snprintf(ctx->err, sizeof(ctx->err), "hipMalloc(%zu): %s", bytes, hipGetErrorString(e));
+        return ENOMEM;
+    }
+    Carve cv{static_cast<char *>(ix->mem)};
+    ix->t.slots = slots;
+    ix->t.keys = cv.take<uint8_t>(24 * slots);
+    ix->t.rep = cv.take<uint64_t>(slots);
+    ix->t.ref = cv.take<uint32_t>(slots);
+    ix->t.state = cv.take<uint32_t>(slots);
+    ix->t.counters = cv.take<uint64_t>(4);
+    if ((e = hipEventCreateWithFlags(&ix->ev, hipEventDisableTiming)) == hipSuccess &&
+        (e = hipMemset(ix->t.counters, 0, 32)) == hipSuccess &&
+        (e = fdfs::launch_index_clear(ix->t.state, slots, nullptr)) == hipSuccess)
+        e = hipDeviceSynchronize();
+    if (e != hipSuccess) {
+        (void)hipFree(ix->mem);
+        if (ix->ev)
+            (void)hipEventDestroy(ix->ev);
+        delete ix;
+        return fail(ctx, e, "index_create");
+    }
+    *out = ix;
+    return 0;
+}
+
+int fdfs_gpu_index_destroy(fdfs_gpu_index *ix)
+{
+    if (!ix)
+        return EINVAL;
+    DeviceGuard g(ix->device);
+    if (ix->used)
+        (void)hipEventSynchronize(ix->ev);
+    (void)hipFree(ix->mem);
+    (void)hipEventDestroy(ix->ev);
+    delete ix;
+    return 0;
+}
+
+int fdfs_gpu_index_ingest(fdfs_gpu_ctx *ctx, fdfs_gpu_index *ix, const uint8_t *sig, const uint64_t *gidx,
+                          uint64_t n, uint64_t *rep_out, uint32_t *ref_out, void *stream)
+{
+    if (!ctx || !ix || ix->device != ctx->device || n >= 0xFFFFFFFFull)
+        return EINVAL;
+    if (n == 0)
+        return 0;
+    if (!sig || !rep_out || !ref_out)
+        return EINVAL;
+    if ((reinterpret_cast<uintptr_t>(sig) | reinterpret_cast<uintptr_t>(gidx) |
+         reinterpret_cast<uintptr_t>(rep_out)) & 7)
+        return EINVAL;
+    std::lock_guard<std::recursive_mutex> lk(ctx->mu);
+    DeviceGuard g(ctx->device);
+    if (!g.ok)
+        return ENODEV;
+    hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+    const size_t dws = dedup_ws_bytes(n);
+    int rc = ensure_ws(ctx, dws + 2 * align_up(8 * n) + 2 * align_up(4 * n), st);
+    if (rc)
+        return rc;
+    WsScope wsc(ctx, st);
+    // successive ingests into one index are ordered whatever their streams
+    if (ix->used && !capturing(st))
+        (void)hipStreamWaitEvent(st, ix->ev, 0);
+    Carve cv{static_cast<char *>(ctx->ws) + dws};
+    uint64_t *rep_pos = cv.take<uint64_t>(n);
+    uint32_t *ref_b = cv.take<uint32_t>(n);
+    uint64_t *res_rep = cv.take<uint64_t>(n);
+    uint32_t *res_ref = cv.take<uint32_t>(n);
+    hipEvent_t a, b;
+    timing_pair(ctx, FDFS_KERNEL_DEDUP, a, b);
+    // 1. the batch on its own (record positions as the ingest order)
+    hipError_t e = fdfs::launch_dedup_group(sig, 24, nullptr, 0, n, ctx->ws, rep_pos, ref_b, st, a, b);
+    // 2. its classes against the index, 3. every record's answer
+    if (e == hipSuccess)
+        e = fdfs::launch_index_ingest(sig, gidx, ix->records, n, rep_pos, ref_b, ix->t, res_rep, res_ref,
+                                      rep_out, ref_out, st);
+    if (e != hipSuccess)
+        return fail(ctx, e, "index_ingest");
+    ix->records += n;
+    if (!capturing(st) && hipEventRecord(ix->ev, st) == hipSuccess)
+        ix->used = true;
+    return 0;
+}
+
+int fdfs_gpu_index_stats(fdfs_gpu_index *ix, uint64_t *classes, uint64_t *records, uint64_t *unplaced)
+{
+    if (!ix)
+        return EINVAL;
+    DeviceGuard g(ix->device);
+    uint64_t c[4] = {0, 0, 0, 0};
+    if (ix->used && hipEventSynchronize(ix->ev) != hipSuccess)
+        return EIO;
+    if (hipMemcpy(c, ix->t.counters, sizeof(c), hipMemcpyDeviceToHost) != hipSuccess)
+        return EIO;
+    if (classes)
+        *classes = c[0];
+    if (records)
+        *records = ix->records;
+    if (unplaced)
+        *unplaced = c[2];
+    return 0;
+}
+
 // ---- multi-GPU dedup over RCCL ---------------------------------------------
 
 static int nccl_fail(fdfs_gpu_ctx *ctx, ncclResult_t r, const char *where)

@@ -106,6 +106,21 @@ hipError_t launch_dedup_bucket(const uint8_t *sig, const uint64_t *gidx, uint64_
                                uint64_t *cursor, uint64_t *row_of_out, hipStream_t st,
                                hipEvent_t ev0, hipEvent_t ev1);
 
+// incremental dedup index (fdfs_index.hip)
+struct IndexTable {
+    uint64_t slots;       // power of two
+    uint8_t *keys;        // [slots][24] signatures
+    uint64_t *rep;        // [slots] class source (ingest index)
+    uint32_t *ref;        // [slots] class size so far
+    uint32_t *state;      // [slots] empty / busy / full
+    uint64_t *counters;   // [4]: classes, -, unplaced classes (table full), -
+};
+hipError_t launch_index_clear(uint32_t *state, uint64_t slots, hipStream_t st);
+hipError_t launch_index_ingest(const uint8_t *sig, const uint64_t *gidx, uint64_t gbase, uint64_t n,
+                               const uint64_t *rep_pos, const uint32_t *ref_b, const IndexTable &t,
+                               uint64_t *res_rep, uint32_t *res_ref, uint64_t *rep_out, uint32_t *ref_out,
+                               hipStream_t st);
+
 hipError_t launch_answer_pack(const uint64_t *rep, const uint32_t *ref, uint64_t m, uint64_t *ans,
                               hipStream_t st);
 hipError_t launch_answer_gather(const uint64_t *back, const uint64_t *row_of, uint64_t n, uint64_t *rep_out,

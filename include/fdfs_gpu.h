@@ -208,6 +208,30 @@ int fdfs_gpu_dedup_bucket(fdfs_gpu_ctx *ctx, const uint8_t *sig, const uint64_t 
 int fdfs_gpu_dedup_group(fdfs_gpu_ctx *ctx, const uint8_t *records, uint64_t n,
                          uint64_t *rep_out, uint32_t *ref_out, void *stream);
 
+/* Incremental dedup across ingest batches: a device-resident signature ->
+ * {source, ref} table that persists between calls, i.e. the FastDHT state
+ * the upload path builds one RPC at a time (storage/storage_service.c:2652
+ * "fid" get, :2714 set on a miss, :2734 / :2984 "ref"), kept in HBM.
+ * fdfs_gpu_index_ingest takes the next batch of an ingest stream (records in
+ * ingest order; gidx: their global ingest indices, increasing across
+ * batches, or NULL for the index's own running count) and returns for each
+ * record rep_out = the ingest index of the first file EVER ingested with its
+ * signature (an earlier batch's source stays the source) and ref_out = the
+ * class size once this batch is in.  After k batches the answers equal
+ * fdfs_gpu_dedup over the concatenation of all k.  max_classes bounds the
+ * distinct signatures (the table keeps load <= 3/4, 40 bytes per slot);
+ * classes that find no slot are answered within their batch and counted in
+ * fdfs_gpu_index_stats' unplaced (synchronous; waits for the last ingest).
+ * Ingests into one index are ordered whatever their streams. */
+typedef struct fdfs_gpu_index fdfs_gpu_index;
+int fdfs_gpu_index_create(fdfs_gpu_ctx *ctx, uint64_t max_classes, fdfs_gpu_index **out);
+int fdfs_gpu_index_destroy(fdfs_gpu_index *index);
+int fdfs_gpu_index_ingest(fdfs_gpu_ctx *ctx, fdfs_gpu_index *index, const uint8_t *sig,
+                          const uint64_t *gidx, uint64_t n, uint64_t *rep_out, uint32_t *ref_out,
+                          void *stream);
+int fdfs_gpu_index_stats(fdfs_gpu_index *index, uint64_t *classes, uint64_t *records,
+                         uint64_t *unplaced);
+
 /* Multi-GPU dedup in one call, over RCCL (xGMI between the GPUs of a node):
  * one process per GPU, each holding its share of the ingest (sig, gidx: the
  * files' global ingest indices); every rank calls it with its share and gets

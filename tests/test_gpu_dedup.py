@@ -248,3 +248,60 @@ def test_dedup_global_c_abi_one_rank(oracle, ctx):
         if comm is not None:
             comm.close()
         dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("nbatch", [1, 2, 5])
+def test_incremental_index_matches_sequential_ingest(oracle, ctx, nbatch):
+    """fdfs_gpu_index: a stream ingested in k batches.  After batch j every
+    record's source is the first file ever ingested with its signature and
+    its ref the class size so far: the oracle's sequential dedup over the
+    prefix of batches 0..j, restricted to batch j."""
+    from fastdfs_amd.api import DedupIndex
+    n = 300_000
+    sig = _sigs(n, 200_000, 40 + nbatch)
+    cuts = np.sort(np.random.default_rng(nbatch).choice(np.arange(1, n), nbatch - 1, replace=False))
+    bounds = [0] + list(cuts) + [n]
+    ix = DedupIndex(ctx, 250_000)
+    try:
+        for j in range(nbatch):
+            lo, hi = bounds[j], bounds[j + 1]
+            part = torch.from_numpy(sig[lo:hi]).cuda()
+            rep, ref = ix.ingest(part)
+            torch.cuda.synchronize()
+            orep, oref = oracle.dedup(sig[:hi], nthreads=8)
+            assert np.array_equal(rep.cpu().numpy(), orep[lo:hi].astype(np.int64)), j
+            assert np.array_equal(ref.cpu().numpy(), oref[lo:hi].astype(np.int32)), j
+        st = ix.stats()
+        assert st["records"] == n and st["unplaced"] == 0
+        assert st["classes"] == np.unique(sig, axis=0).shape[0]
+    finally:
+        ix.close()
+
+
+def test_incremental_index_gidx_and_collisions(oracle, ctx):
+    """Explicit increasing ingest indices, crafted signatures sharing a whole
+    64-bit dedup key across batches, and a full table (unplaced classes are
+    answered within their batch and counted)."""
+    from fastdfs_amd.api import DedupIndex
+    coll = _colliding(300, 5)
+    sig = np.concatenate([coll, coll[:100], _sigs(5000, 3000, 6), coll[50:250]])
+    gidx = np.cumsum(np.random.default_rng(2).integers(1, 9, len(sig))).astype(np.int64)
+    ix = DedupIndex(ctx, 20_000)
+    try:
+        for lo, hi in [(0, 350), (350, 3000), (3000, len(sig))]:
+            rep, ref = ix.ingest(torch.from_numpy(sig[lo:hi]).cuda(), torch.from_numpy(gidx[lo:hi]).cuda())
+            orep, oref = oracle.dedup(sig[:hi])
+            assert np.array_equal(rep.cpu().numpy(), gidx[orep[lo:hi].astype(np.int64)])
+            assert np.array_equal(ref.cpu().numpy(), oref[lo:hi].astype(np.int32))
+    finally:
+        ix.close()
+    small = DedupIndex(ctx, 10)  # 1024 slots for ~3,300 classes: most find no slot
+    try:
+        rep, ref = small.ingest(torch.from_numpy(sig).cuda())
+        orep, oref = oracle.dedup(sig)
+        assert np.array_equal(rep.cpu().numpy(), orep.astype(np.int64))
+        assert np.array_equal(ref.cpu().numpy(), oref.astype(np.int32))
+        st = small.stats()
+        assert st["classes"] == 1024 and st["unplaced"] == np.unique(sig, axis=0).shape[0] - 1024
+    finally:
+        small.close()
