@@ -33,6 +33,86 @@ def shard_lpt(sizes: np.ndarray, nranks: int) -> list[np.ndarray]:
     return [np.nonzero(owner == r)[0] for r in range(nranks)]
 
 
+def plan_crc_pieces(sizes, nranks: int) -> list[list[tuple[int, int, int]]]:
+    """CRC-only work split by bytes: the files' concatenated
+    byte stream is cut into nranks contiguous shares of equal size, so a
+    file larger than a share (or straddling a cut) is split into pieces on
+    consecutive ranks, in byte order.  CRC32 is linear over GF(2), so the
+    pieces are hashed independently and joined by crc32_combine; ELFHash and
+    MD5 are not splittable and use shard_lpt.  Returns, per rank, its
+    (file, start, length) pieces; every rank computes the same plan."""
+    sizes = np.asarray(sizes, dtype=np.int64)
+    total = int(sizes.sum())
+    share = -(-total // nranks) if total else 0
+    plan: list[list[tuple[int, int, int]]] = [[] for _ in range(nranks)]
+    r, room = 0, share
+    for f, sz in enumerate(sizes.tolist()):
+        a = 0
+        while a < sz:
+            while room == 0 and r < nranks - 1:
+                r, room = r + 1, share
+            take = sz - a if r == nranks - 1 else min(sz - a, room)
+            plan[r].append((f, a, take))
+            a += take
+            room -= take
+    return plan
+
+
+def crc_batch_global(kernels, sizes, plan, data: torch.Tensor, offsets: torch.Tensor, group=None):
+    """CRC32 of files whose bytes are spread over the ranks as `plan`
+    (plan_crc_pieces) says: this rank holds its pieces in `data` at
+    `offsets` (int64, one per piece of plan[rank], in plan order).
+
+    Each rank hashes its pieces from a zero state (fdfs_gpu_update_batch on
+    zeroed states: CRC32_ex(piece, 0)), one all-gather moves the 4-byte
+    partial states, and every rank folds each file's pieces in byte order:
+    acc = M^|piece| acc ^ part (fdfs_gpu_crc_combine), from CRC32_XINIT; the
+    file CRC is CRC32_FINAL(acc).  Returns uint32 CRCs (int32 bit patterns)
+    of all files on every rank.  kernels: a fastdfs_amd.Context (tests
+    substitute a CPU double)."""
+    rank, world = dist.get_rank(group), dist.get_world_size(group)
+    dev = data.device
+    sizes = np.asarray(sizes, dtype=np.int64)
+    nfiles = sizes.size
+    mine = plan[rank]
+    m = len(mine)
+    lens = torch.tensor([p[2] for p in mine], dtype=torch.int64, device=dev)
+    part = torch.zeros(max(m, 1), dtype=torch.int32, device=dev)
+    if m:
+        states = torch.zeros((m, 128), dtype=torch.uint8, device=dev)  # crc32 = 0, count = 0
+        kernels.update_batch(states, data, offsets, lens, method=0)
+        part[:m] = states[:, :4].contiguous().view(torch.int32).view(-1)
+    # 4 bytes per piece to every rank (padded to the longest piece list)
+    mp = max(max(len(p) for p in plan), 1)
+    send = torch.zeros(mp, dtype=torch.int32, device=dev)
+    send[:m] = part[:m]
+    gathered = [torch.empty_like(send) for _ in range(world)]
+    dist.all_gather(gathered, send, group=group)
+    # piece k of every file, byte order = rank order then plan order
+    per_file: list[list[tuple[int, int, int]]] = [[] for _ in range(nfiles)]
+    for r in range(world):
+        for j, (f, a, ln) in enumerate(plan[r]):
+            per_file[f].append((a, r * mp + j, ln))
+    for pcs in per_file:
+        pcs.sort()
+    kmax = max((len(p) for p in per_file), default=0)
+    flat = torch.cat(gathered)
+    acc = torch.full((nfiles,), -1, dtype=torch.int32, device=dev)  # CRC32_XINIT
+    for k in range(kmax):
+        idx = np.zeros(nfiles, np.int64)
+        ln = np.zeros(nfiles, np.int64)
+        has = np.zeros(nfiles, bool)
+        for f, pcs in enumerate(per_file):
+            if k < len(pcs):
+                _, idx[f], ln[f] = pcs[k]
+                has[f] = True
+        b = torch.where(torch.from_numpy(has).to(dev), flat[torch.from_numpy(idx).to(dev)],
+                        torch.zeros((), dtype=torch.int32, device=dev))
+        # missing piece: length 0 and part 0 leave acc unchanged
+        acc = kernels.crc_combine(acc, b.contiguous(), torch.from_numpy(ln).to(dev))
+    return acc ^ -1  # CRC32_FINAL
+
+
 def dedup_global(kernels, sig: torch.Tensor, gidx: torch.Tensor, group=None, stats=None, comm=None):
     """Dedup across all ranks of `group`.
 

@@ -15,7 +15,7 @@ import torch
 import torch.distributed as dist
 import torch.multiprocessing as mp
 
-from fastdfs_amd.dist import dedup_global, shard_lpt
+from fastdfs_amd.dist import crc_batch_global, dedup_global, plan_crc_pieces, shard_lpt
 
 
 class CpuKernelsDouble:
@@ -128,3 +128,83 @@ def test_c5_signature_shares(world):
     assert torch.equal(gidx1, torch.arange(total))
     uniq = np.unique(one.numpy(), axis=0).shape[0]
     assert uniq <= total - total // 10 and uniq > total * 0.85
+
+
+class CpuCrcDouble:
+    """Test double of Context.update_batch (CRC only) and crc_combine, from
+    the oracle's CRC32_ex restatement: update = CRC32_ex(chunk, state),
+    combine(a, b, n) = CRC32_ex(n zero bytes, a) ^ b."""
+
+    def __init__(self, variant=0):
+        from oracle import oracle as O
+        self.O, self.v = O, variant
+
+    def update_batch(self, states, data, offsets, sizes, method=0):
+        assert method == 0
+        d = data.numpy()
+        crc = states[:, :4].contiguous().view(torch.int32).view(-1)
+        for i, (o, n) in enumerate(zip(offsets.tolist(), sizes.tolist())):
+            c = self.O.crc32_ex(d[o:o + n], int(crc[i]), self.v)
+            states[i, :4] = torch.tensor([c], dtype=torch.int32).view(torch.uint8)
+
+    def crc_combine(self, a, b, n):
+        out = [self.O.crc32_ex(np.zeros(int(ln), np.uint8), int(x), self.v) ^ int(y)
+               for x, y, ln in zip(a.tolist(), b.tolist(), n.tolist())]
+        return torch.tensor(np.array(out, np.int64).astype(np.uint32).view(np.int32))
+
+
+def _crc_worker(rank, world, port, sizes, blob, out_q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        starts = np.concatenate([[0], np.cumsum(sizes)[:-1]])
+        plan = plan_crc_pieces(sizes, world)
+        parts, offs, pos = [], [], 0
+        for f, a, ln in plan[rank]:
+            offs.append(pos)
+            parts.append(blob[starts[f] + a: starts[f] + a + ln])
+            pos += ln
+        data = torch.from_numpy(np.concatenate(parts + [np.zeros(1, np.uint8)]))
+        crc = crc_batch_global(CpuCrcDouble(), sizes, plan, data, torch.tensor(offs, dtype=torch.int64))
+        out_q.put((rank, crc.numpy().view(np.uint32)))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_crc_batch_global_gloo(oracle, world):
+    """Files split across ranks by bytes: one file much larger
+    than a share is cut over every rank, small ones straddle cuts; the
+    partial CRC32_ex states travel by all-gather and fold by crc32_combine
+    to the oracle's CRC on every rank."""
+    rng = np.random.default_rng(10 + world)
+    sizes = np.array([3, 70_000, 0, 11, 5_000, 1234, 1], np.int64)
+    blob = rng.integers(0, 256, int(sizes.sum()), dtype=np.uint8)
+    plan = plan_crc_pieces(sizes, world)
+    assert sum(1 for p in plan for _ in p) > len(sizes) - 1  # something was split
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_crc_worker, args=(r, world, port, sizes, blob, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    got = dict(q.get(timeout=120) for _ in range(world))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    starts = np.concatenate([[0], np.cumsum(sizes)[:-1]])
+    want = np.array([oracle.crc32(blob[s:s + n]) for s, n in zip(starts, sizes)], np.uint32)
+    for r in range(world):
+        assert np.array_equal(got[r], want)
+
+
+def test_plan_crc_pieces_balance():
+    sizes = np.array([1 << 30] * 4, np.int64)  # 4 x 1 GiB on 8 GPUs: every file on 2 ranks
+    plan = plan_crc_pieces(sizes, 8)
+    loads = [sum(p[2] for p in pr) for pr in plan]
+    assert loads == [1 << 29] * 8
+    for f in range(4):
+        pcs = sorted((a, ln) for pr in plan for g, a, ln in pr if g == f)
+        assert pcs[0][0] == 0 and sum(ln for _, ln in pcs) == 1 << 30
+    assert plan_crc_pieces(np.array([], np.int64), 3) == [[], [], []]

@@ -236,3 +236,46 @@ def test_many_uploads_one_chunk_each(oracle, ctxs):
     ocrc, osig = oracle.dio_batch(np.concatenate(files), offs, sizes.astype(np.uint64), 2, 0, nthreads=8)
     assert np.array_equal(crc, ocrc)
     assert np.array_equal(sig, osig)
+
+
+def test_crc_batch_global_one_rank(oracle, ctxs):
+    """dist.crc_batch_global on the HIP kernels over a real RCCL group (one
+    rank): every file cut into several pieces (zero-state updates, the
+    all-gather, crc32_combine folds in byte order) gives the oracle's CRC.
+    The multi-rank exchange is covered by the gloo tests."""
+    import socket
+    import torch.distributed as dist
+    from fastdfs_amd.dist import crc_batch_global
+
+    rng = np.random.default_rng(61)
+    sizes = np.array([0, 5, (3 << 20) + 11, 70_001, 1 << 20], np.int64)
+    files = _files(rng, sizes)
+    plan = [[]]
+    for f, n in enumerate(sizes):
+        cuts = np.sort(rng.choice(np.arange(1, max(int(n), 2)), size=min(3, max(int(n) - 1, 0)), replace=False))
+        edges = [0] + [int(c) for c in cuts] + [int(n)]
+        for a, b in zip(edges[:-1], edges[1:]):
+            plan[0].append((f, a, b - a))
+    offs, parts, pos = [], [], 0
+    for f, a, ln in plan[0]:
+        pos += int(rng.integers(0, 5))
+        offs.append(pos)
+        parts.append((pos, files[f][a:a + ln]))
+        pos += ln
+    buf = np.zeros(pos + 1, np.uint8)
+    for p0, b in parts:
+        buf[p0:p0 + len(b)] = b
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    dist.init_process_group("nccl", init_method=f"tcp://127.0.0.1:{port}", rank=0, world_size=1,
+                            device_id=torch.device("cuda", 0))
+    try:
+        for v in (0, 1):
+            crc = crc_batch_global(ctxs[v], sizes, plan, torch.from_numpy(buf).cuda(),
+                                   torch.tensor(offs, dtype=torch.int64, device="cuda"))
+            got = crc.cpu().numpy().view(np.uint32)
+            assert [int(x) for x in got] == [oracle.crc32(f, v) for f in files], v
+    finally:
+        dist.destroy_process_group()
