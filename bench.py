@@ -481,7 +481,7 @@ def main():
                            "peak": HBM_PEAK_GBS, "unit": "GB/s",
                            "frac": round(nb / (avg_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
                            "traffic": None,
-                           "kernel": "dedup_group (dp_keys + scan + dp_scatter + dp_split + dp_group)",
+                           "kernel": "dedup_group (dp_tile + scan + chunks + dp_split + dp_group)",
                            "kernel_ms_avg": round(avg_ms, 4), "algorithmic_bytes_per_launch": nb,
                            "algorithmic_bytes_per_record": per_rec}
         if world == 1:

@@ -12,18 +12,21 @@
 //    partition, storage/fdht_client/fdht_client.c:301-305, re-expressed as a
 //    GPU bucket).
 //  * dedup_group: partition, then group each partition in LDS.
-//      K1 dp_keys      key32 = low half of a 64-bit mix of the signature;
-//                      per-tile LDS histogram of its top D1 bits
+//      K1 dp_tile      key32 = low half of a 64-bit mix of the signature;
+//                      each 8192-record tile sorted by the top D1 bits in LDS
+//                      and written back contiguously
 //      K2 scan         exclusive scan of the [digit][tile] counts
-//      K3 dp_scatter   (key32, record) pairs to their D1 bucket (LDS ranks)
-//      K4 dp_split     one workgroup per D1 bucket splits it by the next D2
-//                      bits (LDS histogram + scan + LDS cursors)
-//      K5 dp_group     one workgroup per partition (~1K records): an
-//                      open-addressing table in LDS keyed by key32, a slot
-//                      is claimed by 64-bit CAS of {key32, claimer} and never
-//                      changes, equal keys are confirmed on the full 24 bytes
-//                      against the claimer's row, class min(gidx) and size
-//                      by LDS atomics, then rep/ref written per record.
+//      K3 chunks       D1 buckets cut into 8192-entry chunks
+//      K4 dp_split     one workgroup per chunk: gathers its entries along the
+//                      tile runs, sorts them by the next D2 bits in LDS and
+//                      writes the chunk back contiguously
+//      K5 dp_group     one workgroup per partition (~1K records): gathers its
+//                      run from each chunk of its bucket; an open-addressing
+//                      table in LDS keyed by key32, a slot is claimed by
+//                      64-bit CAS of {key32, claimer} and never changes,
+//                      equal keys are confirmed on the full 24 bytes against
+//                      the claimer's row, class min(gidx) and size by LDS
+//                      atomics, then rep/ref written per record.
 //    Every random-access atomic stays in LDS: device-scope atomics to
 //    random addresses run at a few percent of the HBM rate on MI355X
 //    (MI355X_MICROARCH.md, global atomics), which is what bounded the
@@ -35,6 +38,7 @@
 #include "fdfs_device.hpp"
 #include "fdfs_kernels.hpp"
 
+#include <climits>
 #include <cstdlib>
 
 namespace fdfs {
@@ -70,64 +74,61 @@ __device__ __forceinline__ bool sig_equal(const uint8_t *sig, uint32_t stride, u
     return a == a2 && b == b2 && c == c2;
 }
 
-constexpr int kDpTileThreads = 256;
+// Partition plan.  Entries are 8 bytes, {key32 << 32 | record}; a record's
+// partition is the top d1 + d2 bits of key32 (~1K records per partition).
+//  K1 dp_tile   a tile of kDpTile records: keys, singleton answers, the tile's
+//               entries sorted by the top d1 bits in LDS and written back
+//               contiguously (one coalesced run per tile, no scatter);
+//               per (digit, tile) count and in-tile start
+//  K2 scan      exclusive scan of the [digit][tile] counts: where each tile's
+//               run of a digit goes in the bucket-sorted order
+//  K3 chunks    each d1 bucket cut into kDpChunk-entry chunks (positions in
+//               the bucket-sorted order); the tile holding each chunk's
+//               first position
+//  K4 dp_split  one workgroup per chunk: gathers the chunk's entries from the
+//               tile runs (coalesced reads along each run), sorts them by the
+//               next d2 bits in LDS, writes the chunk back contiguously and
+//               the chunk's d2 digit starts (u16)
+//  K5 dp_group  one workgroup per partition (bucket b, digit d): gathers its
+//               run from each chunk of bucket b, then groups in LDS
+// Every HBM write of K1 and K4 is a whole contiguous tile/chunk (round 1's
+// scatter and split wrote ~16-entry runs per digit: partial lines, 1.2x
+// their bytes), and the split needs no counting pass.
+constexpr int kDpTileThreads = 512;
 constexpr int kDpTileItems = 16;
-constexpr int kDpTile = kDpTileThreads * kDpTileItems;  // records per K1/K3 tile
+constexpr int kDpTile = kDpTileThreads * kDpTileItems;  // records per K1 tile
 constexpr int kDpMaxD1 = 8;
 constexpr int kDpMaxD2 = 12;
-constexpr int kDpSlotsLog = 11;  // LDS table: 2048 slots
+constexpr int kDpSplitThreads = 1024;
+constexpr int kDpSplitPer = 8;
+constexpr int kDpChunk = kDpSplitThreads * kDpSplitPer;  // entries per K4 chunk
+static_assert(kDpChunk < 65536, "chunk digit starts are u16");
+constexpr int kDpSlotsLog = 12;  // LDS table: 4096 slots (80 KB, two workgroups per CU)
 constexpr int kDpSlots = 1 << kDpSlotsLog;
 constexpr uint32_t kDpCap = kDpSlots * 3 / 4;  // records per partition grouped in LDS
 constexpr uint64_t kDpEmpty = ~0ull;
-constexpr int kDpGroupThreads = 512;
+constexpr int kDpGroupThreads = 1024;
+constexpr int kDpRuns = kDpGroupThreads;  // chunk runs per K5 gather batch (one per thread)
 
 struct DpPlan {
-    int d1, d2;          // partition bits: top d1 of key32 (K3), next d2 (K4)
-    uint64_t tiles;      // K1/K3 tiles
+    int d1, d2;          // partition bits: top d1 of key32 (K1), next d2 (K4)
+    uint64_t tiles;      // K1 tiles
+    uint64_t chunks;     // bound on K4 chunks: sum over buckets of ceil(size / kDpChunk)
     uint64_t nparts() const { return 1ull << (d1 + d2); }
+    uint64_t ncnt() const { return (1ull << d1) * tiles; }
 };
 
 DpPlan dp_plan(uint64_t n)
 {
-    int p = 1;  // partitions of ~1K records: mean n / 2^p <= 1024
-    while (p < kDpMaxD1 + kDpMaxD2 && (n >> p) > 1024)
+    int p = 1;  // partitions of ~2K records: mean n / 2^p <= 2048
+    while (p < kDpMaxD1 + kDpMaxD2 && (n >> p) > 2048)
         p++;
     DpPlan pl;
     pl.d1 = p < kDpMaxD1 ? p : kDpMaxD1;
     pl.d2 = p - pl.d1;
     pl.tiles = (n + kDpTile - 1) / kDpTile;
+    pl.chunks = (n + kDpChunk - 1) / kDpChunk + (1ull << pl.d1);
     return pl;
-}
-
-// K1: key32 per record + the tile's histogram of the top d1 bits; the
-// singleton answer (rep = own gidx, ref = 1) for every record
-__global__ __launch_bounds__(kDpTileThreads) void dp_keys_kernel(
-    const uint8_t *__restrict__ sig, uint32_t stride, const uint64_t *__restrict__ gidx,
-    uint32_t gstride, uint64_t n, int d1, uint64_t tiles, uint32_t *__restrict__ keys,
-    uint64_t *__restrict__ rep_out, uint32_t *__restrict__ ref_out, uint64_t *__restrict__ counts)
-{
-    __shared__ uint32_t h[1 << kDpMaxD1];
-    for (int k = threadIdx.x; k < (1 << d1); k += blockDim.x)
-        h[k] = 0;
-    __syncthreads();
-    const uint64_t t0 = (uint64_t)blockIdx.x * kDpTile;
-    for (int it = 0; it < kDpTileItems; it++) {
-        const uint64_t r = t0 + (uint64_t)it * kDpTileThreads + threadIdx.x;
-        if (r < n) {
-            uint64_t a, b, c;
-            load_sig(sig + r * stride, a, b, c);
-            const uint32_t key = (uint32_t)sig_hash(a, b, c);
-            keys[r] = key;
-            // every record starts as its own class; dp_group overwrites the
-            // records of classes with more than one member
-            rep_out[r] = gstride ? gidx[r * gstride] : r;
-            ref_out[r] = 1;
-            atomicAdd(&h[key >> (32 - d1)], 1u);
-        }
-    }
-    __syncthreads();
-    for (int k = threadIdx.x; k < (1 << d1); k += blockDim.x)
-        counts[(uint64_t)k * tiles + blockIdx.x] = h[k];
 }
 
 // Exclusive scan of cnt[0, nb) into out[] by the whole block (each thread
@@ -167,25 +168,94 @@ __device__ __forceinline__ void block_scan_bins(const uint32_t *cnt, uint32_t *o
     __syncthreads();
 }
 
-// K3: the 8-byte entry {key32 << 32 | record} to its d1 bucket.  The tile is
-// ranked by LDS counters (unstable: order inside a partition does not
-// matter), sorted by digit in LDS and written out as contiguous runs (one run
-// per digit).  The ingest index is not carried: dp_group reads it only for
-// records of multi-member classes.
-__global__ __launch_bounds__(kDpTileThreads) void dp_scatter_kernel(
-    const uint32_t *__restrict__ keys, uint64_t n, int d1, uint64_t tiles,
-    const uint64_t *__restrict__ off, uint64_t *__restrict__ ent)
+// One value per thread: exclusive prefix over the block and the block total.
+__device__ __forceinline__ uint32_t block_scan1(uint32_t v, uint32_t *wsum, uint32_t &total)
 {
-    __shared__ uint32_t cnt[1 << kDpMaxD1];
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    uint32_t x = v;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t y = __shfl_up(x, o);
+        if (lane >= o)
+            x += y;
+    }
+    if (lane == 63)
+        wsum[wid] = x;
+    __syncthreads();
+    uint32_t pre = 0, tot = 0;
+    for (int k = 0; k < (int)(blockDim.x >> 6); k++) {
+        if (k < wid)
+            pre += wsum[k];
+        tot += wsum[k];
+    }
+    __syncthreads();
+    total = tot;
+    return pre + x - v;
+}
+
+__device__ __forceinline__ uint64_t block_exclusive_scan64(uint64_t v, uint64_t *wsum, uint64_t &total)
+{
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    uint64_t x = v;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint64_t y = __shfl_up(x, o);
+        if (lane >= o)
+            x += y;
+    }
+    if (lane == 63)
+        wsum[wid] = x;
+    __syncthreads();
+    uint64_t pre = 0, tot = 0;
+    for (int k = 0; k < (int)(blockDim.x >> 6); k++) {
+        if (k < wid)
+            pre += wsum[k];
+        tot += wsum[k];
+    }
+    __syncthreads();
+    total = tot;
+    return pre + x - v;
+}
+
+// Max over the threads before this one (-1 for thread 0).
+__device__ __forceinline__ int32_t block_max_excl(int32_t v, int32_t *wmax)
+{
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    int32_t x = v;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const int32_t y = __shfl_up(x, o);
+        if (lane >= o)
+            x = y > x ? y : x;
+    }
+    if (lane == 63)
+        wmax[wid] = x;
+    __syncthreads();
+    int32_t run = __shfl_up(x, 1);
+    if (lane == 0)
+        run = -1;
+    for (int k = 0; k < wid; k++)
+        run = wmax[k] > run ? wmax[k] : run;
+    __syncthreads();
+    return run;
+}
+
+// K1: keys, the singleton answer (rep = own gidx, ref = 1) of every record,
+// and the tile's entries sorted by digit (top d1 bits; unstable: order inside
+// a partition does not matter) written back as one contiguous run.
+__global__ __launch_bounds__(kDpTileThreads) void dp_tile_kernel(
+    const uint8_t *__restrict__ sig, uint32_t stride, const uint64_t *__restrict__ gidx,
+    uint32_t gstride, uint64_t n, int d1, uint64_t tiles, uint64_t *__restrict__ ent1,
+    uint64_t *__restrict__ rep_out, uint32_t *__restrict__ ref_out, uint64_t *__restrict__ cnt1,
+    uint32_t *__restrict__ loc1)
+{
+    __shared__ uint32_t h[1 << kDpMaxD1];
     __shared__ uint32_t lst[1 << kDpMaxD1];
-    __shared__ uint64_t bas[1 << kDpMaxD1];
     __shared__ uint32_t wsum[kDpTileThreads / 64];
     __shared__ uint64_t stage[kDpTile];
     const uint32_t nb = 1u << d1;
-    for (uint32_t k = threadIdx.x; k < nb; k += blockDim.x) {
-        cnt[k] = 0;
-        bas[k] = off[(uint64_t)k * tiles + blockIdx.x];
-    }
+    for (uint32_t k = threadIdx.x; k < nb; k += blockDim.x)
+        h[k] = 0;
     __syncthreads();
     const uint64_t t0 = (uint64_t)blockIdx.x * kDpTile;
     const uint32_t m = (uint32_t)((n - t0) < (uint64_t)kDpTile ? (n - t0) : (uint64_t)kDpTile);
@@ -194,12 +264,24 @@ __global__ __launch_bounds__(kDpTileThreads) void dp_scatter_kernel(
     for (int it = 0; it < kDpTileItems; it++) {
         const uint32_t l = it * kDpTileThreads + threadIdx.x;
         if (l < m) {
-            key[it] = keys[t0 + l];
-            rank[it] = atomicAdd(&cnt[key[it] >> (32 - d1)], 1u);
+            const uint64_t r = t0 + l;
+            uint64_t a, b, c;
+            load_sig(sig + r * stride, a, b, c);
+            key[it] = (uint32_t)sig_hash(a, b, c);
+            // every record starts as its own class; dp_group overwrites the
+            // records of classes with more than one member
+            rep_out[r] = gstride ? gidx[r * gstride] : r;
+            ref_out[r] = 1;
         }
     }
+#pragma unroll
+    for (int it = 0; it < kDpTileItems; it++) {
+        const uint32_t l = it * kDpTileThreads + threadIdx.x;
+        if (l < m)
+            rank[it] = atomicAdd(&h[key[it] >> (32 - d1)], 1u);
+    }
     __syncthreads();
-    block_scan_bins<1, kDpTileThreads>(cnt, lst, nb, wsum);
+    block_scan_bins<1, kDpTileThreads>(h, lst, nb, wsum);
 #pragma unroll
     for (int it = 0; it < kDpTileItems; it++) {
         const uint32_t l = it * kDpTileThreads + threadIdx.x;
@@ -207,93 +289,160 @@ __global__ __launch_bounds__(kDpTileThreads) void dp_scatter_kernel(
             stage[lst[key[it] >> (32 - d1)] + rank[it]] = ((uint64_t)key[it] << 32) | (uint32_t)(t0 + l);
     }
     __syncthreads();
-    for (uint32_t j = threadIdx.x; j < m; j += blockDim.x) {
-        const uint64_t en = stage[j];
-        const uint32_t d = (uint32_t)(en >> (64 - d1));
-        ent[bas[d] + (j - lst[d])] = en;
+    for (uint32_t j = threadIdx.x; j < m; j += blockDim.x)
+        ent1[t0 + j] = stage[j];
+    for (uint32_t k = threadIdx.x; k < nb; k += blockDim.x) {
+        cnt1[(uint64_t)k * tiles + blockIdx.x] = h[k];
+        loc1[(uint64_t)k * tiles + blockIdx.x] = lst[k];
     }
 }
 
-// K4: one workgroup per d1 bucket: split by the next d2 bits into ent2 and
-// write the partition starts (pstart[nparts] = n).  A first pass counts the
-// whole bucket; the second goes chunk by chunk (rank, LDS sort by digit,
-// contiguous runs out, per-digit cursors advanced by the chunk's counts).
-constexpr int kDpSplitThreads = 1024;
-constexpr int kDpSplitPer = 8;  // entries per thread per chunk (FDFS_GPU_DEDUP_SPLIT=4: A/B)
+// K3a: chunks per bucket, exclusive prefix -> cb[0..nb1] (one block of 256).
+__global__ __launch_bounds__(256) void dp_chunks_kernel(const uint64_t *__restrict__ off1, int d1,
+                                                        uint64_t tiles, uint32_t *__restrict__ cb,
+                                                        uint32_t *__restrict__ slow)
+{
+    if (threadIdx.x == 0)
+        slow[0] = 0;  // K5's list of partitions for dp_group_slow_kernel
+    __shared__ uint32_t c[1 << kDpMaxD1];
+    __shared__ uint32_t s[1 << kDpMaxD1];
+    __shared__ uint32_t wsum[4];
+    const uint32_t nb1 = 1u << d1;
+    for (uint32_t k = threadIdx.x; k < nb1; k += blockDim.x) {
+        const uint64_t size = off1[(uint64_t)(k + 1) * tiles] - off1[(uint64_t)k * tiles];
+        c[k] = (uint32_t)((size + kDpChunk - 1) / kDpChunk);
+    }
+    __syncthreads();
+    block_scan_bins<1, 256>(c, s, nb1, wsum);
+    for (uint32_t k = threadIdx.x; k < nb1; k += blockDim.x)
+        cb[k] = s[k];
+    if (threadIdx.x == 0)
+        cb[nb1] = s[nb1 - 1] + c[nb1 - 1];
+}
 
-template <int PER_T>
+// K3b: for every non-empty (digit, tile) run, the chunks of that bucket whose
+// first position falls inside it start at that tile.
+__global__ void dp_chunk_ta_kernel(const uint64_t *__restrict__ off1, uint64_t tiles, uint64_t ncnt,
+                                   const uint32_t *__restrict__ cb, uint32_t *__restrict__ chunk_ta)
+{
+    for (uint64_t idx = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; idx < ncnt;
+         idx += (uint64_t)gridDim.x * blockDim.x) {
+        const uint64_t o = off1[idx], o2 = off1[idx + 1];
+        if (o2 <= o)
+            continue;
+        const uint64_t b = idx / tiles, t = idx - b * tiles;
+        const uint64_t bs = off1[b * tiles];
+        for (uint64_t k = (o - bs + kDpChunk - 1) / kDpChunk; bs + k * kDpChunk < o2; k++)
+            chunk_ta[cb[b] + k] = (uint32_t)t;
+    }
+}
+
+// K4: one workgroup per chunk (global chunk id g; bucket b = the one with
+// cb[b] <= g < cb[b + 1]).  Every position of the chunk is mapped to its
+// source in the tile-sorted K1 output: each tile run overlapping the chunk
+// marks its first position with (source - position), a block max-scan carries
+// the mark over the run, and the entries are loaded along the runs.  They are
+// then ranked by the d2 digit in LDS and the chunk goes back contiguously.
+constexpr int64_t kDpNoMark = INT64_MIN;
+
+// NB: digit bins (1 << d2 <= NB); 1024 bins keep the LDS at 72 KB, two
+// workgroups per CU.
+template <int NB>
 __global__ __launch_bounds__(kDpSplitThreads) void dp_split_kernel(
-    const uint64_t *__restrict__ ent, uint64_t n, int d1, int d2, uint64_t tiles,
-    const uint64_t *__restrict__ off, uint64_t *__restrict__ ent2, uint32_t *__restrict__ pstart)
+    const uint64_t *__restrict__ ent1, int d1, int d2, uint64_t tiles, const uint64_t *__restrict__ off1,
+    const uint32_t *__restrict__ loc1, const uint32_t *__restrict__ cb, const uint32_t *__restrict__ chunk_ta,
+    uint64_t *__restrict__ ent2, uint16_t *__restrict__ cdo)
 {
-    constexpr int NB = 1 << kDpMaxD2;
-    constexpr int PER = NB / kDpSplitThreads;
-    __shared__ uint32_t h[NB];    // bucket counts, then the running cursor (relative to s)
-    __shared__ uint32_t cc[NB];   // chunk counts
-    __shared__ uint32_t cl[NB];   // chunk-local starts
-    __shared__ uint32_t wsum[kDpSplitThreads / 64];
-    constexpr int kDpChunk = kDpSplitThreads * PER_T;
-    __shared__ uint64_t stage[kDpChunk];
-    const uint32_t nd2 = 1u << d2;
-    const uint64_t s = off[(uint64_t)blockIdx.x * tiles];
-    const uint64_t e = (blockIdx.x + 1 == (1u << d1)) ? n : off[(uint64_t)(blockIdx.x + 1) * tiles];
-    const int sh = 64 - d1 - d2;  // d2 digit = (entry.x >> sh) & (nd2 - 1)
-    for (uint32_t k = threadIdx.x; k < nd2; k += blockDim.x)
-        h[k] = 0;
+    constexpr int NT = kDpSplitThreads;
+    constexpr int PER = NB / NT;
+    static_assert(NB % NT == 0, "bins per thread");
+    __shared__ int64_t buf[kDpChunk];  // position -> source offset, then the digit-sorted chunk
+    __shared__ uint32_t cc[NB];        // chunk digit counts
+    __shared__ uint32_t cl[NB];        // chunk digit starts
+    __shared__ uint32_t wsum[NT / 64];
+    __shared__ int32_t wmax[NT / 64];
+    __shared__ uint32_t sbk;
+    const uint32_t nb1 = 1u << d1, nd2 = 1u << d2;
+    const uint32_t g = blockIdx.x;
+    if (g >= cb[nb1])  // past the last chunk (the grid is a bound)
+        return;
+    if (threadIdx.x < nb1 && cb[threadIdx.x] <= g && g < cb[threadIdx.x + 1])
+        sbk = threadIdx.x;
+    for (uint32_t k = threadIdx.x; k < nd2; k += NT)
+        cc[k] = 0;
     __syncthreads();
-    for (uint64_t i = s + threadIdx.x; i < e; i += blockDim.x)
-        atomicAdd(&h[(uint32_t)(ent[i] >> sh) & (nd2 - 1)], 1u);
+    const uint32_t b = sbk;
+    const uint64_t *ob = off1 + (uint64_t)b * tiles;
+    const uint32_t *lb = loc1 + (uint64_t)b * tiles;
+    const uint64_t bs = ob[0], be = ob[tiles];
+    const uint64_t P0 = bs + (uint64_t)(g - cb[b]) * kDpChunk;
+    const uint32_t m = (uint32_t)((be - P0) < (uint64_t)kDpChunk ? (be - P0) : (uint64_t)kDpChunk);
+    const uint32_t ta = chunk_ta[g];
+    const uint32_t tb = (g + 1 < cb[b + 1]) ? chunk_ta[g + 1] : (uint32_t)(tiles - 1);
+    for (uint32_t i = threadIdx.x; i < m; i += NT)
+        buf[i] = kDpNoMark;
     __syncthreads();
-    block_scan_bins<PER, kDpSplitThreads>(h, h, nd2, wsum);
-    for (uint32_t k = threadIdx.x; k < nd2; k += blockDim.x)
-        pstart[((uint64_t)blockIdx.x << d2) + k] = (uint32_t)(s + h[k]);
-    if (blockIdx.x + 1 == (1u << d1) && threadIdx.x == 0)
-        pstart[(uint64_t)1 << (d1 + d2)] = (uint32_t)n;
-    for (uint64_t c0 = s; c0 < e; c0 += kDpChunk) {
-        const uint32_t m = (uint32_t)((e - c0) < (uint64_t)kDpChunk ? (e - c0) : (uint64_t)kDpChunk);
-        for (uint32_t k = threadIdx.x; k < nd2; k += blockDim.x)
-            cc[k] = 0;
-        __syncthreads();
-        uint64_t en[PER_T];
-        uint32_t rk[PER_T];
-#pragma unroll
-        for (int q = 0; q < PER_T; q++) {
-            const uint32_t l = q * kDpSplitThreads + threadIdx.x;
-            if (l < m) {
-                en[q] = ent[c0 + l];
-                rk[q] = atomicAdd(&cc[(uint32_t)(en[q] >> sh) & (nd2 - 1)], 1u);
-            }
-        }
-        __syncthreads();
-        block_scan_bins<PER, kDpSplitThreads>(cc, cl, nd2, wsum);
-#pragma unroll
-        for (int q = 0; q < PER_T; q++) {
-            const uint32_t l = q * kDpSplitThreads + threadIdx.x;
-            if (l < m)
-                stage[cl[(uint32_t)(en[q] >> sh) & (nd2 - 1)] + rk[q]] = en[q];
-        }
-        __syncthreads();
-        for (uint32_t j = threadIdx.x; j < m; j += blockDim.x) {
-            const uint64_t v = stage[j];
-            const uint32_t d = (uint32_t)(v >> sh) & (nd2 - 1);
-            ent2[s + h[d] + (j - cl[d])] = v;
-        }
-        __syncthreads();
-        for (uint32_t k = threadIdx.x; k < nd2; k += blockDim.x)
-            h[k] += cc[k];
-        __syncthreads();
+    for (uint32_t t = ta + threadIdx.x; t <= tb; t += NT) {
+        const uint64_t o = ob[t], o2 = ob[t + 1];
+        const uint64_t lo = o > P0 ? o : P0;
+        const uint64_t hi = o2 < P0 + m ? o2 : P0 + m;
+        if (lo < hi)
+            buf[lo - P0] = (int64_t)((uint64_t)t * kDpTile + lb[t]) - (int64_t)o;
     }
-}
-
-// d2 == 0: the d1 buckets are the partitions
-__global__ void dp_starts_kernel(const uint64_t *__restrict__ off, uint64_t n, int d1,
-                                 uint64_t tiles, uint32_t *__restrict__ pstart)
-{
-    const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
-    if (k < (1u << d1))
-        pstart[k] = (uint32_t)off[(uint64_t)k * tiles];
-    if (k == 0)
-        pstart[1u << d1] = (uint32_t)n;
+    __syncthreads();
+    // carry each mark over its run: thread owns positions [i0, i0 + PER8)
+    const uint32_t i0 = threadIdx.x * kDpSplitPer;
+    int64_t bv[kDpSplitPer];
+    int32_t lp = -1;
+#pragma unroll
+    for (int q = 0; q < kDpSplitPer; q++)
+        if (i0 + q < m && buf[i0 + q] != kDpNoMark)
+            lp = (int32_t)(i0 + q);
+    int32_t cur = block_max_excl(lp, wmax);
+#pragma unroll
+    for (int q = 0; q < kDpSplitPer; q++) {
+        bv[q] = 0;
+        if (i0 + q < m) {
+            if (buf[i0 + q] != kDpNoMark)
+                cur = (int32_t)(i0 + q);
+            bv[q] = buf[cur];  // position 0 is always marked (chunk_ta)
+        }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int q = 0; q < kDpSplitPer; q++)
+        if (i0 + q < m)
+            buf[i0 + q] = bv[q];
+    __syncthreads();
+    const int sh = 64 - d1 - d2;  // d2 digit = (entry >> sh) & (nd2 - 1)
+    uint64_t en[kDpSplitPer];
+    uint32_t rk[kDpSplitPer];
+#pragma unroll
+    for (int q = 0; q < kDpSplitPer; q++) {
+        const uint32_t l = q * NT + threadIdx.x;
+        if (l < m)
+            en[q] = ent1[(uint64_t)(buf[l] + (int64_t)(P0 + l))];
+    }
+#pragma unroll
+    for (int q = 0; q < kDpSplitPer; q++) {
+        const uint32_t l = q * NT + threadIdx.x;
+        if (l < m)
+            rk[q] = atomicAdd(&cc[(uint32_t)(en[q] >> sh) & (nd2 - 1)], 1u);
+    }
+    __syncthreads();
+    block_scan_bins<PER, NT>(cc, cl, nd2, wsum);
+    uint64_t *stage = reinterpret_cast<uint64_t *>(buf);
+#pragma unroll
+    for (int q = 0; q < kDpSplitPer; q++) {
+        const uint32_t l = q * NT + threadIdx.x;
+        if (l < m)
+            stage[cl[(uint32_t)(en[q] >> sh) & (nd2 - 1)] + rk[q]] = en[q];
+    }
+    __syncthreads();
+    for (uint32_t j = threadIdx.x; j < m; j += NT)
+        ent2[P0 + j] = stage[j];
+    for (uint32_t k = threadIdx.x; k < nd2; k += NT)
+        cdo[(uint64_t)g * nd2 + k] = (uint16_t)cl[k];
 }
 
 // Open-addressing tables (LDS or a partition's HBM region) hold one 64-bit
@@ -353,7 +502,7 @@ __device__ __forceinline__ uint32_t dp_insert(uint64_t *word, uint32_t size, uin
 // A record's ingest index for the class minimum (only multi-member classes
 // read it).  GM_ROW: the 32-byte exchange rows carry it at byte 24, on the
 // line the confirmation just read.  GM_REP: from the record's own rep_out
-// slot (dp_keys wrote gidx[r] there): the line its final store lands on,
+// slot (dp_tile wrote gidx[r] there): the line its final store lands on,
 // instead of a third array.  GM_INDEX: no gidx, the record index itself.
 enum { GM_INDEX = 0, GM_REP = 1, GM_ROW = 2 };
 
@@ -364,6 +513,58 @@ __device__ __forceinline__ uint64_t gidx_of(const uint64_t *rep, const uint8_t *
         return *reinterpret_cast<const uint64_t *>(sig + (uint64_t)r * stride + 24);
     return gmode == GM_REP ? rep[r] : (uint64_t)r;
 }
+
+// The partition's entries, gathered from its run in each chunk of its
+// bucket, in batches of up to kDpRuns runs: rpos[k] = partition-local index
+// of run k's first entry, rsrc[k] = ent2 index of local index 0 along run k.
+struct DpRuns {
+    const uint16_t *cdo;
+    uint64_t bs, bsize;
+    uint32_t c0, nch, nd2, d;
+    __device__ void run(uint32_t k, uint32_t &s, uint32_t &len) const
+    {
+        const uint16_t *c = cdo + (uint64_t)(c0 + k) * nd2;
+        s = c[d];
+        const uint64_t rem = bsize - (uint64_t)k * kDpChunk;
+        const uint32_t e = d + 1 < nd2 ? c[d + 1] : (uint32_t)(rem < (uint64_t)kDpChunk ? rem : (uint64_t)kDpChunk);
+        len = e - s;
+    }
+};
+
+// Build batch [kb, kb + kDpRuns) starting at local index l0: one scan of
+// {s << 32 | len} gives the run positions (low half) and the batch's sums of
+// run lengths and of run starts (the entries of the bucket with a smaller
+// digit, for the partition's virtual start).  Ends with a barrier.
+__device__ __forceinline__ uint64_t dp_batch(const DpRuns &R, uint32_t kb, uint32_t l0, uint32_t *rpos,
+                                             uint64_t *rsrc, uint64_t *wsum)
+{
+    const uint32_t k = kb + threadIdx.x;
+    uint32_t s = 0, len = 0;
+    if (k < R.nch)
+        R.run(k, s, len);
+    uint64_t tot;
+    const uint64_t ex = block_exclusive_scan64((uint64_t)s << 32 | len, wsum, tot);
+    const uint32_t pos = l0 + (uint32_t)ex;
+    rpos[threadIdx.x] = pos;
+    rsrc[threadIdx.x] = R.bs + (uint64_t)k * kDpChunk + s - pos;
+    __syncthreads();
+    return tot;
+}
+
+// ent2 index of local index l: the last run of the batch starting at or before it.
+__device__ __forceinline__ uint64_t dp_src(uint32_t l, uint32_t nk, const uint32_t *rpos, const uint64_t *rsrc)
+{
+    uint32_t lo = 0, hi = nk;
+    while (hi - lo > 1) {
+        const uint32_t mid = (lo + hi) >> 1;
+        if (rpos[mid] <= l)
+            lo = mid;
+        else
+            hi = mid;
+    }
+    return rsrc[lo] + l;
+}
+
 // Only records of classes with more than one member are written (random
 // stores); K1 already wrote every record's singleton answer.  The class
 // minimum needs ingest indices only there: every member that joined a
@@ -371,124 +572,265 @@ __device__ __forceinline__ uint64_t gidx_of(const uint64_t *rep, const uint8_t *
 // members gets all k indices and a singleton reads none.
 constexpr int kDpEpt = (kDpCap + kDpGroupThreads - 1) / kDpGroupThreads;  // entries per thread
 
-__global__ __launch_bounds__(kDpGroupThreads) __attribute__((amdgpu_waves_per_eu(8))) void dp_group_kernel(
-    const uint64_t *__restrict__ ent, const uint32_t *__restrict__ pstart,
-    const uint8_t *__restrict__ sig, uint32_t stride, int gmode, uint64_t *__restrict__ gword, uint64_t *__restrict__ gmin,
-    uint32_t *__restrict__ gcnt, uint32_t *__restrict__ gslot, uint64_t *__restrict__ rep_out,
-    uint32_t *__restrict__ ref_out)
+struct DpLds {  // dp_group_kernel's LDS table (80 KB: two workgroups per CU)
+    uint64_t word[kDpSlots];
+    uint64_t mn[kDpSlots];
+    uint32_t cn[kDpSlots];
+};
+
+struct DpArgs {
+    const uint64_t *ent2;
+    const uint8_t *sig;
+    uint32_t stride;
+    int gmode;
+    uint64_t *gword, *gmin;
+    uint32_t *gcnt, *gslot;
+    uint64_t *rep_out;
+    uint32_t *ref_out;
+};
+
+// The LDS grouping of one partition whose entries are in registers (the
+// round-1 code path).  Ends with a barrier.
+// probe: measurement build only (make probes), FDFS_GPU_DEDUP_PROBE bit 0 =
+// no confirmation reads (every equal key taken as equal), bit 1 = no final
+// stores; results are wrong under either
+template <int PROBE, int GM>
+__device__ __forceinline__ void dp_group_lds(DpLds &L, const DpArgs &A, const uint64_t (&en)[kDpEpt], uint32_t cnt)
 {
-    __shared__ uint64_t word[kDpSlots];
-    __shared__ uint64_t mn[kDpSlots];
-    __shared__ uint32_t cn[kDpSlots];
-    const uint32_t s = pstart[blockIdx.x], e = pstart[blockIdx.x + 1];
-    const uint32_t cnt = e - s;
+    for (int k = threadIdx.x; k < kDpSlots; k += blockDim.x) {
+        L.word[k] = kDpEmpty;
+        L.mn[k] = kDpEmpty;
+        L.cn[k] = 0;
+    }
+    __syncthreads();
+    // (1) key-only probes: LDS only
+    uint32_t slot[kDpEpt], own[kDpEpt];
+#pragma unroll
+    for (int k = 0; k < kDpEpt; k++) {
+        const uint32_t l = threadIdx.x + k * kDpGroupThreads;
+        own[k] = (uint32_t)en[k];
+        if (l < cnt) {
+            const uint32_t key = (uint32_t)(en[k] >> 32);
+            slot[k] = dp_probe<true>(L.word, kDpSlots, key, (uint32_t)en[k], dp_home(key, kDpSlots, true), own[k]);
+        }
+    }
+    // (2) confirmations of every joined entry issued together: both
+    // signature rows and both ingest indices per entry
+    uint64_t ra[kDpEpt], rb[kDpEpt], rc[kDpEpt], oa[kDpEpt], ob[kDpEpt], oc[kDpEpt];
+    uint64_t gr[kDpEpt], go[kDpEpt];
+#pragma unroll
+    for (int k = 0; k < kDpEpt; k++) {
+        const uint32_t r = (uint32_t)en[k];
+        if constexpr (PROBE & 1) {
+            ra[k] = rb[k] = rc[k] = oa[k] = ob[k] = oc[k] = 0;
+            gr[k] = r;
+            go[k] = own[k];
+        } else if (own[k] != r) {
+            load_sig(A.sig + (uint64_t)r * A.stride, ra[k], rb[k], rc[k]);
+            load_sig(A.sig + (uint64_t)own[k] * A.stride, oa[k], ob[k], oc[k]);
+            gr[k] = gidx_of(A.rep_out, A.sig, A.stride, GM, r);
+            go[k] = gidx_of(A.rep_out, A.sig, A.stride, GM, own[k]);
+        }
+    }
+#pragma unroll
+    for (int k = 0; k < kDpEpt; k++) {
+        const uint32_t l = threadIdx.x + k * kDpGroupThreads;
+        if (l < cnt) {
+            const uint32_t r = (uint32_t)en[k];
+            if (own[k] != r && !(ra[k] == oa[k] && rb[k] == ob[k] && rc[k] == oc[k])) {
+                // 32-bit key collision with a different signature: walk on
+                slot[k] = dp_insert<true>(L.word, kDpSlots, (uint32_t)(en[k] >> 32), r, dp_next(slot[k], kDpSlots, true),
+                                          A.sig, A.stride, own[k]);
+                if (own[k] != r)
+                    go[k] = gidx_of(A.rep_out, A.sig, A.stride, GM, own[k]);
+            }
+            atomicAdd(&L.cn[slot[k]], 1u);
+            if (own[k] != r)
+                atomicMin(reinterpret_cast<unsigned long long *>(&L.mn[slot[k]]),
+                          (unsigned long long)(gr[k] < go[k] ? gr[k] : go[k]));
+        }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < kDpEpt; k++) {
+        const uint32_t l = threadIdx.x + k * kDpGroupThreads;
+        if (l < cnt) {
+            const uint32_t c = L.cn[slot[k]];
+            if (c > 1 && !(PROBE & 2)) {
+                const uint32_t r = (uint32_t)en[k];
+                const uint64_t m = L.mn[slot[k]];
+                if (GM != GM_INDEX || m != r)  // the class's first record keeps dp_tile's rep = r
+                    A.rep_out[r] = m;
+                A.ref_out[r] = c;
+            }
+        }
+    }
+    __syncthreads();
+}
+
+// A partition the pipeline did not gather: a bucket of more than kDpRuns
+// chunks (its runs come in batches), or more records than the LDS table
+// holds (grouped on a table in its own HBM region, 2 * cnt slots at
+// 2 * its virtual start).  Ends with a barrier.
+__device__ __forceinline__ void dp_group_slow(DpLds &L, uint32_t *rpos, uint64_t *rsrc, uint64_t *wsum,
+                                              const DpArgs &A, const DpRuns &R)
+{
+    uint32_t cnt = 0, below = 0;
+    for (uint32_t kb = 0; kb < R.nch; kb += kDpRuns) {
+        uint32_t s = 0, len = 0;
+        if (kb + threadIdx.x < R.nch)
+            R.run(kb + threadIdx.x, s, len);
+        uint64_t t2;
+        block_exclusive_scan64((uint64_t)s << 32 | len, wsum, t2);
+        cnt += (uint32_t)t2;
+        below += (uint32_t)(t2 >> 32);
+    }
     if (cnt == 0)
         return;
     if (cnt <= kDpCap) {
-        // all of this thread's entries in flight at once
         uint64_t en[kDpEpt];
 #pragma unroll
-        for (int k = 0; k < kDpEpt; k++) {
-            const uint32_t l = threadIdx.x + k * kDpGroupThreads;
-            en[k] = l < cnt ? ent[s + l] : 0ull;
-        }
-        for (int k = threadIdx.x; k < kDpSlots; k += blockDim.x) {
-            word[k] = kDpEmpty;
-            mn[k] = kDpEmpty;
-            cn[k] = 0;
-        }
-        __syncthreads();
-        // (1) key-only probes: LDS only
-        uint32_t slot[kDpEpt], own[kDpEpt];
+        for (int k = 0; k < kDpEpt; k++)
+            en[k] = 0;
+        for (uint32_t kb = 0, l0 = 0; kb < R.nch; kb += kDpRuns) {
+            const uint32_t nk = (R.nch - kb) < (uint32_t)kDpRuns ? (R.nch - kb) : (uint32_t)kDpRuns;
+            const uint32_t l1 = l0 + (uint32_t)dp_batch(R, kb, l0, rpos, rsrc, wsum);
 #pragma unroll
-        for (int k = 0; k < kDpEpt; k++) {
-            const uint32_t l = threadIdx.x + k * kDpGroupThreads;
-            own[k] = (uint32_t)en[k];
-            if (l < cnt) {
-                const uint32_t key = (uint32_t)(en[k] >> 32);
-                slot[k] = dp_probe<true>(word, kDpSlots, key, (uint32_t)en[k], dp_home(key, kDpSlots, true),
-                                         own[k]);
+            for (int k = 0; k < kDpEpt; k++) {
+                const uint32_t l = threadIdx.x + k * kDpGroupThreads;
+                if (l >= l0 && l < l1)
+                    en[k] = A.ent2[dp_src(l, nk, rpos, rsrc)];
             }
+            __syncthreads();
+            l0 = l1;
         }
-        // (2) confirmations of every joined entry issued together: both
-        // signature rows and both ingest indices per entry
-        uint64_t ra[kDpEpt], rb[kDpEpt], rc[kDpEpt], oa[kDpEpt], ob[kDpEpt], oc[kDpEpt];
-        uint64_t gr[kDpEpt], go[kDpEpt];
-#pragma unroll
-        for (int k = 0; k < kDpEpt; k++) {
-            const uint32_t r = (uint32_t)en[k];
-            if (own[k] != r) {
-                load_sig(sig + (uint64_t)r * stride, ra[k], rb[k], rc[k]);
-                load_sig(sig + (uint64_t)own[k] * stride, oa[k], ob[k], oc[k]);
-                gr[k] = gidx_of(rep_out, sig, stride, gmode, r);
-                go[k] = gidx_of(rep_out, sig, stride, gmode, own[k]);
-            }
-        }
-#pragma unroll
-        for (int k = 0; k < kDpEpt; k++) {
-            const uint32_t l = threadIdx.x + k * kDpGroupThreads;
-            if (l < cnt) {
-                const uint32_t r = (uint32_t)en[k];
-                if (own[k] != r && !(ra[k] == oa[k] && rb[k] == ob[k] && rc[k] == oc[k])) {
-                    // 32-bit key collision with a different signature: walk on
-                    slot[k] = dp_insert<true>(word, kDpSlots, (uint32_t)(en[k] >> 32), r,
-                                              dp_next(slot[k], kDpSlots, true), sig, stride, own[k]);
-                    if (own[k] != r)
-                        go[k] = gidx_of(rep_out, sig, stride, gmode, own[k]);
-                }
-                atomicAdd(&cn[slot[k]], 1u);
-                if (own[k] != r)
-                    atomicMin(reinterpret_cast<unsigned long long *>(&mn[slot[k]]),
-                              (unsigned long long)(gr[k] < go[k] ? gr[k] : go[k]));
-            }
-        }
-        __syncthreads();
-#pragma unroll
-        for (int k = 0; k < kDpEpt; k++) {
-            const uint32_t l = threadIdx.x + k * kDpGroupThreads;
-            if (l < cnt) {
-                const uint32_t c = cn[slot[k]];
-                if (c > 1) {
-                    const uint32_t r = (uint32_t)en[k];
-                    rep_out[r] = mn[slot[k]];
-                    ref_out[r] = c;
-                }
-            }
-        }
+        if (A.gmode == GM_ROW)
+            dp_group_lds<0, GM_ROW>(L, A, en, cnt);
+        else if (A.gmode == GM_REP)
+            dp_group_lds<0, GM_REP>(L, A, en, cnt);
+        else
+            dp_group_lds<0, GM_INDEX>(L, A, en, cnt);
         return;
     }
-    // oversized partition: the same grouping on this partition's own HBM
-    // region (2 * cnt slots at 2 * s)
+    const uint64_t vs = R.bs + below;
     const uint32_t size = 2 * cnt;
-    uint64_t *w = gword + 2ull * s;
-    uint64_t *m = gmin + 2ull * s;
-    uint32_t *c = gcnt + 2ull * s;
+    uint64_t *w = A.gword + 2ull * vs;
+    uint64_t *m = A.gmin + 2ull * vs;
+    uint32_t *c = A.gcnt + 2ull * vs;
     for (uint32_t k = threadIdx.x; k < size; k += blockDim.x) {
         w[k] = kDpEmpty;
         m[k] = kDpEmpty;
         c[k] = 0;
     }
     __syncthreads();
-    for (uint32_t l = threadIdx.x; l < cnt; l += blockDim.x) {
-        const uint64_t en = ent[s + l];
-        const uint32_t r = (uint32_t)en, key = (uint32_t)(en >> 32);
-        uint32_t o;
-        const uint32_t slot = dp_insert<false>(w, size, key, r, dp_home(key, size, false), sig, stride, o);
-        atomicAdd(&c[slot], 1u);
-        if (o != r) {
-            const uint64_t a = gidx_of(rep_out, sig, stride, gmode, r), b = gidx_of(rep_out, sig, stride, gmode, o);
-            atomicMin(reinterpret_cast<unsigned long long *>(&m[slot]), (unsigned long long)(a < b ? a : b));
+    for (uint32_t kb = 0, l0 = 0; kb < R.nch; kb += kDpRuns) {
+        const uint32_t nk = (R.nch - kb) < (uint32_t)kDpRuns ? (R.nch - kb) : (uint32_t)kDpRuns;
+        const uint32_t l1 = l0 + (uint32_t)dp_batch(R, kb, l0, rpos, rsrc, wsum);
+        for (uint32_t l = l0 + threadIdx.x; l < l1; l += blockDim.x) {
+            const uint64_t en = A.ent2[dp_src(l, nk, rpos, rsrc)];
+            const uint32_t r = (uint32_t)en, key = (uint32_t)(en >> 32);
+            uint32_t o;
+            const uint32_t slot = dp_insert<false>(w, size, key, r, dp_home(key, size, false), A.sig, A.stride, o);
+            atomicAdd(&c[slot], 1u);
+            if (o != r) {
+                const uint64_t a = gidx_of(A.rep_out, A.sig, A.stride, A.gmode, r);
+                const uint64_t b2 = gidx_of(A.rep_out, A.sig, A.stride, A.gmode, o);
+                atomicMin(reinterpret_cast<unsigned long long *>(&m[slot]), (unsigned long long)(a < b2 ? a : b2));
+            }
+            A.gslot[vs + l] = slot;
         }
-        gslot[s + l] = slot;
+        __syncthreads();
+        l0 = l1;
     }
+    __threadfence_block();
     __syncthreads();
-    for (uint32_t l = threadIdx.x; l < cnt; l += blockDim.x) {
-        const uint32_t slot = gslot[s + l];
-        if (c[slot] > 1) {
-            const uint32_t r = (uint32_t)ent[s + l];
-            rep_out[r] = m[slot];
-            ref_out[r] = c[slot];
+    for (uint32_t kb = 0, l0 = 0; kb < R.nch; kb += kDpRuns) {
+        const uint32_t nk = (R.nch - kb) < (uint32_t)kDpRuns ? (R.nch - kb) : (uint32_t)kDpRuns;
+        const uint32_t l1 = l0 + (uint32_t)dp_batch(R, kb, l0, rpos, rsrc, wsum);
+        for (uint32_t l = l0 + threadIdx.x; l < l1; l += blockDim.x) {
+            const uint32_t slot = A.gslot[vs + l];
+            if (c[slot] > 1) {
+                const uint32_t r = (uint32_t)A.ent2[dp_src(l, nk, rpos, rsrc)];
+                A.rep_out[r] = m[slot];
+                A.ref_out[r] = c[slot];
+            }
         }
+        __syncthreads();
+        l0 = l1;
+    }
+}
+
+// K5: one workgroup per partition.  The run table (rpos, rsrc) and the scan
+// partials live in the table's mn array until the table is initialised.  A
+// partition of a bucket with more than kDpRuns chunks (its runs come in
+// batches) or of more than kDpCap records (the HBM table) is listed for
+// dp_group_slow_kernel instead.
+static_assert(kDpRuns == kDpGroupThreads, "one run per thread in a batch");
+
+__device__ __forceinline__ void dp_runs_of(uint32_t q, int d2, uint64_t tiles, const uint64_t *off1,
+                                           const uint32_t *cb, const uint16_t *cdo, DpRuns &R)
+{
+    R.nd2 = 1u << d2;
+    R.d = q & (R.nd2 - 1);
+    const uint32_t b = q >> d2;
+    R.cdo = cdo;
+    R.c0 = cb[b];
+    R.nch = cb[b + 1] - R.c0;
+    R.bs = off1[(uint64_t)b * tiles];
+    R.bsize = off1[(uint64_t)(b + 1) * tiles] - R.bs;
+}
+
+template <int PROBE, int GM>
+__global__ __launch_bounds__(kDpGroupThreads) __attribute__((amdgpu_waves_per_eu(8))) void dp_group_kernel(
+    const uint64_t *__restrict__ ent2, int d2, uint64_t tiles, const uint64_t *__restrict__ off1,
+    const uint32_t *__restrict__ cb, const uint16_t *__restrict__ cdo, const uint8_t *__restrict__ sig,
+    uint32_t stride, uint64_t *__restrict__ rep_out, uint32_t *__restrict__ ref_out, uint32_t *__restrict__ slow)
+{
+    __shared__ DpLds L;
+    uint32_t *rpos = reinterpret_cast<uint32_t *>(L.mn);
+    uint64_t *rsrc = L.mn + kDpRuns / 2;
+    uint64_t *wsum = L.mn + kDpRuns / 2 + kDpRuns;
+    static_assert(kDpRuns / 2 + kDpRuns + kDpGroupThreads / 64 <= kDpSlots, "gather tables fit in mn");
+    DpRuns R;
+    dp_runs_of(blockIdx.x, d2, tiles, off1, cb, cdo, R);
+    const uint32_t cnt = R.nch > (uint32_t)kDpRuns ? ~0u : (uint32_t)dp_batch(R, 0, 0, rpos, rsrc, wsum);
+    if (cnt == 0)
+        return;
+    if (cnt > kDpCap) {
+        if (threadIdx.x == 0)
+            slow[1 + atomicAdd(slow, 1u)] = blockIdx.x;
+        return;
+    }
+    uint64_t en[kDpEpt];
+#pragma unroll
+    for (int k = 0; k < kDpEpt; k++) {
+        const uint32_t l = threadIdx.x + k * kDpGroupThreads;
+        en[k] = l < cnt ? ent2[dp_src(l, R.nch, rpos, rsrc)] : 0ull;
+    }
+    __syncthreads();  // run table reads done before the table init
+    const DpArgs A{ent2, sig, stride, GM, nullptr, nullptr, nullptr, nullptr, rep_out, ref_out};
+    dp_group_lds<PROBE, GM>(L, A, en, cnt);
+}
+
+// The listed partitions (slow[0] of them), a few persistent workgroups.
+__global__ __launch_bounds__(kDpGroupThreads) void dp_group_slow_kernel(
+    const uint64_t *__restrict__ ent2, int d2, uint64_t tiles, const uint64_t *__restrict__ off1,
+    const uint32_t *__restrict__ cb, const uint16_t *__restrict__ cdo, const uint8_t *__restrict__ sig,
+    uint32_t stride, int gmode, uint64_t *__restrict__ gword, uint64_t *__restrict__ gmin,
+    uint32_t *__restrict__ gcnt, uint32_t *__restrict__ gslot, uint64_t *__restrict__ rep_out,
+    uint32_t *__restrict__ ref_out, const uint32_t *__restrict__ slow)
+{
+    __shared__ DpLds L;
+    uint32_t *rpos = reinterpret_cast<uint32_t *>(L.mn);
+    uint64_t *rsrc = L.mn + kDpRuns / 2;
+    uint64_t *wsum = L.mn + kDpRuns / 2 + kDpRuns;
+    const DpArgs A{ent2, sig, stride, gmode, gword, gmin, gcnt, gslot, rep_out, ref_out};
+    const uint32_t ns = slow[0];
+    for (uint32_t i = blockIdx.x; i < ns; i += gridDim.x) {
+        DpRuns R;
+        dp_runs_of(slow[1 + i], d2, tiles, off1, cb, cdo, R);
+        dp_group_slow(L, rpos, rsrc, wsum, A, R);
+        __syncthreads();
     }
 }
 
@@ -498,10 +840,10 @@ static inline uint64_t al(uint64_t x) { return (x + 255) & ~255ull; }
 uint64_t dedup_ws_bytes(uint64_t n)
 {
     const DpPlan pl = dp_plan(n);
-    const uint64_t ncnt = (1ull << pl.d1) * pl.tiles;
-    return al(4 * n) + al(8 * n) + al(8 * (ncnt + 1)) + al(8 * (ncnt + 1)) +
-           al(8 * scan_workspace_elems(ncnt)) + al(8 * n) + al(8 * n) + al(4 * (pl.nparts() + 1)) +
-           al(16 * n) + al(16 * n);
+    const uint64_t ncnt = pl.ncnt();
+    return al(8 * n) + al(8 * n) + al(8 * (ncnt + 1)) + al(8 * (ncnt + 1)) + al(8 * scan_workspace_elems(ncnt)) +
+           al(4 * ncnt) + al(4 * ((1ull << pl.d1) + 1)) + al(4 * pl.chunks) + al((2 * pl.chunks) << pl.d2) +
+           al(16 * n) + al(16 * n) + al(8 * n) + al(4 * (pl.nparts() + 1));
 }
 
 static unsigned grid_for(uint64_t n, unsigned block)
@@ -519,60 +861,74 @@ hipError_t launch_dedup_group(const uint8_t *sig, uint32_t sig_stride, const uin
     if (n == 0)
         return hipSuccess;
     const DpPlan pl = dp_plan(n);
-    const uint64_t ncnt = (1ull << pl.d1) * pl.tiles;
+    const uint64_t ncnt = pl.ncnt();
     char *p = static_cast<char *>(ws);
     auto take = [&](uint64_t bytes) {
         char *q = p;
         p += al(bytes);
         return q;
     };
-    uint32_t *keys = reinterpret_cast<uint32_t *>(take(4 * n));
-    uint64_t *counts = reinterpret_cast<uint64_t *>(take(8 * (ncnt + 1)));
-    uint64_t *off = reinterpret_cast<uint64_t *>(take(8 * (ncnt + 1)));
-    uint64_t *bsum = reinterpret_cast<uint64_t *>(take(8 * scan_workspace_elems(ncnt)));
-    uint64_t *ent = reinterpret_cast<uint64_t *>(take(8 * n));
+    uint64_t *ent1 = reinterpret_cast<uint64_t *>(take(8 * n));
     uint64_t *ent2 = reinterpret_cast<uint64_t *>(take(8 * n));
-    uint32_t *pstart = reinterpret_cast<uint32_t *>(take(4 * (pl.nparts() + 1)));
+    uint64_t *cnt1 = reinterpret_cast<uint64_t *>(take(8 * (ncnt + 1)));
+    uint64_t *off1 = reinterpret_cast<uint64_t *>(take(8 * (ncnt + 1)));
+    uint64_t *bsum = reinterpret_cast<uint64_t *>(take(8 * scan_workspace_elems(ncnt)));
+    uint32_t *loc1 = reinterpret_cast<uint32_t *>(take(4 * ncnt));
+    uint32_t *cb = reinterpret_cast<uint32_t *>(take(4 * ((1ull << pl.d1) + 1)));
+    uint32_t *chunk_ta = reinterpret_cast<uint32_t *>(take(4 * pl.chunks));
+    uint16_t *cdo = reinterpret_cast<uint16_t *>(take((2 * pl.chunks) << pl.d2));
     uint64_t *gword = reinterpret_cast<uint64_t *>(take(16 * n));  // oversized-partition tables
     uint64_t *gmin = reinterpret_cast<uint64_t *>(take(16 * n));
     uint32_t *gcnt = reinterpret_cast<uint32_t *>(take(8 * n));
-    uint32_t *gslot = keys;  // keys are dead after K3
+    uint32_t *slow = reinterpret_cast<uint32_t *>(take(4 * (pl.nparts() + 1)));  // count, partitions
+    uint32_t *gslot = reinterpret_cast<uint32_t *>(ent1);  // ent1 is dead after dp_split
     hipError_t e;
     if (ev0)
         (void)hipEventRecord(ev0, st);
-    dp_keys_kernel<<<(unsigned)pl.tiles, kDpTileThreads, 0, st>>>(sig, sig_stride, gidx, gidx_stride, n,
-                                                                  pl.d1, pl.tiles, keys, rep_out, ref_out,
-                                                                  counts);
-    if ((e = launch_exclusive_scan(counts, ncnt, off, bsum, st)) != hipSuccess)
+    dp_tile_kernel<<<(unsigned)pl.tiles, kDpTileThreads, 0, st>>>(sig, sig_stride, gidx, gidx_stride, n, pl.d1,
+                                                                  pl.tiles, ent1, rep_out, ref_out, cnt1, loc1);
+    if ((e = launch_exclusive_scan(cnt1, ncnt, off1, bsum, st)) != hipSuccess)
         return e;
-    dp_scatter_kernel<<<(unsigned)pl.tiles, kDpTileThreads, 0, st>>>(keys, n, pl.d1, pl.tiles, off, ent);
-    const uint64_t *parts = ent;
-    if (pl.d2) {
-#ifdef FDFS_PROBES
-        static int per = -1;
-        if (per < 0) {  // A/B (make probes): FDFS_GPU_DEDUP_SPLIT=4 -> 4096-entry chunks
-            const char *ev = getenv("FDFS_GPU_DEDUP_SPLIT");
-            per = (ev && atoi(ev) == 4) ? 4 : kDpSplitPer;
-        }
-#else
-        constexpr int per = kDpSplitPer;
-#endif
-        if (per == 4)
-            dp_split_kernel<4><<<1u << pl.d1, kDpSplitThreads, 0, st>>>(ent, n, pl.d1, pl.d2, pl.tiles, off,
-                                                                     ent2, pstart);
-        else
-            dp_split_kernel<kDpSplitPer><<<1u << pl.d1, kDpSplitThreads, 0, st>>>(ent, n, pl.d1, pl.d2, pl.tiles,
-                                                                               off, ent2, pstart);
-        parts = ent2;
-    } else {
-        dp_starts_kernel<<<((1u << pl.d1) + 255) / 256, 256, 0, st>>>(off, n, pl.d1, pl.tiles, pstart);
-    }
+    dp_chunks_kernel<<<1, 256, 0, st>>>(off1, pl.d1, pl.tiles, cb, slow);
+    dp_chunk_ta_kernel<<<grid_for(ncnt, 256), 256, 0, st>>>(off1, pl.tiles, ncnt, cb, chunk_ta);
+    if (pl.d2 <= 10)
+        dp_split_kernel<1024><<<(unsigned)pl.chunks, kDpSplitThreads, 0, st>>>(ent1, pl.d1, pl.d2, pl.tiles, off1,
+                                                                              loc1, cb, chunk_ta, ent2, cdo);
+    else
+        dp_split_kernel<1 << kDpMaxD2><<<(unsigned)pl.chunks, kDpSplitThreads, 0, st>>>(
+            ent1, pl.d1, pl.d2, pl.tiles, off1, loc1, cb, chunk_ta, ent2, cdo);
     const int gmode = !gidx_stride ? GM_INDEX
                       : (gidx == reinterpret_cast<const uint64_t *>(sig + 24) && 8 * gidx_stride == sig_stride)
                           ? GM_ROW
                           : GM_REP;
-    dp_group_kernel<<<(unsigned)pl.nparts(), kDpGroupThreads, 0, st>>>(
-        parts, pstart, sig, sig_stride, gmode, gword, gmin, gcnt, gslot, rep_out, ref_out);
+#define DP_GROUP(P, G)                                                                                       \
+    dp_group_kernel<P, G><<<(unsigned)pl.nparts(), kDpGroupThreads, 0, st>>>(ent2, pl.d2, pl.tiles, off1, cb, cdo, \
+                                                                           sig, sig_stride, rep_out, ref_out, slow)
+#ifdef FDFS_PROBES
+    // measurement build only (make probes): FDFS_GPU_DEDUP_PROBE bit 0 = no
+    // confirmation reads, bit 1 = no final stores (wrong results)
+    static int probe = -1;
+    if (probe < 0) {
+        const char *ev = getenv("FDFS_GPU_DEDUP_PROBE");
+        probe = ev ? atoi(ev) : 0;
+    }
+    if (probe == 1 && gmode == GM_INDEX)
+        DP_GROUP(1, GM_INDEX);
+    else if (probe == 2 && gmode == GM_INDEX)
+        DP_GROUP(2, GM_INDEX);
+    else if (probe == 3 && gmode == GM_INDEX)
+        DP_GROUP(3, GM_INDEX);
+    else
+#endif
+    if (gmode == GM_ROW)
+        DP_GROUP(0, GM_ROW);
+    else if (gmode == GM_REP)
+        DP_GROUP(0, GM_REP);
+    else
+        DP_GROUP(0, GM_INDEX);
+#undef DP_GROUP
+    dp_group_slow_kernel<<<256, kDpGroupThreads, 0, st>>>(ent2, pl.d2, pl.tiles, off1, cb, cdo, sig, sig_stride, gmode,
+                                                          gword, gmin, gcnt, gslot, rep_out, ref_out, slow);
     if (ev1)
         (void)hipEventRecord(ev1, st);
     return hipGetLastError();

@@ -18,7 +18,7 @@ BENCH_KERNEL = {"c2": ("sig_hash_kernel<true, 0, 0>", "sig_hash_kernel<SAR>"),
                 "c4": ("crc_seg_kernel<true, 2>", "crc_seg_kernel<SAR,2>")}
 
 
-BENCH_C5_KERNEL = "dedup_group (dp_keys + scan + dp_scatter + dp_split + dp_group)"
+BENCH_C5_KERNEL = "dedup_group (dp_tile + scan + chunks + dp_split + dp_group)"
 
 
 def short(name):
@@ -54,7 +54,7 @@ def main(src, dst):
                         if "fdfs::" in k:
                             out.write(f"{short(k)} {json.dumps(v)}\n")
                 for k, v in d.items():
-                    if any(x in k for x in ("dp_keys", "dp_scatter", "dp_split", "dp_group", "dp_starts",
+                    if any(x in k for x in ("dp_tile", "dp_chunk", "dp_split", "dp_group",
                                             "scan_reduce", "scan_sums", "scan_apply")):
                         for m, val in v.items():
                             tot[m] = tot.get(m, 0.0) + val

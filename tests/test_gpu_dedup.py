@@ -45,8 +45,10 @@ def test_dedup_with_gidx(oracle, ctx):
     assert np.array_equal(ref.cpu().numpy(), oref.astype(np.int32))
 
 
-def test_all_identical(ctx):
-    n = 1 << 20
+@pytest.mark.parametrize("n", [1 << 20, 9_000_000])
+def test_all_identical(ctx, n):
+    """One class: one bucket, one partition over the LDS capacity (the HBM
+    table); at 9M the bucket has more chunks than one gather batch holds."""
     sig = torch.zeros((n, 24), dtype=torch.uint8, device="cuda")
     rep, ref = ctx.dedup(sig)
     assert int(rep.max()) == 0 and int(ref.min()) == n
@@ -132,10 +134,10 @@ def _colliding(count, seed):
     return out
 
 
-@pytest.mark.parametrize("ncoll,reps", [(40, 3), (700, 2), (2500, 1)])
+@pytest.mark.parametrize("ncoll,reps", [(40, 3), (700, 2), (3500, 1)])
 def test_dedup_full_hash_collisions(oracle, ctx, ncoll, reps):
     """Distinct signatures sharing the whole 64-bit key (one partition, one
-    probe chain) stay distinct classes; with 2500 of them the partition is
+    probe chain) stay distinct classes; with 3500 of them the partition is
     over the LDS capacity and takes the HBM-table path."""
     coll = _colliding(ncoll, ncoll)
     bg = _sigs(30_000, 20_000, 77)

@@ -197,10 +197,10 @@ def test_md5_staged_multiwave(oracle, ctxs):
 
 
 def test_md5_many_chunks(oracle, ctxs):
-    """More 64-file chunks than the MD5 kernel keeps wave pairs resident
-    (150K files = 2344 chunks > 2 x 4 pairs x 256 CUs), so pairs walk a chunk
-    sequence and their LDS handover counters run across chunks; two
-    misaligned files put lane-serial chunks inside those sequences."""
+    """Many more 64-file chunks than the MD5 kernel has queue waves (150K
+    files = 2344 chunks > 4 waves x 256 CUs), so waves take chunk after chunk
+    from the device queue counter; two misaligned files put byte-offset
+    staged loads inside that sequence."""
     rng = np.random.default_rng(32)
     sizes = rng.integers(0, 2600, 150_000)
     buf, offs, sz = _packed(sizes, 16, rng, slack=64)
