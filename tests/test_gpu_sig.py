@@ -48,7 +48,10 @@ def _check(oracle, ctx, variant, buf, offs, sizes, methods=METHODS, dev_batch=No
         assert bad.size == 0, (m, variant, bad[:10], sizes[bad[:10]])
         if m:
             badsig = np.nonzero(np.any(sig != osig, axis=1))[0]
-            assert badsig.size == 0, (m, variant, badsig[:10], sizes[badsig[:10]])
+            # which 4-byte fields differ: size hi/lo, then crc/elf/simple/time33 (HASH)
+            fields = [int(np.any(sig[:, 4 * k:4 * k + 4] != osig[:, 4 * k:4 * k + 4], axis=1).sum())
+                      for k in range(6)]
+            assert badsig.size == 0, (m, variant, badsig[:10], sizes[badsig[:10]], fields)
 
 
 def _packed(sizes, align, rng, slack=0):
