@@ -208,6 +208,26 @@ __device__ __forceinline__ void elf_word4(uint32_t w, uint32_t &e)
 #undef ELF_STEP
 #undef ELF_LAST
 
+// The same word of ELF steps in plain C, for waves bound by ELF's dependent
+// chain rather than by issue: hipcc emits v_lshl_add_u32 (shift + byte add in
+// one op), v_ashrrev / v_lshrrev and v_bitop3 -- three ops on the chain per
+// byte instead of four -- and extracts the bytes (v_and / v_bfe / v_lshr)
+// off the chain, where they fill its latency gaps.
+template <bool SAR, bool LAST>
+__device__ __forceinline__ void elf_word4_chain(uint32_t w, uint32_t &e)
+{
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+        const uint32_t t = (e << 4) + ((w >> (8 * k)) & 0xFFu);
+        if (LAST && k == 3) {
+            const uint32_t x = t & 0xF0000000u;
+            e = (t ^ (SAR ? (uint32_t)((int32_t)x >> 24) : (x >> 24))) & ~x;
+        } else {
+            e = t ^ ((SAR ? (uint32_t)((int32_t)t >> 24) : (t >> 24)) & 0xFFFFFFF0u);
+        }
+    }
+}
+
 // ---- simple_hash_ex (M = 31) / Time33Hash_ex (M = 33), one word -----------
 // h4 = M^4 h + M^3 b0 + M^2 b1 + M b2 + b3 (mod 2^32).  M^3 < 2^16, so the
 // word polynomial is two v_dot4 byte planes.

@@ -245,19 +245,60 @@ __global__ __launch_bounds__(TM == 2 ? 1024 : kHashBlock) void sig_hash_kernel(
             asm volatile("s_waitcnt vmcnt(8)" : "+v"(R[0]), "+v"(R[1]), "+v"(R[2]), "+v"(R[3]) :: "memory");
             asm volatile("" : "+v"(R[4]), "+v"(R[5]), "+v"(R[6]), "+v"(R[7]));
         };
-        issue(RA, 0);
-        for (uint32_t st = 0; st < nmax; st += 2) {
-            issue(RB, st + 1);
-            wait_older(RA);
-            step(RA, st < nsteps);
-            issue(RA, st + 2);
-            wait_older(RB);
-            if (st + 1 < nmax)
-                step(RB, st + 1 < nsteps);
+        auto drain = [&]() {
+            asm volatile("s_waitcnt vmcnt(0)"
+                         : "+v"(RA[0]), "+v"(RA[1]), "+v"(RA[2]), "+v"(RA[3]), "+v"(RA[4]), "+v"(RA[5]),
+                           "+v"(RA[6]), "+v"(RA[7]) :: "memory");
+            asm volatile("" : "+v"(RB[0]), "+v"(RB[1]), "+v"(RB[2]), "+v"(RB[3]), "+v"(RB[4]), "+v"(RB[5]),
+                              "+v"(RB[6]), "+v"(RB[7]));
+        };
+        // Small lanes only ever end, so the steps where a lane below big_min
+        // is still hashing are a prefix [0, nfull) of the wave's steps.  The
+        // rest (waves of big files) hash ELF alone and are bound by its
+        // dependent chain: the 3-op form (elf_word4_chain) there.
+        uint32_t nfull = small ? nsteps : 0;
+#pragma unroll
+        for (int o = 32; o; o >>= 1) {
+            const uint32_t y = __shfl_xor(nfull, o);
+            nfull = y > nfull ? y : nfull;
         }
-        asm volatile("s_waitcnt vmcnt(0)"
-                     : "+v"(RA[0]), "+v"(RA[1]), "+v"(RA[2]), "+v"(RA[3]), "+v"(RA[4]), "+v"(RA[5]),
-                       "+v"(RA[6]), "+v"(RA[7]) :: "memory");
+        if (nfull) {
+            issue(RA, 0);
+            for (uint32_t st = 0; st < nfull; st += 2) {
+                issue(RB, st + 1);
+                wait_older(RA);
+                step(RA, st < nsteps);
+                issue(RA, st + 2);
+                wait_older(RB);
+                if (st + 1 < nfull)
+                    step(RB, st + 1 < nsteps);
+            }
+            drain();
+        }
+        auto step_chain = [&](const u32x4 (&a)[8], bool ok) {
+            if (MODE == 1 || !ok)
+                return;
+#pragma unroll
+            for (int q = 0; q < 8; q++) {
+                elf_word4_chain<SAR, false>(a[q][0], e);
+                elf_word4_chain<SAR, false>(a[q][1], e);
+                elf_word4_chain<SAR, false>(a[q][2], e);
+                elf_word4_chain<SAR, true>(a[q][3], e);
+            }
+        };
+        if (nfull < nmax) {
+            issue(RA, nfull);
+            for (uint32_t st = nfull; st < nmax; st += 2) {
+                issue(RB, st + 1);
+                wait_older(RA);
+                step_chain(RA, st < nsteps);
+                issue(RA, st + 2);
+                wait_older(RB);
+                if (st + 1 < nmax)
+                    step_chain(RB, st + 1 < nsteps);
+            }
+            drain();
+        }
         // planes -> value: sum_j P_j << 8j over the lane quad (j = lane & 3),
         // then back to the file's lane; undo the padded steps (M^-128 each)
         uint32_t s31 = 0, s33 = 0;

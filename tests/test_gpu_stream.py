@@ -279,3 +279,61 @@ def test_crc_batch_global_one_rank(oracle, ctxs):
             assert [int(x) for x in got] == [oracle.crc32(f, v) for f in files], v
     finally:
         dist.destroy_process_group()
+
+
+def test_two_streams_one_context(oracle):
+    """The context contract (include/fdfs_gpu.h): one context used from two
+    host threads on two streams at once, with batches that grow (the
+    workspace is regrown while the other stream's kernels may still run):
+    HASH signatures on one, dedup on the other, every result exact."""
+    import threading
+
+    import fastdfs_amd as F
+    ctx = F.Context(0)
+    dev = torch.device("cuda", 0)
+    s1, s2 = torch.cuda.Stream(dev), torch.cuda.Stream(dev)
+    errors = []
+
+    def sigs():
+        try:
+            rng = np.random.default_rng(41)
+            for n in (200, 3000, 20_000, 60_000):
+                sizes = rng.integers(0, 9000, n)
+                offs = np.zeros(n, np.int64)
+                offs[1:] = np.cumsum(sizes)[:-1]
+                buf = rng.integers(0, 256, int(sizes.sum()) + 1, dtype=np.uint8)
+                with torch.cuda.stream(s1):
+                    d = torch.from_numpy(buf).to(dev, non_blocking=False)
+                    o = torch.from_numpy(offs).to(dev)
+                    z = torch.from_numpy(sizes.astype(np.int64)).to(dev)
+                    crc, sig, _ = ctx.sig_batch(d, o, z, method=F.SIG_HASH, stream=s1)
+                s1.synchronize()
+                ocrc, osig = oracle.dio_batch(buf, offs, sizes, 1, 0, nthreads=4)
+                assert np.array_equal(crc.cpu().numpy().view(np.uint32), ocrc), ("crc", n)
+                assert np.array_equal(sig.cpu().numpy(), osig), ("sig", n)
+        except Exception as e:  # noqa: BLE001 - reported by the main thread
+            errors.append(e)
+
+    def dedups():
+        try:
+            rng = np.random.default_rng(43)
+            for n in (1000, 50_000, 400_000, 1_500_000):
+                base = rng.integers(0, 256, size=(max(1, n // 2), 24), dtype=np.uint8)
+                sig = base[rng.integers(0, len(base), size=n)]
+                with torch.cuda.stream(s2):
+                    st = torch.from_numpy(sig).to(dev)
+                    rep, ref = ctx.dedup(st, stream=s2)
+                s2.synchronize()
+                orep, oref = oracle.dedup(sig)
+                assert np.array_equal(rep.cpu().numpy(), orep.astype(np.int64)), ("rep", n)
+                assert np.array_equal(ref.cpu().numpy(), oref.astype(np.int32)), ("ref", n)
+        except Exception as e:  # noqa: BLE001
+            errors.append(e)
+
+    ts = [threading.Thread(target=sigs), threading.Thread(target=dedups)]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join()
+    ctx.close()
+    assert not errors, errors
