@@ -327,15 +327,52 @@ def chain_floor_ms(ctx, data, offs_t, sizes_t, sizes, method, kernel):
     return ms / max(cnt, 1), int(sizes[k])
 
 
+def rccl_exchange_check(ctx, world, rank, dev):
+    """N > 1: set up libfdfs_gpu's RCCL communicator and check that
+    fdfs_gpu_dedup_global gives every rank the same answers as the
+    torch.distributed form of the exchange on a seeded 200K-record set with
+    duplicates across ranks.  All ranks agree (all-reduce MIN of a flag)
+    before the timed run; on a failure or a mismatch anywhere the run uses
+    the torch.distributed exchange and the line says why.
+    Returns (Comm or None, the check's record for the JSON line)."""
+    from fastdfs_amd.api import Comm
+    comm, why = None, "ok"
+    try:
+        comm = Comm(ctx)
+        g = torch.Generator(device="cpu").manual_seed(97)
+        base = torch.randint(0, 256, (150_000, 24), dtype=torch.uint8, generator=g)
+        pick = torch.randint(0, base.shape[0], (200_000,), generator=g)
+        per = (200_000 + world - 1) // world
+        lo, hi = rank * per, min(200_000, (rank + 1) * per)
+        sig = base[pick[lo:hi]].contiguous().to(dev)
+        gidx = torch.arange(lo, hi, dtype=torch.int64, device=dev)
+        rep_a, ref_a = dedup_global(ctx, sig, gidx, comm=comm)
+        rep_b, ref_b = dedup_global(ctx, sig, gidx, comm=None)
+        torch.cuda.synchronize()
+        if not (torch.equal(rep_a, rep_b) and torch.equal(ref_a, ref_b)):
+            why = "mismatch"
+    except Exception as e:  # noqa: BLE001 - reported in the JSON line
+        why = f"error: {e}"[:200]
+    flag = torch.tensor([1 if why == "ok" else 0], dtype=torch.int32, device=dev)
+    dist.all_reduce(flag, op=dist.ReduceOp.MIN)
+    if int(flag.item()) == 1:
+        return comm, {"records": 200_000, "vs_torch_exchange": "equal"}
+    if comm is not None:
+        comm.close()
+    if rank == 0:
+        print(f"warning: RCCL dedup exchange check failed ({why}); using torch.distributed", file=sys.stderr)
+    return None, {"records": 200_000, "vs_torch_exchange": why if why != "ok" else "failed on another rank"}
+
+
 def main():
     args = parse()
     world, rank, local = setup_dist(args)
     dev = torch.device("cuda", local)
     ctx = F.Context(local, unsigned_hash=args.unsigned_hash)
     global COMM
+    rccl_check = None
     if world > 1 and args.exchange == "rccl":
-        from fastdfs_amd.api import Comm
-        COMM = Comm(ctx)
+        COMM, rccl_check = rccl_exchange_check(ctx, world, rank, dev)
     variant = 1 if args.unsigned_hash else 0
     threads = host_threads(args)
     res = {"metric": METRIC, "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
@@ -493,6 +530,8 @@ def main():
             res["cpu_baseline"] = cpu_dedup_baseline(sig, args.cpu_seconds, threads)
         else:
             res["cpu_baseline"] = None
+    if rccl_check is not None:
+        res.setdefault("config", {})["rccl_check"] = rccl_check
     if world > 1:
         res.setdefault("config", {})["dedup_exchange"] = (
             "fdfs_gpu_dedup_global (libfdfs_gpu, RCCL send/recv)" if COMM is not None
