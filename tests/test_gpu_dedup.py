@@ -307,3 +307,25 @@ def test_incremental_index_gidx_and_collisions(oracle, ctx):
         assert st["classes"] == 1024 and st["unplaced"] == np.unique(sig, axis=0).shape[0] - 1024
     finally:
         small.close()
+
+
+def test_dedup_600m_known_classes(ctx):
+    """600M records (the split kernel's 4096-bin form: d2 = 11), checked by
+    construction instead of the oracle: 300M distinct signatures, record i
+    and i + 300M carry the same one, so rep = i mod 300M and ref = 2."""
+    half = 300_000_000
+    n = 2 * half
+    free, _ = torch.cuda.mem_get_info()
+    if free < 80 << 30:
+        pytest.skip("needs ~60 GB of device memory")
+    cls = torch.arange(half, dtype=torch.int64, device="cuda")
+    words = torch.stack([cls, cls * 0x9E3779B97F4A7C15 + 12345, cls ^ 0x5555AAAA5555AAAA], dim=1)
+    one = words.contiguous().view(torch.uint8).view(half, 24)
+    sig = torch.cat([one, one])
+    del words, one
+    rep, ref = ctx.dedup(sig)
+    torch.cuda.synchronize()
+    del sig
+    idx = torch.arange(n, dtype=torch.int64, device="cuda")
+    assert torch.equal(rep, idx % half)
+    assert int(ref.min()) == 2 and int(ref.max()) == 2
