@@ -22,6 +22,7 @@ struct fdfs_gpu_ctx {
     bool sar = true;
     fdfs::DevTables *d_tabs = nullptr;
     unsigned seg_grid = 0;
+    uint32_t lat_files = 0;  // lane batches up to one wave per SIMD (BigCrcWs::lat_files)
     void *ws = nullptr;
     size_t ws_bytes = 0;
     char err[256] = {0};
@@ -97,10 +98,35 @@ size_t sig_ws_bytes(uint64_t n)
     size_t lane = align_up(sizeof(uint32_t) * fdfs::kLaneWsDwords) + align_up(sizeof(uint32_t) * n) +
                   align_up(sizeof(uint32_t)) + 2 * align_up(sizeof(uint64_t) * n) +
                   align_up(sizeof(uint64_t) * (n + 1)) + align_up(sizeof(uint32_t) * n) +
-                  align_up(2 * sizeof(uint32_t) * n);  // + BigCrcWs
+                  align_up(2 * sizeof(uint32_t) * n) + align_up(sizeof(uint64_t));  // + BigCrcWs
     size_t seg = align_up(sizeof(uint64_t) * n) + align_up(sizeof(uint64_t) * (n + 1)) +
                  align_up(sizeof(uint64_t) * fdfs::scan_workspace_elems(n));
     return lane > seg ? lane : seg;  // one path per call
+}
+
+// The big-file offload lists of the HASH lane path (sig_ws_bytes counts them).
+fdfs::BigCrcWs carve_big(const fdfs_gpu_ctx *ctx, Carve &cv, uint32_t n)
+{
+    fdfs::BigCrcWs big;
+    big.nbig = cv.take<uint32_t>(1);
+    big.offs = cv.take<uint64_t>(n);
+    big.sizes = cv.take<uint64_t>(n);
+    big.seg_first = cv.take<uint64_t>((size_t)n + 1);
+    big.crc = cv.take<uint32_t>(n);
+    big.poly = cv.take<uint32_t>(2 * (size_t)n);
+    big.big_min = cv.take<uint64_t>(1);
+    big.lat_files = ctx->lat_files;
+#ifdef FDFS_PROBES
+    // measurement build only: FDFS_GPU_LAT_FILES overrides (0 = always kBigCrcMin)
+    static long lf = -2;
+    if (lf == -2) {
+        const char *ev = getenv("FDFS_GPU_LAT_FILES");
+        lf = ev ? atol(ev) : -1;
+    }
+    if (lf >= 0)
+        big.lat_files = (uint32_t)lf;
+#endif
+    return big;
 }
 
 size_t dedup_ws_bytes(uint64_t n) { return fdfs::dedup_ws_bytes(n) + align_up(8 * 64); }
@@ -279,6 +305,7 @@ int fdfs_gpu_open(int device, unsigned flags, fdfs_gpu_ctx **out)
     if (hipGetDeviceProperties(&prop, device) == hipSuccess && prop.multiProcessorCount > 0)
         ncu = prop.multiProcessorCount;
     ctx->seg_grid = (unsigned)(ncu * fdfs::crc_seg_blocks_per_cu());
+    ctx->lat_files = (uint32_t)ncu * 4 * 64;
     *out = ctx;
     return 0;
 }
@@ -395,13 +422,7 @@ int fdfs_gpu_sig_batch(fdfs_gpu_ctx *ctx, const fdfs_gpu_batch *batch, int metho
     } else {
         uint32_t *hist = cv.take<uint32_t>(fdfs::kLaneWsDwords);
         uint32_t *order = cv.take<uint32_t>(n);
-        fdfs::BigCrcWs big;
-        big.nbig = cv.take<uint32_t>(1);
-        big.offs = cv.take<uint64_t>(n);
-        big.sizes = cv.take<uint64_t>(n);
-        big.seg_first = cv.take<uint64_t>((size_t)n + 1);
-        big.crc = cv.take<uint32_t>(n);
-        big.poly = cv.take<uint32_t>(2 * (size_t)n);
+        const fdfs::BigCrcWs big = carve_big(ctx, cv, n);
         hipEvent_t a, b;
         timing_pair(ctx, FDFS_KERNEL_SIG_LANE, a, b);
         e = fdfs::launch_sig_lane(ctx->sar, method, base, batch->offset, batch->size, n, hist,
@@ -470,13 +491,7 @@ int fdfs_gpu_update_batch(fdfs_gpu_ctx *ctx, const fdfs_gpu_batch *chunks, const
     } else {
         uint32_t *hist = cv.take<uint32_t>(fdfs::kLaneWsDwords);
         uint32_t *order = cv.take<uint32_t>(n);
-        fdfs::BigCrcWs big;
-        big.nbig = cv.take<uint32_t>(1);
-        big.offs = cv.take<uint64_t>(n);
-        big.sizes = cv.take<uint64_t>(n);
-        big.seg_first = cv.take<uint64_t>((size_t)n + 1);
-        big.crc = cv.take<uint32_t>(n);
-        big.poly = cv.take<uint32_t>(2 * (size_t)n);
+        const fdfs::BigCrcWs big = carve_big(ctx, cv, n);
         hipEvent_t a, b;
         timing_pair(ctx, FDFS_KERNEL_SIG_LANE, a, b);
         e = fdfs::launch_sig_lane(ctx->sar, method, base, chunks->offset, chunks->size, n, hist, order, &big,

@@ -95,8 +95,8 @@ template <bool SAR, int TM, int MODE, bool ST>
 __global__ __launch_bounds__(TM == 2 ? 1024 : kHashBlock) void sig_hash_kernel(
     const uint8_t *__restrict__ base, const uint64_t *__restrict__ offs,
     const uint64_t *__restrict__ sizes, const uint32_t *__restrict__ order, uint32_t n,
-    const DevTables *__restrict__ tabs, uint64_t big_min, uint32_t *__restrict__ crc_out,
-    uint8_t *__restrict__ sig_out, int32_t *__restrict__ codes_out,
+    const DevTables *__restrict__ tabs, const uint64_t *__restrict__ big_min_p,
+    uint32_t *__restrict__ crc_out, uint8_t *__restrict__ sig_out, int32_t *__restrict__ codes_out,
     fdfs_gpu_file_state *__restrict__ states, const uint32_t *__restrict__ sidx)
 {
     __shared__ uint32_t sD[TM == 2 ? kRep8Dwords : 16 * 256];
@@ -141,6 +141,7 @@ __global__ __launch_bounds__(TM == 2 ? 1024 : kHashBlock) void sig_hash_kernel(
     // are few and issue-bound, the rest is ~half of their instructions, and
     // once a wave's smaller files have ended its CRC blocks run with an
     // empty exec mask (branched over) and its MFMA steps are skipped.
+    const uint64_t big_min = big_min_p ? *big_min_p : ~0ull;  // big_plan_kernel's T
     const bool small = L < big_min;
 
     // bytes to 16-byte alignment, then vectors to 128-byte alignment (lane-serial)
@@ -361,7 +362,7 @@ __global__ __launch_bounds__(TM == 2 ? 1024 : kHashBlock) void sig_hash_kernel(
         reinterpret_cast<int4 *>(codes_out)[f] = make_int4((int)c, (int)e, (int)s, (int)t);
 }
 
-// simple_hash_ex / Time33Hash_ex of the files >= kBigCrcMin, segment-parallel
+// simple_hash_ex / Time33Hash_ex of the big files (>= T), segment-parallel
 // (INIT_HASH_CODES4 starts both at 0, so a file's hash is the polynomial
 // sum_pos b_pos M^(L-1-pos) mod 2^32 and splits over any cut).  One wave per
 // 64 KiB segment of the big-file list big_plan_kernel made; lane l hashes
@@ -443,7 +444,7 @@ hipError_t launch_poly_seg(const uint8_t *base, const uint64_t *boffs, const uin
 
 hipError_t launch_sig_hash(bool sar, const uint8_t *base, const uint64_t *offs,
                            const uint64_t *sizes, uint32_t n, const uint32_t *order,
-                           const DevTables *tabs, uint64_t big_min, uint32_t *crc_out, uint8_t *sig_out,
+                           const DevTables *tabs, const uint64_t *big_min, uint32_t *crc_out, uint8_t *sig_out,
                            int32_t *codes_out, fdfs_gpu_file_state *states, const uint32_t *sidx,
                            hipStream_t st)
 {

@@ -18,15 +18,20 @@ constexpr int kLaneWsDwords = 2 * kSizeBins + 64;  // size-bin histogram + curso
 uint64_t scan_workspace_elems(uint64_t n);
 hipError_t launch_exclusive_scan(const uint64_t *in, uint64_t n, uint64_t *out, uint64_t *bsum,
                                  hipStream_t st);
-// HASH method: files of at least kBigCrcMin bytes get their CRC, simple_hash
+// HASH method: files of at least a threshold T get their CRC, simple_hash
 // and Time33 from segment-parallel kernels (a wave of such files is
-// issue-bound, see fdfs_hash.hip); their lanes keep only ELFHash.
+// issue-bound, see fdfs_hash.hip); their lanes keep only ELFHash.  Batches
+// of more than lat_files files (one wave per SIMD) use T = kBigCrcMin;
+// smaller ones are latency-bound and big_plan_kernel picks T from the size
+// histogram (fdfs_sig.hip).
 constexpr uint64_t kBigCrcMin = 4ull << 20;
 struct BigCrcWs {  // device arrays of n entries (seg_first n + 1)
     uint32_t *nbig;
     uint64_t *offs, *sizes, *seg_first;
     uint32_t *crc;
-    uint32_t *poly;  // [2n]: simple_hash, Time33 per big file
+    uint32_t *poly;      // [2n]: simple_hash, Time33 per big file
+    uint64_t *big_min;   // [1]: the T big_plan_kernel chose (read by the lane kernel)
+    uint32_t lat_files;  // host: batches up to this many files choose T adaptively (0: never)
 };
 hipError_t launch_poly_seg(const uint8_t *base, const uint64_t *boffs, const uint64_t *bsizes,
                            const uint64_t *seg_first, const uint32_t *nbig, uint32_t *bpoly,
@@ -52,7 +57,7 @@ hipError_t launch_md5_stage(bool sar, const uint8_t *base, const uint64_t *offs,
                             hipStream_t st);
 hipError_t launch_sig_hash(bool sar, const uint8_t *base, const uint64_t *offs,
                            const uint64_t *sizes, uint32_t n, const uint32_t *order,
-                           const DevTables *tabs, uint64_t big_min, uint32_t *crc_out, uint8_t *sig_out,
+                           const DevTables *tabs, const uint64_t *big_min, uint32_t *crc_out, uint8_t *sig_out,
                            int32_t *codes_out, fdfs_gpu_file_state *states, const uint32_t *sidx,
                            hipStream_t st);
 

@@ -459,21 +459,132 @@ __global__ __launch_bounds__(kScanBlock) void scan_apply_kernel(const uint64_t *
 }
 
 // ------------------------------------------------- big-file CRC offload (HASH)
-// Files of >= kBigCrcMin bytes (a power of two, so exactly the size bins from
-// bin(kBigCrcMin) up) are the first nbig entries of the size-descending
-// order.  One block lists them for crc_seg_kernel: compacted offsets/sizes,
-// the exclusive scan of their 64 KiB segment counts, zeroed CRC slots.
+// Files of >= T bytes (a power of two, so exactly the size bins from bin(T)
+// up) are the first nbig entries of the size-descending order.  One block
+// picks T, then lists them for crc_seg_kernel / poly_seg_kernel: compacted
+// offsets/sizes, the exclusive scan of their 64 KiB segment counts, zeroed
+// CRC and polynomial slots.
+//
+// Choosing T.  A batch of more than lat_files files puts several waves on a
+// SIMD; the lane kernel is issue-bound there and T = kBigCrcMin (tuned on
+// configs 1 and 2).  A smaller batch (the daemon's per-wakeup chunk batches,
+// fdfs_gpu_update_batch) has at most one wave per SIMD, so the lane kernel
+// lasts as long as its longest chain: ~kFullPs per byte for a file hashed
+// whole in its lane, ~kElfPs per byte for one that keeps only ELFHash
+// (measured: a 256 KiB chunk alone, `profiles/r02/chunk_sweep.txt`; the
+// 100 MiB file of config 1).  Offloading the files >= T adds their bytes to
+// two HBM passes (~kOffPs per byte).  T = 2^k (k in [kMinLog, 22]) or no
+// offload minimises max(chain below T, ELF chain at or above T) + offload.
+constexpr uint64_t kFullPs = 21000, kElfPs = 8600, kOffHalfPs = 1;  // ps per byte (kOffHalfPs: 0.5 ps)
+constexpr int kMinLog = 13;
+
+__device__ __forceinline__ uint64_t bin_hi(int b)  // an upper bound of the sizes in bin b
+{
+    if (b < 0)
+        return 0;
+    const int e = b >> 5, m = b & 31;
+    if (e >= 41)
+        return 1ull << 42;  // keeps the costs below far from overflow
+    return e >= 5 ? (uint64_t)(33 + m) << (e - 5) : 1ull << (e + 1);
+}
+__device__ __forceinline__ uint64_t bin_lo(int b)
+{
+    const int e = b >> 5, m = b & 31;
+    return e >= 5 ? (uint64_t)(32 + m) << (e - 5) : (uint64_t)b;
+}
+
 __global__ __launch_bounds__(1024) void big_plan_kernel(
     const uint32_t *__restrict__ hist, const uint32_t *__restrict__ order,
     const uint64_t *__restrict__ offs, const uint64_t *__restrict__ sizes, uint32_t n,
-    uint32_t *__restrict__ nbig_out, uint64_t *__restrict__ boffs, uint64_t *__restrict__ bsizes,
+    uint32_t lat_files, uint32_t *__restrict__ nbig_out, uint64_t *__restrict__ big_min,
+    uint64_t *__restrict__ boffs, uint64_t *__restrict__ bsizes,
     uint64_t *__restrict__ seg_first, uint32_t *__restrict__ bcrc, uint32_t *__restrict__ bpoly)
 {
+    static_assert(kSizeBins == 2 * 1024, "two bins per thread");
     __shared__ uint32_t wsum[16];
     __shared__ uint64_t wsum64[16];
-    __shared__ uint32_t nb_s;
+    __shared__ uint64_t eb[64];  // per exponent: bytes (from bin lower bounds)
+    __shared__ int em[64];       // per exponent: largest nonempty bin, -1 if none
+    __shared__ uint32_t nb_s, b0_s;
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-    const uint32_t b0 = size_bin(kBigCrcMin);
+    if (n > lat_files) {
+        if (threadIdx.x == 0)
+            b0_s = size_bin(kBigCrcMin);
+    } else {
+        // thread t: bins 2t, 2t + 1, both of exponent t >> 4
+        const int t = threadIdx.x;
+        uint64_t by = 0;
+        int mb = -1;
+#pragma unroll
+        for (int k = 0; k < 2; k++) {
+            const int b = 2 * t + k;
+            const uint32_t c = hist[b];
+            if (c) {
+                by += (uint64_t)c * bin_lo(b);
+                mb = b;
+            }
+        }
+#pragma unroll
+        for (int o = 8; o; o >>= 1) {
+            by += __shfl_xor(by, o);
+            const int y = __shfl_xor(mb, o);
+            mb = y > mb ? y : mb;
+        }
+        if ((t & 15) == 0) {
+            eb[t >> 4] = by;
+            em[t >> 4] = mb;
+        }
+        __syncthreads();
+        if (wid == 0) {  // lane = exponent k: the candidate T = 2^k
+            const int k = lane;
+            uint64_t above = eb[k];  // bytes in exponents >= k (suffix sum)
+            int below = em[k];       // largest bin in exponents < k (exclusive prefix max)
+#pragma unroll
+            for (int o = 1; o < 64; o <<= 1) {
+                const uint64_t a = __shfl_down(above, o);
+                if (lane + o < 64)
+                    above += a;
+            }
+#pragma unroll
+            for (int o = 1; o < 64; o <<= 1) {
+                const int y = __shfl_up(below, o);
+                if (lane >= o)
+                    below = y > below ? y : below;
+            }
+            below = __shfl_up(below, 1);
+            if (lane == 0)
+                below = -1;
+            above = above < (1ull << 42) ? above : (1ull << 42);
+            int top = em[k];
+#pragma unroll
+            for (int o = 32; o; o >>= 1) {
+                const int y = __shfl_xor(top, o);
+                top = y > top ? y : top;
+            }
+            // key = cost * 64 + (63 - k): the smallest cost, ties to the larger T
+            const uint64_t none = bin_hi(top) * kFullPs * 2;
+            uint64_t key = none * 64;  // k = 63: no offload
+            if (k >= kMinLog && k <= 22) {
+                const uint64_t chain_small = bin_hi(below) * kFullPs * 2;
+                const uint64_t chain_big = (top >> 5) >= k ? bin_hi(top) * kElfPs * 2 : 0;
+                const uint64_t cost = (chain_small > chain_big ? chain_small : chain_big) + above * kOffHalfPs;
+                key = cost * 64 + (uint64_t)(63 - k);
+            }
+#pragma unroll
+            for (int o = 32; o; o >>= 1) {
+                const uint64_t y = __shfl_xor(key, o);
+                key = y < key ? y : key;
+            }
+            if (lane == 0) {
+                const int kb = 63 - (int)(key & 63);
+                b0_s = kb >= 63 ? (uint32_t)kSizeBins : (uint32_t)(kb * 32);  // bin(2^kb)
+            }
+        }
+    }
+    __syncthreads();
+    const uint32_t b0 = b0_s;
+    if (threadIdx.x == 0)
+        *big_min = b0 >= (uint32_t)kSizeBins ? ~0ull : 1ull << (b0 >> 5);
     uint32_t cnt = 0;
     for (uint32_t b = b0 + threadIdx.x; b < kSizeBins; b += blockDim.x)
         cnt += hist[b];
@@ -619,9 +730,10 @@ hipError_t launch_sig_lane(bool sar, int method, const uint8_t *base, const uint
     bin_scan_kernel<<<1, 1024, 0, st>>>(hist, cursor);
     bin_scatter_kernel<<<hb, 1024, 0, st>>>(sizes, n, cursor, order);
     const bool offload = method == 1 && big != nullptr;
-    if (offload) {  // CRC of the files >= kBigCrcMin by the segmented kernel, before the lane kernel
-        big_plan_kernel<<<1, 1024, 0, st>>>(hist, order, offs, sizes, n, big->nbig, big->offs, big->sizes,
-                                            big->seg_first, big->crc, big->poly);
+    if (offload) {  // CRC, simple_hash, Time33 of the files >= T by the segmented kernels, first
+        big_plan_kernel<<<1, 1024, 0, st>>>(hist, order, offs, sizes, n, big->lat_files, big->nbig,
+                                            big->big_min, big->offs, big->sizes, big->seg_first, big->crc,
+                                            big->poly);
         if ((e = crc_seg_run(sar, base, big->offs, big->sizes, big->seg_first, n, big->nbig, tabs, big->crc,
                              seg_grid, st)) != hipSuccess)
             return e;
@@ -634,7 +746,7 @@ hipError_t launch_sig_lane(bool sar, int method, const uint8_t *base, const uint
     e = (method == 2) ? launch_md5_stage(sar, base, offs, sizes, n, order, tabs, hist + 2 * kSizeBins,
                                          crc_out, sig_out, codes_out, states, sidx, st)
                       : launch_sig_hash(sar, base, offs, sizes, n, order, tabs,
-                                        offload ? kBigCrcMin : ~0ull, crc_out, sig_out, codes_out, states,
+                                        offload ? big->big_min : nullptr, crc_out, sig_out, codes_out, states,
                                         sidx, st);
     if (e != hipSuccess)
         return e;

@@ -138,15 +138,20 @@ def test_large_file_segmented(oracle, ctxs, variant):
 
 @pytest.mark.parametrize("variant", [0, 1])
 @pytest.mark.parametrize("align", [16, 1])
-def test_big_file_crc_offload(oracle, ctxs, variant, align):
-    """HASH method with whole waves of files >= 4 MiB (kBigCrcMin): their CRC
-    comes from the segmented kernel and is patched into crc_out, the
-    signature and the codes; files at and just below the threshold, a mixed
-    wave and small files in the same batch."""
-    rng = np.random.default_rng(31 + variant * 2 + (align == 1))
+@pytest.mark.parametrize("pad", [False, True])
+def test_big_file_crc_offload(oracle, ctxs, variant, align, pad):
+    """HASH method with whole waves of files >= 4 MiB: their CRC, simple_hash
+    and Time33 come from the segmented kernels and are patched into crc_out,
+    the signature and the codes; files at and just below 4 MiB, a mixed wave
+    and small files in the same batch.  pad=True adds 70,000 tiny files, so
+    the batch has more files than one wave per SIMD and takes the fixed
+    threshold kBigCrcMin = 4 MiB; without it big_plan_kernel chooses T."""
+    rng = np.random.default_rng(31 + variant * 2 + (align == 1) + 4 * pad)
     big = rng.integers(4 << 20, (4 << 20) + 300_000, size=130)
     sizes = np.concatenate([big, [4 << 20, (4 << 20) - 1, (4 << 20) + 1, 9 << 20],
                             rng.integers(0, 70000, 200)])
+    if pad:
+        sizes = np.concatenate([sizes, rng.integers(0, 100, 70_000)])
     rng.shuffle(sizes)
     buf, offs, sz = _packed(sizes, align, rng)
     dev_batch = _to_dev(buf, offs, sz)
@@ -155,6 +160,22 @@ def test_big_file_crc_offload(oracle, ctxs, variant, align):
     assert np.array_equal(codes[:, 0].view(np.uint32), crc)
     crc0, _, _ = _gpu(ctxs[variant], dev_batch, 0)
     assert np.array_equal(crc0, crc)
+
+
+@pytest.mark.parametrize("variant", [0, 1])
+@pytest.mark.parametrize("top", [13, 17, 21, 23])
+def test_adaptive_offload_threshold(oracle, ctxs, variant, top):
+    """Small batches (one wave per SIMD or less) offload the files >= T with
+    T = 2^k chosen from the size histogram (big_plan_kernel): sizes 2^k - 1,
+    2^k, 2^k + 1 for every candidate k up to `top`, plus a few random files,
+    put a file on each side of whichever T it picks."""
+    rng = np.random.default_rng(41 + variant + 2 * top)
+    ks = range(12, top + 1)
+    sizes = np.concatenate([[(1 << k) + d for k in ks for d in (-1, 0, 1)],
+                            rng.integers(0, 1 << top, 20), [0, 1, 4095]])
+    rng.shuffle(sizes)
+    buf, offs, sz = _packed(sizes, 1, rng)
+    _check(oracle, ctxs[variant], variant, buf, offs, sz, methods=(1,))
 
 
 def test_crc_paths_agree_at_scale(oracle, ctxs):

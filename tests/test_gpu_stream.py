@@ -201,10 +201,13 @@ def test_crc_combine(oracle, ctxs, variant):
     assert [int(x) for x in got] == [w[0] for w in want]
 
 
-def test_many_uploads_one_chunk_each(oracle, ctxs):
-    """The daemon's shape: 20K concurrent uploads, each call advances every
-    one by one 256 KiB-or-less chunk (the first shorter by a header), MD5."""
-    rng = np.random.default_rng(12)
+@pytest.mark.parametrize("method", [1, 2])
+def test_many_uploads_one_chunk_each(oracle, ctxs, method):
+    """The daemon's shape: 2,000 concurrent uploads, each call advances every
+    one by one 256 KiB-or-less chunk (the first shorter by a header).  For
+    HASH such a batch is latency-bound and offloads the CRC and polynomials
+    of its chunks at the threshold big_plan_kernel picks."""
+    rng = np.random.default_rng(12 + method)
     sizes = rng.integers(0, 1_200_000, 2000)
     files = _files(rng, sizes)
     ctx = ctxs[0]
@@ -227,13 +230,13 @@ def test_many_uploads_one_chunk_each(oracle, ctxs):
             p += c
         ctx.update_batch(states, torch.from_numpy(np.concatenate(parts + [np.zeros(1, np.uint8)])).cuda(),
                          torch.tensor(offs, dtype=torch.int64, device="cuda"),
-                         torch.tensor(szs, dtype=torch.int64, device="cuda"), method=2,
+                         torch.tensor(szs, dtype=torch.int64, device="cuda"), method=method,
                          state_idx=torch.tensor(live, dtype=torch.int32, device="cuda"))
         k += 1
-    crc, sig, _ = _final(ctx, states, 2)
+    crc, sig, _ = _final(ctx, states, method)
     offs = np.zeros(n, np.uint64)
     offs[1:] = np.cumsum(sizes)[:-1]
-    ocrc, osig = oracle.dio_batch(np.concatenate(files), offs, sizes.astype(np.uint64), 2, 0, nthreads=8)
+    ocrc, osig = oracle.dio_batch(np.concatenate(files), offs, sizes.astype(np.uint64), method, 0, nthreads=8)
     assert np.array_equal(crc, ocrc)
     assert np.array_equal(sig, osig)
 
