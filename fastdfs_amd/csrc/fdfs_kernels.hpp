@@ -18,12 +18,13 @@ constexpr int kLaneWsDwords = 2 * kSizeBins + 64;  // size-bin histogram + curso
 uint64_t scan_workspace_elems(uint64_t n);
 hipError_t launch_exclusive_scan(const uint64_t *in, uint64_t n, uint64_t *out, uint64_t *bsum,
                                  hipStream_t st);
-// HASH method: files of at least a threshold T get their CRC, simple_hash
-// and Time33 from segment-parallel kernels (a wave of such files is
-// issue-bound, see fdfs_hash.hip); their lanes keep only ELFHash.  Batches
-// of more than lat_files files (one wave per SIMD) use T = kBigCrcMin;
-// smaller ones are latency-bound and big_plan_kernel picks T from the size
-// histogram (fdfs_sig.hip).
+// Lane paths: files of at least a threshold T get their CRC (and for HASH
+// simple_hash and Time33) from segment-parallel kernels; their lanes keep
+// only ELFHash (HASH, a wave of such files is issue-bound, see
+// fdfs_hash.hip) or MD5.  Batches of more than lat_files files (one wave per
+// SIMD) use T = kBigCrcMin (HASH) or no offload (MD5: its single fused pass
+// is HBM-bound there); smaller ones are latency-bound and big_plan_kernel
+// picks T from the size histogram (fdfs_sig.hip).
 constexpr uint64_t kBigCrcMin = 4ull << 20;
 struct BigCrcWs {  // device arrays of n entries (seg_first n + 1)
     uint32_t *nbig;
@@ -52,9 +53,9 @@ hipError_t launch_crc_seg(bool sar, const uint8_t *base, const uint64_t *offs, c
                           hipEvent_t ev0, hipEvent_t ev1);
 hipError_t launch_md5_stage(bool sar, const uint8_t *base, const uint64_t *offs,
                             const uint64_t *sizes, uint32_t n, const uint32_t *order,
-                            const DevTables *tabs, uint32_t *queue, uint32_t *crc_out, uint8_t *sig_out,
-                            int32_t *codes_out, fdfs_gpu_file_state *states, const uint32_t *sidx,
-                            hipStream_t st);
+                            const DevTables *tabs, const uint64_t *big_min, uint32_t *queue, uint32_t *crc_out,
+                            uint8_t *sig_out, int32_t *codes_out, fdfs_gpu_file_state *states,
+                            const uint32_t *sidx, hipStream_t st);
 hipError_t launch_sig_hash(bool sar, const uint8_t *base, const uint64_t *offs,
                            const uint64_t *sizes, uint32_t n, const uint32_t *order,
                            const DevTables *tabs, const uint64_t *big_min, uint32_t *crc_out, uint8_t *sig_out,

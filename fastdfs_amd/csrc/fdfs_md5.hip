@@ -68,7 +68,11 @@ __device__ __forceinline__ void md5_finish(uint32_t st[4], const uint8_t *tp, ui
 // CRC + MD5.  Its table lookups are independent of the MD5 chain, so they
 // fill the issue slots a latency-bound MD5 wave leaves empty.  The slice-by-16
 // tables are shared by the workgroup's waves (waves are otherwise
-// independent: no barrier after the table fill).
+// independent: no barrier after the table fill).  Exception: in a batch too
+// small to fill the chip (big_plan_kernel, fdfs_sig.hip) the files >= the
+// threshold *big_min leave their CRC to crc_seg_kernel, and their lanes hash
+// MD5 alone (a 256 KiB chunk: 5.2 -> 3.0 ms of lane time,
+// profiles/r02/chunk_sweep.txt); big_min == nullptr: every lane does both.
 //
 // ST (fdfs_gpu_update_batch): the lane continues a StorageFileContext-shaped
 // state instead of starting one.  The (count / 8) % 64 bytes my_md5_update
@@ -86,7 +90,8 @@ template <bool SAR, bool ST>
 __global__ __launch_bounds__(64 * kMd5Waves) void md5_stage_kernel(
     const uint8_t *__restrict__ base, const uint64_t *__restrict__ offs,
     const uint64_t *__restrict__ sizes, const uint32_t *__restrict__ order, uint32_t n,
-    const DevTables *__restrict__ tabs, uint32_t w1, uint32_t *__restrict__ queue,
+    const DevTables *__restrict__ tabs, const uint64_t *__restrict__ big_min_p, uint32_t w1,
+    uint32_t *__restrict__ queue,
     uint32_t *__restrict__ crc_out, uint8_t *__restrict__ sig_out, int32_t *__restrict__ codes_out,
     fdfs_gpu_file_state *__restrict__ states, const uint32_t *__restrict__ sidx)
 {
@@ -124,6 +129,7 @@ __global__ __launch_bounds__(64 * kMd5Waves) void md5_stage_kernel(
     uint8_t *mine = tile + lane * STRIDE;
     const uint8_t *safe = reinterpret_cast<const uint8_t *>(tabs);  // >= 16 readable bytes
     const uint32_t K16 = tabs->t.K16;
+    const uint64_t big_min = big_min_p ? *big_min_p : ~0ull;
     uint32_t chunk;
     if (queue) {
         uint32_t c0 = 0;
@@ -143,6 +149,7 @@ __global__ __launch_bounds__(64 * kMd5Waves) void md5_stage_kernel(
     const uint32_t f = valid ? order[i] : 0;
     const uint64_t L = valid ? sizes[f] : 0;
     const uint8_t *p = valid ? base + offs[f] : safe;
+    const bool small = L < big_min;  // else the CRC comes from crc_seg_kernel
     uint32_t st[4] = {0x67452301u, 0xefcdab89u, 0x98badcfeu, 0x10325476u};  // my_md5_init
     uint32_t c = 0xFFFFFFFFu;  // CRC32_XINIT (storage/storage_service.c:7149)
     fdfs_gpu_file_state *fs = nullptr;
@@ -164,7 +171,8 @@ __global__ __launch_bounds__(64 * kMd5Waves) void md5_stage_kernel(
             for (uint32_t k = 0; k < (uint32_t)pre; k++) {
                 const uint32_t b = p[k];
                 mine[have + k] = (uint8_t)b;
-                c = crc_byte<SAR>(sT, c, b);
+                if (small)
+                    c = crc_byte<SAR>(sT, c, b);
             }
             if (have + pre == 64) {
                 const uint4 *q = reinterpret_cast<const uint4 *>(mine);
@@ -183,10 +191,12 @@ __global__ __launch_bounds__(64 * kMd5Waves) void md5_stage_kernel(
         const uint32_t m[16] = {a0.x, a0.y, a0.z, a0.w, a1.x, a1.y, a1.z, a1.w,
                                 a2.x, a2.y, a2.z, a2.w, a3.x, a3.y, a3.z, a3.w};
         md5_compress(st, m);
-        c = chain16<SAR>(sD, c, a0, K16);
-        c = chain16<SAR>(sD, c, a1, K16);
-        c = chain16<SAR>(sD, c, a2, K16);
-        c = chain16<SAR>(sD, c, a3, K16);
+        if (small) {
+            c = chain16<SAR>(sD, c, a0, K16);
+            c = chain16<SAR>(sD, c, a1, K16);
+            c = chain16<SAR>(sD, c, a2, K16);
+            c = chain16<SAR>(sD, c, a3, K16);
+        }
     };
 
     {
@@ -251,7 +261,7 @@ __global__ __launch_bounds__(64 * kMd5Waves) void md5_stage_kernel(
     if (valid) {
         const uint8_t *tp = s0 + (nblk << 6);
         const uint32_t r = (uint32_t)((L - pre) & 63u);
-        for (uint32_t k = 0; k < r; k++)  // CRC of the tail bytes
+        for (uint32_t k = 0; k < r && small; k++)  // CRC of the tail bytes
             c = crc_byte<SAR>(sT, c, tp[k]);
         if constexpr (ST) {
             // the new pending bytes: the chunk appended to a still-partial
@@ -263,7 +273,8 @@ __global__ __launch_bounds__(64 * kMd5Waves) void md5_stage_kernel(
                 for (uint32_t k = 0; k < r; k++)
                     fs->md5_buffer[k] = tp[k];
             }
-            fs->crc32 = (int32_t)c;
+            if (small)  // else big_patch_state_kernel carries the segmented CRC
+                fs->crc32 = (int32_t)c;
 #pragma unroll
             for (int k = 0; k < 4; k++)
                 fs->md5_state[k] = st[k];
@@ -273,7 +284,8 @@ __global__ __launch_bounds__(64 * kMd5Waves) void md5_stage_kernel(
             fs->md5_count[1] = cnt[1];
         } else {
             md5_finish(st, tp, L);
-            crc_out[f] = c ^ 0xFFFFFFFFu;  // CRC32_FINAL (storage/storage_dio.c:500)
+            if (small)  // else big_patch_kernel writes the segmented CRC
+                crc_out[f] = c ^ 0xFFFFFFFFu;  // CRC32_FINAL (storage/storage_dio.c:500)
             if (sig_out)  // memcpy(sig + 8, md5 digest, 16) (storage/storage_service.c:119)
                 store_sig(sig_out + 24ull * f, L, st[0], st[1], st[2], st[3]);
             if (codes_out)
@@ -292,9 +304,9 @@ __global__ __launch_bounds__(64 * kMd5Waves) void md5_stage_kernel(
 
 hipError_t launch_md5_stage(bool sar, const uint8_t *base, const uint64_t *offs,
                             const uint64_t *sizes, uint32_t n, const uint32_t *order,
-                            const DevTables *tabs, uint32_t *queue, uint32_t *crc_out, uint8_t *sig_out,
-                            int32_t *codes_out, fdfs_gpu_file_state *states, const uint32_t *sidx,
-                            hipStream_t st)
+                            const DevTables *tabs, const uint64_t *big_min, uint32_t *queue, uint32_t *crc_out,
+                            uint8_t *sig_out, int32_t *codes_out, fdfs_gpu_file_state *states,
+                            const uint32_t *sidx, hipStream_t st)
 {
     static int ncu[64];
     int dev = 0;
@@ -326,8 +338,8 @@ hipError_t launch_md5_stage(bool sar, const uint8_t *base, const uint64_t *offs,
     }
     const uint32_t w1 = (uint32_t)ncu[dev] * kMd5Waves;
 #define MD5_LAUNCH(S, T)                                                                              \
-    md5_stage_kernel<S, T><<<grid, kBlk, 0, st>>>(base, offs, sizes, order, n, tabs, w1, q, crc_out, \
-                                                  sig_out, codes_out, states, sidx)
+    md5_stage_kernel<S, T><<<grid, kBlk, 0, st>>>(base, offs, sizes, order, n, tabs, big_min, w1, q, \
+                                                  crc_out, sig_out, codes_out, states, sidx)
     if (states)
         sar ? MD5_LAUNCH(true, true) : MD5_LAUNCH(false, true);
     else

@@ -466,16 +466,20 @@ __global__ __launch_bounds__(kScanBlock) void scan_apply_kernel(const uint64_t *
 // CRC and polynomial slots.
 //
 // Choosing T.  A batch of more than lat_files files puts several waves on a
-// SIMD; the lane kernel is issue-bound there and T = kBigCrcMin (tuned on
-// configs 1 and 2).  A smaller batch (the daemon's per-wakeup chunk batches,
+// SIMD; the lane kernel is issue-bound there and T = kBigCrcMin for HASH
+// (tuned on configs 1 and 2), no offload for MD5 (its fused CRC + MD5 pass
+// is HBM-bound on config 3: a second pass would cost more than it saves).
+// A smaller batch (the daemon's per-wakeup chunk batches,
 // fdfs_gpu_update_batch) has at most one wave per SIMD, so the lane kernel
-// lasts as long as its longest chain: ~kFullPs per byte for a file hashed
-// whole in its lane, ~kElfPs per byte for one that keeps only ELFHash
-// (measured: a 256 KiB chunk alone, `profiles/r02/chunk_sweep.txt`; the
-// 100 MiB file of config 1).  Offloading the files >= T adds their bytes to
-// two HBM passes (~kOffPs per byte).  T = 2^k (k in [kMinLog, 22]) or no
-// offload minimises max(chain below T, ELF chain at or above T) + offload.
-constexpr uint64_t kFullPs = 21000, kElfPs = 8600, kOffHalfPs = 1;  // ps per byte (kOffHalfPs: 0.5 ps)
+// lasts as long as its longest chain: kLanePs[method][0] per byte for a file
+// hashed whole in its lane, kLanePs[method][1] for one whose CRC (and
+// polynomials) are offloaded (measured: 256 KiB chunks alone,
+// profiles/r02/chunk_sweep.txt; the 100 MiB file of config 1).  Offloading
+// the files >= T adds their bytes to the segmented passes (kOffPs8 / 8 ps
+// per byte: two passes for HASH, one for MD5).  T = 2^k (k in [kMinLog, 22])
+// or no offload minimises max(chain below T, chain at or above T) + offload.
+constexpr uint64_t kLanePs[2][2] = {{21000, 8600}, {20000, 11500}};  // [HASH, MD5][whole, offloaded]
+constexpr uint64_t kOffPs8[2] = {4, 2};
 constexpr int kMinLog = 13;
 
 __device__ __forceinline__ uint64_t bin_hi(int b)  // an upper bound of the sizes in bin b
@@ -483,8 +487,8 @@ __device__ __forceinline__ uint64_t bin_hi(int b)  // an upper bound of the size
     if (b < 0)
         return 0;
     const int e = b >> 5, m = b & 31;
-    if (e >= 41)
-        return 1ull << 42;  // keeps the costs below far from overflow
+    if (e >= 35)
+        return 1ull << 36;  // keeps the costs below far from overflow
     return e >= 5 ? (uint64_t)(33 + m) << (e - 5) : 1ull << (e + 1);
 }
 __device__ __forceinline__ uint64_t bin_lo(int b)
@@ -495,7 +499,7 @@ __device__ __forceinline__ uint64_t bin_lo(int b)
 
 __global__ __launch_bounds__(1024) void big_plan_kernel(
     const uint32_t *__restrict__ hist, const uint32_t *__restrict__ order,
-    const uint64_t *__restrict__ offs, const uint64_t *__restrict__ sizes, uint32_t n,
+    const uint64_t *__restrict__ offs, const uint64_t *__restrict__ sizes, uint32_t n, int method,
     uint32_t lat_files, uint32_t *__restrict__ nbig_out, uint64_t *__restrict__ big_min,
     uint64_t *__restrict__ boffs, uint64_t *__restrict__ bsizes,
     uint64_t *__restrict__ seg_first, uint32_t *__restrict__ bcrc, uint32_t *__restrict__ bpoly)
@@ -507,9 +511,10 @@ __global__ __launch_bounds__(1024) void big_plan_kernel(
     __shared__ int em[64];       // per exponent: largest nonempty bin, -1 if none
     __shared__ uint32_t nb_s, b0_s;
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    const int mi = method == 2 ? 1 : 0;
     if (n > lat_files) {
         if (threadIdx.x == 0)
-            b0_s = size_bin(kBigCrcMin);
+            b0_s = mi ? (uint32_t)kSizeBins : size_bin(kBigCrcMin);
     } else {
         // thread t: bins 2t, 2t + 1, both of exponent t >> 4
         const int t = threadIdx.x;
@@ -554,7 +559,7 @@ __global__ __launch_bounds__(1024) void big_plan_kernel(
             below = __shfl_up(below, 1);
             if (lane == 0)
                 below = -1;
-            above = above < (1ull << 42) ? above : (1ull << 42);
+            above = above < (1ull << 40) ? above : (1ull << 40);
             int top = em[k];
 #pragma unroll
             for (int o = 32; o; o >>= 1) {
@@ -562,12 +567,13 @@ __global__ __launch_bounds__(1024) void big_plan_kernel(
                 top = y > top ? y : top;
             }
             // key = cost * 64 + (63 - k): the smallest cost, ties to the larger T
-            const uint64_t none = bin_hi(top) * kFullPs * 2;
+            const uint64_t whole = kLanePs[mi][0] * 8, lean = kLanePs[mi][1] * 8;  // 1/8 ps per byte
+            const uint64_t none = bin_hi(top) * whole;
             uint64_t key = none * 64;  // k = 63: no offload
             if (k >= kMinLog && k <= 22) {
-                const uint64_t chain_small = bin_hi(below) * kFullPs * 2;
-                const uint64_t chain_big = (top >> 5) >= k ? bin_hi(top) * kElfPs * 2 : 0;
-                const uint64_t cost = (chain_small > chain_big ? chain_small : chain_big) + above * kOffHalfPs;
+                const uint64_t chain_small = bin_hi(below) * whole;
+                const uint64_t chain_big = (top >> 5) >= k ? bin_hi(top) * lean : 0;
+                const uint64_t cost = (chain_small > chain_big ? chain_small : chain_big) + above * kOffPs8[mi];
                 key = cost * 64 + (uint64_t)(63 - k);
             }
 #pragma unroll
@@ -646,13 +652,15 @@ __global__ __launch_bounds__(1024) void big_plan_kernel(
 // Time33 into crc_out, their signature fields and codes[0], [2], [3].
 __global__ void big_patch_kernel(const uint32_t *__restrict__ nbig, const uint32_t *__restrict__ order,
                                  const uint32_t *__restrict__ bcrc, const uint32_t *__restrict__ bpoly,
-                                 uint32_t *__restrict__ crc_out, uint8_t *__restrict__ sig_out,
+                                 bool md5, uint32_t *__restrict__ crc_out, uint8_t *__restrict__ sig_out,
                                  int32_t *__restrict__ codes_out)
 {
     const uint32_t nb = *nbig;
     for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < nb; i += gridDim.x * blockDim.x) {
         const uint32_t f = order[i], c = bcrc[i], s = bpoly[2ull * i], t = bpoly[2ull * i + 1];
         crc_out[f] = c;
+        if (md5)  // the signature and codes hold the MD5 digest
+            continue;
         if (sig_out) {  // be32 crc at 8, be32 simple at 16, be32 Time33 at 20
             uint32_t *sp = reinterpret_cast<uint32_t *>(sig_out + 24ull * f);
             sp[2] = bswap32(c);
@@ -675,7 +683,7 @@ __global__ void big_patch_kernel(const uint32_t *__restrict__ nbig, const uint32
 __global__ void big_patch_state_kernel(const uint32_t *__restrict__ nbig, const uint32_t *__restrict__ order,
                                        const uint32_t *__restrict__ bcrc, const uint32_t *__restrict__ bpoly,
                                        const uint64_t *__restrict__ sizes, const uint32_t *__restrict__ sidx,
-                                       fdfs_gpu_file_state *__restrict__ states,
+                                       bool md5, fdfs_gpu_file_state *__restrict__ states,
                                        const DevTables *__restrict__ tabs)
 {
     const uint32_t nb = *nbig;
@@ -684,6 +692,10 @@ __global__ void big_patch_state_kernel(const uint32_t *__restrict__ nbig, const 
         const uint64_t L = sizes[f];
         fdfs_gpu_file_state *fs = states + (sidx ? sidx[f] : f);
         const uint32_t c = bcrc[i] ^ 0xFFFFFFFFu ^ advance_bytes(tabs->t, ~(uint32_t)fs->crc32, L);
+        if (md5) {
+            fs->crc32 = (int32_t)c;
+            continue;
+        }
         const uint32_t e = (uint32_t)(L & 0x3FFFFFFFull);
         const uint32_t s = pow_dev(31u, e) * (uint32_t)fs->hash_codes[2] + bpoly[2ull * i];
         const uint32_t t = pow_dev(33u, e) * (uint32_t)fs->hash_codes[3] + bpoly[2ull * i + 1];
@@ -729,35 +741,35 @@ hipError_t launch_sig_lane(bool sar, int method, const uint8_t *base, const uint
     bin_hist_kernel<<<hb < 1024 ? hb : 1024, 256, 0, st>>>(sizes, n, hist);
     bin_scan_kernel<<<1, 1024, 0, st>>>(hist, cursor);
     bin_scatter_kernel<<<hb, 1024, 0, st>>>(sizes, n, cursor, order);
-    const bool offload = method == 1 && big != nullptr;
-    if (offload) {  // CRC, simple_hash, Time33 of the files >= T by the segmented kernels, first
-        big_plan_kernel<<<1, 1024, 0, st>>>(hist, order, offs, sizes, n, big->lat_files, big->nbig,
+    const bool offload = big != nullptr;
+    if (offload) {  // CRC (HASH: simple_hash, Time33 too) of the files >= T by the segmented kernels, first
+        big_plan_kernel<<<1, 1024, 0, st>>>(hist, order, offs, sizes, n, method, big->lat_files, big->nbig,
                                             big->big_min, big->offs, big->sizes, big->seg_first, big->crc,
                                             big->poly);
         if ((e = crc_seg_run(sar, base, big->offs, big->sizes, big->seg_first, n, big->nbig, tabs, big->crc,
                              seg_grid, st)) != hipSuccess)
             return e;
-        if ((e = launch_poly_seg(base, big->offs, big->sizes, big->seg_first, big->nbig, big->poly, seg_grid,
-                                 st)) != hipSuccess)
+        if (method == 1 && (e = launch_poly_seg(base, big->offs, big->sizes, big->seg_first, big->nbig, big->poly,
+                                                seg_grid, st)) != hipSuccess)
             return e;
     }
+    const uint64_t *bmin = offload ? big->big_min : nullptr;
     if (ev0)
         (void)hipEventRecord(ev0, st);
-    e = (method == 2) ? launch_md5_stage(sar, base, offs, sizes, n, order, tabs, hist + 2 * kSizeBins,
+    e = (method == 2) ? launch_md5_stage(sar, base, offs, sizes, n, order, tabs, bmin, hist + 2 * kSizeBins,
                                          crc_out, sig_out, codes_out, states, sidx, st)
-                      : launch_sig_hash(sar, base, offs, sizes, n, order, tabs,
-                                        offload ? big->big_min : nullptr, crc_out, sig_out, codes_out, states,
-                                        sidx, st);
+                      : launch_sig_hash(sar, base, offs, sizes, n, order, tabs, bmin, crc_out, sig_out,
+                                        codes_out, states, sidx, st);
     if (e != hipSuccess)
         return e;
     if (ev1)
         (void)hipEventRecord(ev1, st);
     if (offload && states)
-        big_patch_state_kernel<<<256, 256, 0, st>>>(big->nbig, order, big->crc, big->poly, sizes, sidx, states,
-                                                    tabs);
+        big_patch_state_kernel<<<256, 256, 0, st>>>(big->nbig, order, big->crc, big->poly, sizes, sidx,
+                                                    method == 2, states, tabs);
     else if (offload)
-        big_patch_kernel<<<256, 256, 0, st>>>(big->nbig, order, big->crc, big->poly, crc_out, sig_out,
-                                              codes_out);
+        big_patch_kernel<<<256, 256, 0, st>>>(big->nbig, order, big->crc, big->poly, method == 2, crc_out,
+                                              sig_out, codes_out);
     return hipGetLastError();
 }
 

@@ -165,17 +165,18 @@ def test_big_file_crc_offload(oracle, ctxs, variant, align, pad):
 @pytest.mark.parametrize("variant", [0, 1])
 @pytest.mark.parametrize("top", [13, 17, 21, 23])
 def test_adaptive_offload_threshold(oracle, ctxs, variant, top):
-    """Small batches (one wave per SIMD or less) offload the files >= T with
-    T = 2^k chosen from the size histogram (big_plan_kernel): sizes 2^k - 1,
-    2^k, 2^k + 1 for every candidate k up to `top`, plus a few random files,
-    put a file on each side of whichever T it picks."""
+    """Small batches (one wave per SIMD or less) offload the CRC (HASH: and
+    the polynomials) of the files >= T with T = 2^k chosen from the size
+    histogram (big_plan_kernel): sizes 2^k - 1, 2^k, 2^k + 1 for every
+    candidate k up to `top`, plus a few random files, put a file on each
+    side of whichever T it picks.  HASH and MD5."""
     rng = np.random.default_rng(41 + variant + 2 * top)
     ks = range(12, top + 1)
     sizes = np.concatenate([[(1 << k) + d for k in ks for d in (-1, 0, 1)],
                             rng.integers(0, 1 << top, 20), [0, 1, 4095]])
     rng.shuffle(sizes)
     buf, offs, sz = _packed(sizes, 1, rng)
-    _check(oracle, ctxs[variant], variant, buf, offs, sz, methods=(1,))
+    _check(oracle, ctxs[variant], variant, buf, offs, sz, methods=(1, 2))
 
 
 def test_crc_paths_agree_at_scale(oracle, ctxs):
