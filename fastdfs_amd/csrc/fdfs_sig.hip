@@ -191,8 +191,12 @@ __global__ __launch_bounds__(kSegBlock) void crc_seg_kernel(
     const uint32_t *__restrict__ n_dev, const DevTables *__restrict__ tabs, uint32_t *__restrict__ crc_out)
 {
     const uint32_t n = n_dev ? *n_dev : n_host;  // file count, or written by big_plan_kernel
-    if (seg_first[n] == 0)  // nothing to do (e.g. no big file): skip the table fill
-        return;
+    const uint64_t total = seg_first[n];
+    {  // a workgroup none of whose waves has a segment (small batches) skips the table fill
+        const uint64_t nw = (uint64_t)gridDim.x * (blockDim.x >> 6), w0 = (uint64_t)blockIdx.x * (blockDim.x >> 6);
+        if ((total * w0) / nw == (total * (w0 + (blockDim.x >> 6))) / nw)
+            return;
+    }
     // TM 2 (64 KiB conflict-free tables): the reduction tables stay in
     // global memory (24 lookups per segment).  TM 0: everything in LDS.
     constexpr int kD = TM == 2 ? kRep8Dwords : 16 * 256;
@@ -217,7 +221,6 @@ __global__ __launch_bounds__(kSegBlock) void crc_seg_kernel(
     const uint64_t wpb = blockDim.x >> 6;
     const uint64_t w = (uint64_t)blockIdx.x * wpb + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const uint64_t nw = (uint64_t)gridDim.x * wpb;
-    const uint64_t total = seg_first[n];
     uint64_t s = (total * w) / nw;
     const uint64_t s_end = (total * (w + 1)) / nw;
     if (s >= s_end)
@@ -282,6 +285,48 @@ __global__ __launch_bounds__(kSegBlock) void crc_seg_kernel(
 }
 
 // ---------------------------------------------------------------- planning
+
+// Batches of at most kPlanSmall files: segment counts, their exclusive scan
+// (seg_first[0..n]) and the zeroed CRC slots in one workgroup, instead of
+// plan_nseg_kernel + the three-kernel scan (a small call is launch-bound).
+constexpr int kPlanSmallItems = 4;
+constexpr uint32_t kPlanSmall = 1024 * kPlanSmallItems;
+
+__global__ __launch_bounds__(1024) void plan_small_kernel(const uint64_t *__restrict__ sizes, uint32_t n,
+                                                          uint64_t *__restrict__ seg_first,
+                                                          uint32_t *__restrict__ crc_out)
+{
+    __shared__ uint64_t wsum[16];
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    const uint32_t i0 = threadIdx.x * kPlanSmallItems;
+    uint64_t v[kPlanSmallItems], x = 0;
+#pragma unroll
+    for (int k = 0; k < kPlanSmallItems; k++) {
+        v[k] = i0 + k < n ? (sizes[i0 + k] + kSegBytes - 1) / kSegBytes : 0;
+        x += v[k];
+        if (i0 + k < n)
+            crc_out[i0 + k] = 0;  // empty files keep CRC 0; multi-segment files accumulate by XOR
+    }
+    const uint64_t mine = x;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint64_t y = __shfl_up(x, o);
+        if (lane >= o)
+            x += y;
+    }
+    if (lane == 63)
+        wsum[wid] = x;
+    __syncthreads();
+    uint64_t run = x - mine;
+    for (int k = 0; k < wid; k++)
+        run += wsum[k];
+#pragma unroll
+    for (int k = 0; k < kPlanSmallItems; k++) {
+        if (i0 + k <= n)
+            seg_first[i0 + k] = run;  // seg_first[n] = the total
+        run += v[k];
+    }
+}
 
 __global__ void plan_nseg_kernel(const uint64_t *__restrict__ sizes, uint32_t n,
                                  uint64_t *__restrict__ nseg, uint32_t *__restrict__ crc_out)
@@ -797,10 +842,14 @@ hipError_t launch_crc_seg(bool sar, const uint8_t *base, const uint64_t *offs, c
                           const DevTables *tabs, uint32_t *crc_out, unsigned grid, hipStream_t st,
                           hipEvent_t ev0, hipEvent_t ev1)
 {
-    plan_nseg_kernel<<<(n + 255) / 256, 256, 0, st>>>(sizes, n, nseg, crc_out);
-    hipError_t e = launch_exclusive_scan(nseg, n, seg_first, bsum, st);
-    if (e != hipSuccess)
-        return e;
+    hipError_t e;
+    if (n < kPlanSmall) {
+        plan_small_kernel<<<1, 1024, 0, st>>>(sizes, n, seg_first, crc_out);
+    } else {
+        plan_nseg_kernel<<<(n + 255) / 256, 256, 0, st>>>(sizes, n, nseg, crc_out);
+        if ((e = launch_exclusive_scan(nseg, n, seg_first, bsum, st)) != hipSuccess)
+            return e;
+    }
     if (ev0)
         (void)hipEventRecord(ev0, st);
     if ((e = crc_seg_run(sar, base, offs, sizes, seg_first, n, nullptr, tabs, crc_out, grid, st)) != hipSuccess)

@@ -127,6 +127,17 @@ def test_tiny_and_mixed_batch(oracle, ctxs):
     _check(oracle, ctxs[0], 0, buf, offs, sz)
 
 
+@pytest.mark.parametrize("n", [1, 4095, 4096])
+def test_crc_plan_small_boundary(oracle, ctxs, n):
+    """CRC only: batches below 4,096 files are planned by one workgroup
+    (plan_small_kernel), larger ones by the three-kernel scan; both sides of
+    the boundary, and a batch of one file spanning many segments."""
+    rng = np.random.default_rng(61 + n)
+    sizes = rng.integers(0, 150_000, n) if n > 1 else np.array([(5 << 20) + 3])
+    buf, offs, sz = _packed(sizes, 1, rng)
+    _check(oracle, ctxs[0], 0, buf, offs, sz, methods=(0,))
+
+
 @pytest.mark.parametrize("variant", [0, 1])
 def test_large_file_segmented(oracle, ctxs, variant):
     """Config 4 shape: large files split into 64 KiB segments + GF(2) combine."""
