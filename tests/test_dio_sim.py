@@ -1,0 +1,115 @@
+"""fdfs_dio_sim: the storage daemon's per-chunk upload loop (dio_write_file,
+storage/storage_dio.c:465-515, initialised at storage/storage_service.c:7147-7161)
+written in C against include/fdfs_gpu.h alone: files as uploads, at most -j
+in flight, one update_batch per wakeup with one chunk per live upload (the
+first shorter by the header), final_batch for the uploads that ended.
+
+CPU: usage and the loud ENODEV without a GPU.  GPU: the printed CRC and
+24-byte signature of every file equal the oracle's dio loop over the file
+(orc_dio_file), for all three methods, both shift variants, uploads that
+end in different wakeups, empty files and chunk-boundary sizes."""
+import errno
+import os
+import subprocess
+
+import numpy as np
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+TOOL = os.path.join(ROOT, "fastdfs_amd", "lib", "fdfs_dio_sim")
+METHOD = {0: "crc", 1: "hash", 2: "md5"}
+
+
+def _run(args, env=None):
+    if not os.path.exists(TOOL):
+        pytest.fail("fdfs_dio_sim not built (python -c 'import __graft_entry__ as g; g.build()')")
+    e = dict(os.environ)
+    e.update(env or {})
+    return subprocess.run([TOOL] + args, capture_output=True, text=True, timeout=300, env=e)
+
+
+def _has_gpu():
+    import torch
+    return torch.cuda.is_available()
+
+
+def test_usage():
+    r = _run([])
+    assert r.returncode == 1 and r.stdout.startswith("Usage: ")
+    r = _run(["-c", "16", "-H", "16", "x"])  # header must be shorter than a chunk
+    assert r.returncode == 1
+
+
+def test_missing_file_errno():
+    r = _run(["/nonexistent/dio_sim_test"])
+    assert r.returncode == errno.ENOENT and "open file /nonexistent/dio_sim_test fail" in r.stdout
+
+
+def test_no_gpu_fails_loudly(tmp_path):
+    if _has_gpu():
+        pytest.skip("a GPU is present")
+    f = tmp_path / "x"
+    f.write_bytes(b"123456789")
+    r = _run([str(f)])
+    assert r.returncode == errno.ENODEV and "fdfs_gpu_open fail" in r.stdout
+
+
+def _write(tmp_path, sizes, seed):
+    rng = np.random.default_rng(seed)
+    paths, bufs = [], []
+    for i, n in enumerate(sizes):
+        b = rng.integers(0, 256, size=int(n), dtype=np.uint8)
+        p = tmp_path / f"u{i}"
+        p.write_bytes(b.tobytes())
+        paths.append(str(p))
+        bufs.append(b)
+    return paths, bufs
+
+
+def _parse(out, method):
+    rows = [ln.split() for ln in out.strip().splitlines()]
+    crc = [int(r[0]) for r in rows]
+    sig = [bytes.fromhex(r[1]) for r in rows] if method else None
+    return crc, sig
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("variant", [0, 1])
+@pytest.mark.parametrize("method", [0, 1, 2])
+def test_uploads_vs_oracle(tmp_path, oracle, method, variant):
+    """65 KiB buffers, 5 uploads in flight: files end in different wakeups,
+    new uploads take the freed places; sizes at the first-chunk and chunk
+    boundaries, MD5 tails, empty files."""
+    buff, hdr = 65536, 25
+    rng = np.random.default_rng(70 + method)
+    sizes = [0, 1, buff - hdr - 1, buff - hdr, buff - hdr + 1, 2 * buff - hdr, 2 * buff - hdr + 63, 0,
+             5 * buff + 7] + list(rng.integers(0, 400_000, 12))
+    paths, bufs = _write(tmp_path, sizes, 80 + method)
+    r = _run(["-m", METHOD[method], "-c", str(buff), "-H", str(hdr), "-j", "5"] + paths,
+             env={"FDFS_UNSIGNED_HASH": str(variant)})
+    assert r.returncode == 0, r.stdout + r.stderr
+    crc, sig = _parse(r.stdout, method)
+    for i, b in enumerate(bufs):
+        oc, os_, _ = oracle.dio_file(b, method, variant)
+        assert crc[i] == oc, (i, len(b))
+        if method:
+            assert sig[i] == os_, (i, len(b))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("method", [1, 2])
+def test_daemon_shape(tmp_path, oracle, method):
+    """1,200 uploads of 0-1 MiB through 256 KiB buffers, 1,024 in flight:
+    the wakeups carry ~1,000 chunks each, the latency-bound batch shape."""
+    rng = np.random.default_rng(90 + method)
+    sizes = rng.integers(0, 1 << 20, 1200)
+    paths, bufs = _write(tmp_path, sizes, 91 + method)
+    r = _run(["-m", METHOD[method], "-j", "1024"] + paths)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "wakeups" in r.stderr
+    crc, sig = _parse(r.stdout, method)
+    offs = np.zeros(len(sizes), np.uint64)
+    offs[1:] = np.cumsum(sizes)[:-1]
+    ocrc, osig = oracle.dio_batch(np.concatenate(bufs), offs, sizes.astype(np.uint64), method, 0, nthreads=8)
+    assert np.array_equal(np.array(crc, np.uint32), ocrc)
+    assert all(sig[i] == osig[i].tobytes() for i in range(len(sizes)))
