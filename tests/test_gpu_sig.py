@@ -216,6 +216,37 @@ def test_crc_paths_agree_at_scale(oracle, ctxs):
     torch.cuda.empty_cache()
 
 
+@pytest.mark.parametrize("extra", [0, 1])
+def test_offload_regime_boundary(oracle, ctxs, extra):
+    """One wave per SIMD (lat_files = CUs x 4 x 64 files) is where the lane
+    path switches from the threshold big_plan_kernel picks to the fixed one
+    (HASH 4 MiB, MD5 no offload).  Batches of exactly lat_files and one more
+    file, small files plus 4-6 MiB ones: the three methods' CRCs agree for
+    every file, and a sample (every big file among it) matches the oracle."""
+    from fastdfs_amd import corpus as C
+    lat = torch.cuda.get_device_properties(0).multi_processor_count * 4 * 64
+    n = lat + extra
+    rng = np.random.default_rng(17 + extra)
+    sizes = rng.integers(0, 65537, n)
+    big = rng.choice(n, size=200, replace=False)
+    sizes[big] = rng.integers(4 << 20, 6 << 20, 200)
+    data, offs_t, sizes_t = C.device_batch(sizes, seed=9 + extra, device="cuda:0")
+    ctx = ctxs[0]
+    out = {m: ctx.sig_batch(data, offs_t, sizes_t, method=m) for m in (0, 1, 2)}
+    torch.cuda.synchronize()
+    assert torch.equal(out[0][0], out[1][0]) and torch.equal(out[0][0], out[2][0])
+    offs = offs_t.cpu().numpy()
+    pick = np.concatenate([big[:12], rng.choice(n, size=400, replace=False)])
+    for m in (1, 2):
+        crc_np, sig_np = out[m][0].cpu().numpy().view(np.uint32), out[m][1].cpu().numpy()
+        for i in pick:
+            d = data[int(offs[i]): int(offs[i] + sizes[i])].cpu().numpy()
+            c, s, _ = oracle.dio_file(d, m, 0)
+            assert c == crc_np[i] and s == sig_np[i].tobytes(), (m, i, sizes[i])
+    del data, out
+    torch.cuda.empty_cache()
+
+
 def test_md5_staged_multiwave(oracle, ctxs):
     """MD5 method over several waves of the staged kernel: files of 0 B to
     1.2 MiB in one aligned batch (lanes finish at different rounds, partial
