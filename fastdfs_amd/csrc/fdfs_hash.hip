@@ -86,12 +86,46 @@ __device__ __forceinline__ uint32_t and_xor80(uint32_t a, uint32_t m)
     return r;
 }
 
+// Quad transpose of one dword position: lane j of a lane quad holds r_k =
+// dword of piece j of quad-file k; afterwards r_k = dword of piece k of its
+// own file j.  Two butterfly stages (lane xor 1, lane xor 2); each output is
+// one v_cndmask_b32 whose src0 is the partner lane's register read through
+// DPP quad_perm, with VCC = the lanes that keep their own value: 8 VALU per
+// 4 x 4 block.  The leading s_nop covers the VALU-write -> DPP-read hazard
+// for inputs written just before the block, the middle one the same hazard
+// between the stages (hipcc does not look inside an asm statement).
+__device__ __forceinline__ void quad_transpose(uint32_t &r0, uint32_t &r1, uint32_t &r2, uint32_t &r3)
+{
+    uint32_t o0, o1, o2, o3;
+#define QDPP(D, S0, S1, P) "v_cndmask_b32_dpp %[" D "], %[" S0 "], %[" S1 "], vcc quad_perm:" P " row_mask:0xf bank_mask:0xf\n\t"
+    asm volatile(
+        "s_nop 1\n\t"
+        "s_mov_b32 vcc_lo, 0x55555555\n\t"  // even lanes keep
+        "s_mov_b32 vcc_hi, 0x55555555\n\t"
+        QDPP("o0", "r1", "r0", "[1,0,3,2]") QDPP("o2", "r3", "r2", "[1,0,3,2]")
+        "s_mov_b32 vcc_lo, 0xaaaaaaaa\n\t"  // odd lanes keep
+        "s_mov_b32 vcc_hi, 0xaaaaaaaa\n\t"
+        QDPP("o1", "r0", "r1", "[1,0,3,2]") QDPP("o3", "r2", "r3", "[1,0,3,2]")
+        "s_mov_b32 vcc_lo, 0x33333333\n\t"  // lanes 0, 1 of the quad keep
+        "s_mov_b32 vcc_hi, 0x33333333\n\t"
+        "s_nop 1\n\t"
+        QDPP("r0", "o2", "o0", "[2,3,0,1]") QDPP("r1", "o3", "o1", "[2,3,0,1]")
+        "s_mov_b32 vcc_lo, 0xcccccccc\n\t"  // lanes 2, 3 keep
+        "s_mov_b32 vcc_hi, 0xcccccccc\n\t"
+        QDPP("r2", "o0", "o2", "[2,3,0,1]") QDPP("r3", "o1", "o3", "[2,3,0,1]")
+        : [r0] "+v"(r0), [r1] "+v"(r1), [r2] "+v"(r2), [r3] "+v"(r3), [o0] "=&v"(o0), [o1] "=&v"(o1),
+          [o2] "=&v"(o2), [o3] "=&v"(o3)
+        :
+        : "vcc");
+#undef QDPP
+}
+
 // ST (fdfs_gpu_update_batch): the lane continues the chunk's
 // StorageFileContext-shaped state (crc32, file_hash_codes) instead of
 // INIT_HASH_CODES4 and writes it back unfinalised; every step above is a
 // recurrence from whatever state it starts in (the polynomial planes start
 // from the lane's running value), so nothing else changes.
-template <bool SAR, int TM, int MODE, bool ST>
+template <bool SAR, int TM, int MODE, bool ST, bool QL>
 __global__ __launch_bounds__(TM == 2 ? 1024 : kHashBlock) void sig_hash_kernel(
     const uint8_t *__restrict__ base, const uint64_t *__restrict__ offs,
     const uint64_t *__restrict__ sizes, const uint32_t *__restrict__ order, uint32_t n,
@@ -192,7 +226,21 @@ __global__ __launch_bounds__(TM == 2 ? 1024 : kHashBlock) void sig_hash_kernel(
         // still hashing (big files get simple/Time33 from poly_seg_kernel):
         // nexec counts them for the padding undo below.
         uint32_t nexec = 0;
-        auto step = [&](const u32x4 (&a)[8], bool ok) {
+        // QL: the step's pieces arrive quad-interleaved (issue_q below) and
+        // are transposed back to their files' lanes, one half line at a time
+        // just before its four vectors are hashed.
+        auto qtr = [](u32x4 (&a)[8], int h) {
+#pragma unroll
+            for (int d = 0; d < 4; d++) {
+                uint32_t r0 = a[4 * h + 0][d], r1 = a[4 * h + 1][d], r2 = a[4 * h + 2][d], r3 = a[4 * h + 3][d];
+                quad_transpose(r0, r1, r2, r3);
+                a[4 * h + 0][d] = r0;
+                a[4 * h + 1][d] = r1;
+                a[4 * h + 2][d] = r2;
+                a[4 * h + 3][d] = r3;
+            }
+        };
+        auto step = [&](u32x4 (&a)[8], bool ok) {
             const bool mon = __any(ok && small);
             nexec += mon ? 1u : 0u;
 #pragma unroll
@@ -204,6 +252,13 @@ __global__ __launch_bounds__(TM == 2 ? 1024 : kHashBlock) void sig_hash_kernel(
             }
 #pragma unroll
             for (int q = 0; q < 8; q++) {
+                if constexpr (QL && MODE != 1) {
+                    if ((q & 3) == 0) {
+                        __builtin_amdgcn_sched_barrier(0);
+                        qtr(a, q >> 2);
+                        __builtin_amdgcn_sched_barrier(0);
+                    }
+                }
                 const uint4 aq = make_uint4(a[q][0], a[q][1], a[q][2], a[q][3]);
                 if constexpr (MODE == 1) {  // PROBE: loads only
                     if (ok)
@@ -242,6 +297,29 @@ __global__ __launch_bounds__(TM == 2 ? 1024 : kHashBlock) void sig_hash_kernel(
             for (int q = 0; q < 8; q++)
                 asm volatile("global_load_dwordx4 %0, %1, off offset:%2" : "=v"(R[q]) : "v"(ln), "i"(16 * q) : "memory");
         };
+        // Quad-cooperative form (QL): lane j of quad Q loads 16-byte piece
+        // 4h + j of quad-file k's line into R[4h + k], so each instruction
+        // reads 16 half lines of 64 contiguous bytes instead of 64 scattered
+        // 16-byte pieces (4x fewer lines and pages per instruction; loads
+        // alone 6.8 -> 6.0 ms on config 2, profiles/r02/hash_quad_ab.md).
+        // The quad's line addresses are broadcast by DPP quad_perm.
+        auto issue_q = [&](u32x4 (&R)[8], uint32_t stp) {
+            const uint8_t *ln = (MODE != 2 && stp < nsteps) ? reinterpret_cast<const uint8_t *>(w + 8 * (uint64_t)stp) : safe;
+            const uint64_t a = reinterpret_cast<uint64_t>(ln);
+            const uint32_t lo = (uint32_t)a, hi = (uint32_t)(a >> 32);
+            auto ld = [&](u32x4 &R0, u32x4 &R1, uint32_t lk, uint32_t hk) {
+                const uint8_t *pk = reinterpret_cast<const uint8_t *>(((uint64_t)hk << 32 | lk) + 16u * (lane & 3));
+                asm volatile("global_load_dwordx4 %0, %1, off offset:0" : "=v"(R0) : "v"(pk) : "memory");
+                asm volatile("global_load_dwordx4 %0, %1, off offset:64" : "=v"(R1) : "v"(pk) : "memory");
+            };
+#define QBC(K) (uint32_t) __builtin_amdgcn_mov_dpp((int)lo, 0x55 * K, 0xF, 0xF, false), \
+               (uint32_t) __builtin_amdgcn_mov_dpp((int)hi, 0x55 * K, 0xF, 0xF, false)
+            ld(R[0], R[4], QBC(0));
+            ld(R[1], R[5], QBC(1));
+            ld(R[2], R[6], QBC(2));
+            ld(R[3], R[7], QBC(3));
+#undef QBC
+        };
         auto wait_older = [&](u32x4 (&R)[8]) {  // R is the older of the two sets in flight
             asm volatile("s_waitcnt vmcnt(8)" : "+v"(R[0]), "+v"(R[1]), "+v"(R[2]), "+v"(R[3]) :: "memory");
             asm volatile("" : "+v"(R[4]), "+v"(R[5]), "+v"(R[6]), "+v"(R[7]));
@@ -264,19 +342,25 @@ __global__ __launch_bounds__(TM == 2 ? 1024 : kHashBlock) void sig_hash_kernel(
             nfull = y > nfull ? y : nfull;
         }
         if (nfull) {
-            issue(RA, 0);
+            auto iss = [&](u32x4 (&R)[8], uint32_t stp) {
+                if constexpr (QL)
+                    issue_q(R, stp);
+                else
+                    issue(R, stp);
+            };
+            iss(RA, 0);
             for (uint32_t st = 0; st < nfull; st += 2) {
-                issue(RB, st + 1);
+                iss(RB, st + 1);
                 wait_older(RA);
                 step(RA, st < nsteps);
-                issue(RA, st + 2);
+                iss(RA, st + 2);
                 wait_older(RB);
                 if (st + 1 < nfull)
                     step(RB, st + 1 < nsteps);
             }
             drain();
         }
-        auto step_chain = [&](const u32x4 (&a)[8], bool ok) {
+        auto step_chain = [&](u32x4 (&a)[8], bool ok) {
             if (MODE == 1 || !ok)
                 return;
 #pragma unroll
@@ -465,18 +549,30 @@ hipError_t launch_sig_hash(bool sar, const uint8_t *base, const uint64_t *offs,
 #else
     constexpr int tm = 0;
 #endif
+#ifdef FDFS_PROBES
+    static int ql = -1;  // FDFS_GPU_HASH_QUAD=0: round-2 lane-per-file loads
+    if (ql < 0) {
+        const char *ev = getenv("FDFS_GPU_HASH_QUAD");
+        ql = ev ? atoi(ev) : 1;
+    }
+#else
+    constexpr int ql = 1;
+#endif
     const unsigned blk = (tm == 2 && !states) ? 1024 : kHashBlock;
     const unsigned grid = (n + blk - 1) / blk;
 #define HASH_LAUNCH(S, M)                                                                                \
     do {                                                                                                 \
         if (states)                                                                                      \
-            sig_hash_kernel<S, 0, M, true><<<grid, blk, 0, st>>>(base, offs, sizes, order, n, tabs, big_min, \
+            sig_hash_kernel<S, 0, M, true, true><<<grid, blk, 0, st>>>(base, offs, sizes, order, n, tabs, big_min, \
                                                                  crc_out, sig_out, codes_out, states, sidx); \
         else if (tm == 2)                                                                                \
-            sig_hash_kernel<S, 2, M, false><<<grid, blk, 0, st>>>(base, offs, sizes, order, n, tabs, big_min, \
+            sig_hash_kernel<S, 2, M, false, false><<<grid, blk, 0, st>>>(base, offs, sizes, order, n, tabs, big_min, \
+                                                                  crc_out, sig_out, codes_out, nullptr, nullptr); \
+        else if (ql)                                                                                     \
+            sig_hash_kernel<S, 0, M, false, true><<<grid, blk, 0, st>>>(base, offs, sizes, order, n, tabs, big_min, \
                                                                   crc_out, sig_out, codes_out, nullptr, nullptr); \
         else                                                                                             \
-            sig_hash_kernel<S, 0, M, false><<<grid, blk, 0, st>>>(base, offs, sizes, order, n, tabs, big_min, \
+            sig_hash_kernel<S, 0, M, false, false><<<grid, blk, 0, st>>>(base, offs, sizes, order, n, tabs, big_min, \
                                                                   crc_out, sig_out, codes_out, nullptr, nullptr); \
     } while (0)
 #ifdef FDFS_PROBES
