@@ -23,6 +23,10 @@ struct fdfs_gpu_ctx {
     fdfs::DevTables *d_tabs = nullptr;
     unsigned seg_grid = 0;
     uint32_t lat_files = 0;  // lane batches up to one wave per SIMD (BigCrcWs::lat_files)
+    // the segmented passes' stream when they run beside the lane kernel
+    // (BigCrcWs::side) and its fork / join events
+    hipStream_t side = nullptr;
+    hipEvent_t fork = nullptr, join = nullptr;
     void *ws = nullptr;
     size_t ws_bytes = 0;
     char err[256] = {0};
@@ -125,6 +129,21 @@ fdfs::BigCrcWs carve_big(const fdfs_gpu_ctx *ctx, Carve &cv, uint32_t n)
     }
     if (lf >= 0)
         big.lat_files = (uint32_t)lf;
+    // FDFS_GPU_MD5_T_BIN: MD5 batches above lat_files offload the CRC of the
+    // files in size bins >= this one; FDFS_GPU_SIDE=1: beside the lane kernel
+    static long mb = -2, sd = -2;
+    if (mb == -2) {
+        const char *ev = getenv("FDFS_GPU_MD5_T_BIN");
+        mb = ev ? atol(ev) : 0;
+        const char *es = getenv("FDFS_GPU_SIDE");
+        sd = es ? atol(es) : 0;
+    }
+    big.md5_bin = (uint32_t)mb;
+    if (sd == 1) {
+        big.side = ctx->side;
+        big.fork = ctx->fork;
+        big.join = ctx->join;
+    }
 #endif
     return big;
 }
@@ -287,6 +306,14 @@ int fdfs_gpu_open(int device, unsigned flags, fdfs_gpu_ctx **out)
             h->Dc[p][x] = h->t.D[p][x ^ 0xFF];
     fdfs::build_poly_mfma_tables(h->pm);
     hipError_t e = hipEventCreateWithFlags(&ctx->ws_ev, hipEventDisableTiming);
+#ifdef FDFS_PROBES  // the side-stream offload measurement (FDFS_GPU_SIDE, carve_big)
+    if (e == hipSuccess)
+        e = hipStreamCreateWithFlags(&ctx->side, hipStreamNonBlocking);
+    if (e == hipSuccess)
+        e = hipEventCreateWithFlags(&ctx->fork, hipEventDisableTiming);
+    if (e == hipSuccess)
+        e = hipEventCreateWithFlags(&ctx->join, hipEventDisableTiming);
+#endif
     if (e == hipSuccess)
         e = hipMalloc(&ctx->d_tabs, sizeof(fdfs::DevTables));
     if (e == hipSuccess)
@@ -297,6 +324,12 @@ int fdfs_gpu_open(int device, unsigned flags, fdfs_gpu_ctx **out)
             (void)hipFree(ctx->d_tabs);
         if (ctx->ws_ev)
             (void)hipEventDestroy(ctx->ws_ev);
+        if (ctx->side)
+            (void)hipStreamDestroy(ctx->side);
+        if (ctx->fork)
+            (void)hipEventDestroy(ctx->fork);
+        if (ctx->join)
+            (void)hipEventDestroy(ctx->join);
         delete ctx;
         return EIO;
     }
@@ -334,6 +367,12 @@ int fdfs_gpu_close(fdfs_gpu_ctx *ctx)
         (void)hipFree(ctx->d_tabs);
     if (ctx->ws_ev)
         (void)hipEventDestroy(ctx->ws_ev);
+    if (ctx->side)
+        (void)hipStreamDestroy(ctx->side);
+    if (ctx->fork)
+        (void)hipEventDestroy(ctx->fork);
+    if (ctx->join)
+        (void)hipEventDestroy(ctx->join);
     delete ctx;
     return 0;
 }

@@ -33,6 +33,11 @@ struct BigCrcWs {  // device arrays of n entries (seg_first n + 1)
     uint32_t *poly;      // [2n]: simple_hash, Time33 per big file
     uint64_t *big_min;   // [1]: the T big_plan_kernel chose (read by the lane kernel)
     uint32_t lat_files;  // host: batches up to this many files choose T adaptively (0: never)
+    uint32_t md5_bin = 0;  // MD5 batches above lat_files: T = the lower bound of this size bin (0: no offload)
+    // side != nullptr: the segmented kernels run on `side`, concurrently with
+    // the lane kernel (fork after big_plan_kernel, join before the patch)
+    hipStream_t side = nullptr;
+    hipEvent_t fork = nullptr, join = nullptr;
 };
 hipError_t launch_poly_seg(const uint8_t *base, const uint64_t *boffs, const uint64_t *bsizes,
                            const uint64_t *seg_first, const uint32_t *nbig, uint32_t *bpoly,

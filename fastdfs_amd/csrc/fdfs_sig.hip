@@ -545,7 +545,7 @@ __device__ __forceinline__ uint64_t bin_lo(int b)
 __global__ __launch_bounds__(1024) void big_plan_kernel(
     const uint32_t *__restrict__ hist, const uint32_t *__restrict__ order,
     const uint64_t *__restrict__ offs, const uint64_t *__restrict__ sizes, uint32_t n, int method,
-    uint32_t lat_files, uint32_t *__restrict__ nbig_out, uint64_t *__restrict__ big_min,
+    uint32_t lat_files, uint32_t md5_bin, uint32_t *__restrict__ nbig_out, uint64_t *__restrict__ big_min,
     uint64_t *__restrict__ boffs, uint64_t *__restrict__ bsizes,
     uint64_t *__restrict__ seg_first, uint32_t *__restrict__ bcrc, uint32_t *__restrict__ bpoly)
 {
@@ -559,7 +559,7 @@ __global__ __launch_bounds__(1024) void big_plan_kernel(
     const int mi = method == 2 ? 1 : 0;
     if (n > lat_files) {
         if (threadIdx.x == 0)
-            b0_s = mi ? (uint32_t)kSizeBins : size_bin(kBigCrcMin);
+            b0_s = mi ? (md5_bin ? md5_bin : (uint32_t)kSizeBins) : size_bin(kBigCrcMin);
     } else {
         // thread t: bins 2t, 2t + 1, both of exponent t >> 4
         const int t = threadIdx.x;
@@ -635,7 +635,7 @@ __global__ __launch_bounds__(1024) void big_plan_kernel(
     __syncthreads();
     const uint32_t b0 = b0_s;
     if (threadIdx.x == 0)
-        *big_min = b0 >= (uint32_t)kSizeBins ? ~0ull : 1ull << (b0 >> 5);
+        *big_min = b0 >= (uint32_t)kSizeBins ? ~0ull : bin_lo((int)b0);  // sizes in bins >= b0
     uint32_t cnt = 0;
     for (uint32_t b = b0 + threadIdx.x; b < kSizeBins; b += blockDim.x)
         cnt += hist[b];
@@ -788,14 +788,23 @@ hipError_t launch_sig_lane(bool sar, int method, const uint8_t *base, const uint
     bin_scatter_kernel<<<hb, 1024, 0, st>>>(sizes, n, cursor, order);
     const bool offload = big != nullptr;
     if (offload) {  // CRC (HASH: simple_hash, Time33 too) of the files >= T by the segmented kernels, first
-        big_plan_kernel<<<1, 1024, 0, st>>>(hist, order, offs, sizes, n, method, big->lat_files, big->nbig,
-                                            big->big_min, big->offs, big->sizes, big->seg_first, big->crc,
-                                            big->poly);
+        big_plan_kernel<<<1, 1024, 0, st>>>(hist, order, offs, sizes, n, method, big->lat_files, big->md5_bin,
+                                            big->nbig, big->big_min, big->offs, big->sizes, big->seg_first,
+                                            big->crc, big->poly);
+        hipStream_t ss = st;
+        if (big->side) {  // fork: the segmented passes beside the lane kernel
+            if ((e = hipEventRecord(big->fork, st)) != hipSuccess ||
+                (e = hipStreamWaitEvent(big->side, big->fork, 0)) != hipSuccess)
+                return e;
+            ss = big->side;
+        }
         if ((e = crc_seg_run(sar, base, big->offs, big->sizes, big->seg_first, n, big->nbig, tabs, big->crc,
-                             seg_grid, st)) != hipSuccess)
+                             seg_grid, ss)) != hipSuccess)
             return e;
         if (method == 1 && (e = launch_poly_seg(base, big->offs, big->sizes, big->seg_first, big->nbig, big->poly,
-                                                seg_grid, st)) != hipSuccess)
+                                                seg_grid, ss)) != hipSuccess)
+            return e;
+        if (big->side && (e = hipEventRecord(big->join, big->side)) != hipSuccess)
             return e;
     }
     const uint64_t *bmin = offload ? big->big_min : nullptr;
@@ -809,6 +818,8 @@ hipError_t launch_sig_lane(bool sar, int method, const uint8_t *base, const uint
         return e;
     if (ev1)
         (void)hipEventRecord(ev1, st);
+    if (offload && big->side && (e = hipStreamWaitEvent(st, big->join, 0)) != hipSuccess)
+        return e;
     if (offload && states)
         big_patch_state_kernel<<<256, 256, 0, st>>>(big->nbig, order, big->crc, big->poly, sizes, sidx,
                                                     method == 2, states, tabs);
