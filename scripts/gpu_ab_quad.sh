@@ -19,3 +19,7 @@ for v in ${VARIANTS:-0 1}; do
 done
 done
 echo done
+if [ -n "$PMC_Q" ]; then  # HBM fetch of one variant (separate pass)
+  FDFS_GPU_HASH_QUAD=$PMC_Q step fetch_q$PMC_Q 300 rocprofv3 --pmc FETCH_SIZE -d $O/fetch_q$PMC_Q -o run --output-format csv -- python3 bench.py --config c2 --no-cpu-baseline --steps 1 --warmup 1 || exit $?
+  python3 scripts/pmc_summary.py $O/fetch_q$PMC_Q 2>/dev/null | grep sig_hash | cut -c1-200
+fi
