@@ -252,26 +252,27 @@ def load_traffic(config: str, kernel: str):
     return None, None
 
 
-SQ_KERNEL = {"c2": "sig_hash_kernel<true, 0, 0>", "c3": "md5_stage_kernel<true>"}
+SQ_KERNEL = {"c2": "sig_hash_kernel<true, 0, 0", "c3": "md5_stage_kernel<true"}  # name prefixes
 
 
 def load_valu(config: str, avg_ms: float):
     """VALU issue of the dominant kernel: SQ_INSTS_VALU per launch from the
-    committed rocprofv3 --pmc pass (profiles/r01/pmc_sq_<config>.txt; the
-    count does not depend on timing) over the live kernel time, in int32
-    lane-ops/s against VALU_PEAK_TOPS."""
-    path = os.path.join(ROOT, "profiles", "r01", f"pmc_sq_{config}.txt")
-    try:
-        for line in open(path):
-            name, _, js = line.partition(" {")
-            if name.strip() == SQ_KERNEL.get(config):
-                insts = json.loads("{" + js)["SQ_INSTS_VALU"]
-                tops = insts * 64 / (avg_ms * 1e-3) / 1e12
-                return {"insts_per_launch": round(insts), "achieved_tops": round(tops, 2),
-                        "peak_tops": VALU_PEAK_TOPS, "frac": round(tops / VALU_PEAK_TOPS, 4),
-                        "source": os.path.relpath(path, ROOT)}
-    except (OSError, ValueError, KeyError):
-        pass
+    newest committed rocprofv3 --pmc pass (profiles/r02, else r01,
+    pmc_sq_<config>.txt; the count does not depend on timing) over the live
+    kernel time, in int32 lane-ops/s against VALU_PEAK_TOPS."""
+    for rnd in ("r02", "r01"):
+        path = os.path.join(ROOT, "profiles", rnd, f"pmc_sq_{config}.txt")
+        try:
+            for line in open(path):
+                name, _, js = line.partition(" {")
+                if config in SQ_KERNEL and name.strip().startswith(SQ_KERNEL[config]):
+                    insts = json.loads("{" + js)["SQ_INSTS_VALU"]
+                    tops = insts * 64 / (avg_ms * 1e-3) / 1e12
+                    return {"insts_per_launch": round(insts), "achieved_tops": round(tops, 2),
+                            "peak_tops": VALU_PEAK_TOPS, "frac": round(tops / VALU_PEAK_TOPS, 4),
+                            "source": os.path.relpath(path, ROOT)}
+        except (OSError, ValueError, KeyError):
+            pass
     return None
 
 
