@@ -105,7 +105,14 @@ constexpr int kDpChunk = kDpSplitThreads * kDpSplitPer;  // entries per K4 chunk
 static_assert(kDpChunk < 65536, "chunk digit starts are u16");
 constexpr int kDpSlotsLog = 12;  // LDS table: 4096 slots (80 KB, two workgroups per CU)
 constexpr int kDpSlots = 1 << kDpSlotsLog;
-constexpr uint32_t kDpCap = kDpSlots * 3 / 4;  // records per partition grouped in LDS
+// Records per partition grouped in LDS: two entries per thread of the
+// 1024-thread group.  At three (cap 3072) the per-thread arrays of the
+// confirmation phase went past the 64 VGPRs of two workgroups per CU and
+// hipcc spilled them to scratch, serialising the three entries' row loads
+// into three round trips.  dp_plan keeps the mean partition at <= 1536
+// records, so a uniform key spread stays far below the cap; larger
+// partitions (heavy duplication, adversarial keys) take dp_group_slow.
+constexpr uint32_t kDpCap = kDpSlots / 2;
 constexpr uint64_t kDpEmpty = ~0ull;
 constexpr int kDpGroupThreads = 1024;
 constexpr int kDpRuns = kDpGroupThreads;  // chunk runs per K5 gather batch (one per thread)
@@ -120,8 +127,8 @@ struct DpPlan {
 
 DpPlan dp_plan(uint64_t n)
 {
-    int p = 1;  // partitions of ~2K records: mean n / 2^p <= 2048
-    while (p < kDpMaxD1 + kDpMaxD2 && (n >> p) > 2048)
+    int p = 1;  // partitions of ~1.5K records: mean n / 2^p <= 1536 (kDpCap = 2048)
+    while (p < kDpMaxD1 + kDpMaxD2 && (n >> p) > 1536)
         p++;
     DpPlan pl;
     pl.d1 = p < kDpMaxD1 ? p : kDpMaxD1;
@@ -615,21 +622,28 @@ __device__ __forceinline__ void dp_group_lds(DpLds &L, const DpArgs &A, const ui
         }
     }
     // (2) confirmations of every joined entry issued together: both
-    // signature rows and both ingest indices per entry
+    // signature rows and both ingest indices per entry.  Branch-free: an
+    // entry that joined nothing reads record 0's row (one cached line per
+    // wave) and ignores it, so every entry's loads leave back to back and
+    // the wave waits once (in if-blocks hipcc waited for each entry's rows
+    // before issuing the next entry's).
     uint64_t ra[kDpEpt], rb[kDpEpt], rc[kDpEpt], oa[kDpEpt], ob[kDpEpt], oc[kDpEpt];
     uint64_t gr[kDpEpt], go[kDpEpt];
 #pragma unroll
     for (int k = 0; k < kDpEpt; k++) {
         const uint32_t r = (uint32_t)en[k];
+        const uint32_t l = threadIdx.x + k * kDpGroupThreads;
+        const bool jn = l < cnt && own[k] != r;
+        const uint32_t x = jn ? r : 0u, y = jn ? own[k] : 0u;
         if constexpr (PROBE & 1) {
             ra[k] = rb[k] = rc[k] = oa[k] = ob[k] = oc[k] = 0;
             gr[k] = r;
             go[k] = own[k];
-        } else if (own[k] != r) {
-            load_sig(A.sig + (uint64_t)r * A.stride, ra[k], rb[k], rc[k]);
-            load_sig(A.sig + (uint64_t)own[k] * A.stride, oa[k], ob[k], oc[k]);
-            gr[k] = gidx_of(A.rep_out, A.sig, A.stride, GM, r);
-            go[k] = gidx_of(A.rep_out, A.sig, A.stride, GM, own[k]);
+        } else {
+            load_sig(A.sig + (uint64_t)x * A.stride, ra[k], rb[k], rc[k]);
+            load_sig(A.sig + (uint64_t)y * A.stride, oa[k], ob[k], oc[k]);
+            gr[k] = gidx_of(A.rep_out, A.sig, A.stride, GM, x);
+            go[k] = gidx_of(A.rep_out, A.sig, A.stride, GM, y);
         }
     }
 #pragma unroll
