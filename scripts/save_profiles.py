@@ -73,6 +73,8 @@ def main(src, dst):
             continue
         pm = {}
         for kind in ("fetch", "write"):
+            if not os.path.isdir(os.path.join(src, f"{kind}_{c}")):
+                continue  # no PMC pass for this config in this run: keep the committed one
             d = load(os.path.join(src, f"{kind}_{c}"))
             with open(os.path.join(dst, f"pmc_{kind}_{c}.txt"), "w") as out:
                 for k, v in d.items():
@@ -99,6 +101,8 @@ def main(src, dst):
             for k, v in sq.items():
                 if "fdfs::" in k:
                     out.write(f"{short(k)} {json.dumps(v)}\n")
+    if not any(os.path.exists(os.path.join(src, f"probe_c2_mode{m}.log")) for m in (1, 2)):
+        return
     with open(os.path.join(dst, "probes_c2.txt"), "w") as out:
         for m in (1, 2):
             log = os.path.join(src, f"probe_c2_mode{m}.log")
