@@ -1289,7 +1289,7 @@ int fdfs_gpu_recovery_batch(fdfs_gpu_ctx *ctx, const fdfs_gpu_batch *batch, int 
     hipStream_t st = reinterpret_cast<hipStream_t>(stream);
     if (n == 0) {
         for (const fdfs_gpu_routed *r : sets)
-            if (hipMemsetAsync(r->group_start, 0, 8ull * (group_count + 1), st) != hipSuccess)
+            if (fdfs::launch_zero_u32(r->group_start, 2ull * (group_count + 1), st) != hipSuccess)
                 return fail(ctx, hipGetLastError(), "recovery_batch memset");
         return 0;
     }

@@ -1063,9 +1063,9 @@ hipError_t launch_dedup_bucket(const uint8_t *sig, const uint64_t *gidx, uint64_
                                hipEvent_t ev0, hipEvent_t ev1)
 {
     hipError_t e;
-    if ((e = hipMemsetAsync(counts_out, 0, nranks * sizeof(uint64_t), st)) != hipSuccess)
+    if ((e = launch_zero_u32(counts_out, 2ull * nranks, st)) != hipSuccess)
         return e;
-    if ((e = hipMemsetAsync(cursor, 0, nranks * sizeof(uint64_t), st)) != hipSuccess)
+    if ((e = launch_zero_u32(cursor, 2ull * nranks, st)) != hipSuccess)
         return e;
     if (n == 0)
         return hipSuccess;

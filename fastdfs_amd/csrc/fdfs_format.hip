@@ -339,7 +339,7 @@ hipError_t launch_fdht_route(bool sar, const uint8_t *keys, uint32_t stride, con
                              uint32_t *server_out, uint32_t *gcount, uint64_t *start,
                              uint64_t *cursor, uint64_t *order, hipStream_t st)
 {
-    hipError_t e = hipMemsetAsync(gcount, 0, sizeof(uint32_t) * group_count, st);
+    hipError_t e = launch_zero_u32(gcount, group_count, st);
     if (e != hipSuccess)
         return e;
     if (n && sar)
@@ -412,7 +412,7 @@ hipError_t launch_sources(const uint64_t *rep, uint64_t n, const uint8_t *sig, c
 hipError_t launch_scrub(const uint32_t *crc, const uint32_t *expect, uint32_t n, uint8_t *bad,
                         uint32_t *nbad, hipStream_t st)
 {
-    hipError_t e = hipMemsetAsync(nbad, 0, sizeof(uint32_t), st);
+    hipError_t e = launch_zero_u32(nbad, 1, st);
     if (e != hipSuccess)
         return e;
     scrub_kernel<<<blocks(n, 256), 256, 0, st>>>(crc, expect, n, bad, nbad);

@@ -16,6 +16,9 @@ constexpr int kLaneWsDwords = 2 * kSizeBins + 64;  // size-bin histogram + curso
 
 // signature path (fdfs_sig.hip)
 uint64_t scan_workspace_elems(uint64_t n);
+// Zero n dwords on st with a kernel (ordered like any kernel node when the
+// sequence is captured in a hipGraph; see zero_u32_kernel).
+hipError_t launch_zero_u32(void *p, uint64_t ndwords, hipStream_t st);
 hipError_t launch_exclusive_scan(const uint64_t *in, uint64_t n, uint64_t *out, uint64_t *bsum,
                                  hipStream_t st);
 // Lane paths: files of at least a threshold T get their CRC (and for HASH

@@ -753,11 +753,29 @@ __global__ void big_patch_state_kernel(const uint32_t *__restrict__ nbig, const 
 
 // ------------------------------------------------------------------ launchers
 
+// Zeroing as a kernel rather than hipMemsetAsync: inside a captured hipGraph
+// a kernel node is ordered like every other node of the chain, and the lane
+// path's size histogram must be zero before bin_hist_kernel counts into it.
+__global__ void zero_u32_kernel(uint32_t *__restrict__ p, uint64_t n)
+{
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x)
+        p[i] = 0;
+}
+
+hipError_t launch_zero_u32(void *p, uint64_t ndwords, hipStream_t st)
+{
+    if (ndwords == 0)
+        return hipSuccess;
+    uint64_t g = (ndwords + 255) / 256;
+    zero_u32_kernel<<<(unsigned)(g < 4096 ? g : 4096), 256, 0, st>>>(static_cast<uint32_t *>(p), ndwords);
+    return hipGetLastError();
+}
+
 hipError_t launch_exclusive_scan(const uint64_t *in, uint64_t n, uint64_t *out, uint64_t *bsum,
                                  hipStream_t st)
 {
     if (n == 0)
-        return hipMemsetAsync(out, 0, sizeof(uint64_t), st);
+        return launch_zero_u32(out, 2, st);
     const uint64_t nb = (n + kScanTile - 1) / kScanTile;
     scan_reduce_kernel<<<(unsigned)nb, kScanBlock, 0, st>>>(in, n, bsum);
     scan_sums_kernel<<<1, kScanBlock, 0, st>>>(bsum, nb);
@@ -778,7 +796,7 @@ hipError_t launch_sig_lane(bool sar, int method, const uint8_t *base, const uint
                            const uint32_t *sidx, unsigned seg_grid, hipStream_t st,
                            hipEvent_t ev0, hipEvent_t ev1)
 {
-    hipError_t e = hipMemsetAsync(hist, 0, sizeof(uint32_t) * kLaneWsDwords, st);
+    hipError_t e = launch_zero_u32(hist, kLaneWsDwords, st);
     if (e != hipSuccess)
         return e;
     uint32_t *cursor = hist + kSizeBins;

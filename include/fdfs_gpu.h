@@ -98,10 +98,10 @@ int fdfs_gpu_close(fdfs_gpu_ctx *ctx);
 
 /* Reserve device workspace for batches of up to max_files files and
  * dedup of up to max_records records, so later calls do no allocation
- * and issue no host synchronisation.  Optional: calls grow it on demand.
- * Stream capture into a hipGraph is verified for the CRC-only batch
- * (tests/test_gpu_graph.py); a captured HASH batch + dedup faulted on its
- * second replay in round-2 testing and is not supported under capture. */
+ * and issue no host synchronisation: a fixed-shape sequence of calls on one
+ * stream can then be captured in a hipGraph and replayed
+ * (tests/test_gpu_graph.py: sig_batch of every method + dedup, replayed
+ * over changing bytes).  Optional: calls grow it on demand. */
 int fdfs_gpu_reserve(fdfs_gpu_ctx *ctx, uint64_t max_files, uint64_t max_records);
 
 /* Per-file CRC32 (always, as uploads do: storage/storage_service.c:4533) and,

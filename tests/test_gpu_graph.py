@@ -1,18 +1,18 @@
 """GPU: the batch calls captured in a hipGraph (include/fdfs_gpu.h,
 fdfs_gpu_reserve: "later calls do no allocation and can be captured").
 
-A daemon that hashes one batch shape per dio wakeup can record the step
-once and replay it.  The test captures sig_batch on one stream with
-torch.cuda.graph (hipGraph underneath), replays the graph, overwrites the
-batch bytes in place and replays again: both replays must equal the oracle
-for the bytes present at replay time (the graph recomputes, nothing is
-cached), and must equal the eager call.
+A daemon that hashes one batch shape per dio wakeup can record the whole
+upload-path step once (signature batch + dedup of its signatures) and
+replay it.  The test captures sig_batch (CRC only, HASH, MD5) and dedup on
+one stream with torch.cuda.graph (hipGraph underneath), replays the graph,
+overwrites the batch bytes in place and replays again: both replays must
+equal the oracle for the bytes present at replay time (the graph recomputes,
+nothing is cached), and must equal the eager calls.
 
-Only the CRC-only batch (the check_file_duplicate=0 default) is covered: in
-round 2 the HASH batch + dedup sequence replayed correctly once and then
-faulted (illegal address) on a second replay over new bytes; the cause is
-not found yet, so that sequence is not claimed to be
-capture-safe and is not run here.
+History: with the lane path's size histogram cleared by hipMemsetAsync, the
+captured HASH batch + dedup replayed correctly once and faulted (illegal
+address) on the second replay; every zeroing in the library is now a
+kernel (launch_zero_u32), and the sequence replays exactly.
 """
 import numpy as np
 import pytest
@@ -50,7 +50,7 @@ def _bytes(rng, offs, sizes, total):
     return buf
 
 
-@pytest.mark.parametrize("method", [0])
+@pytest.mark.parametrize("method", [0, 1, 2])
 def test_sig_batch_and_dedup_replay_in_graph(oracle, ctx, method):
     import fastdfs_amd as F
     rng = np.random.default_rng(4242 + method)
