@@ -465,11 +465,13 @@ __global__ __launch_bounds__(kScanBlock) void scan_reduce_kernel(const uint64_t 
 {
     __shared__ uint64_t wsum[kScanBlock / 64];
     const uint64_t b0 = (uint64_t)blockIdx.x * kScanTile + threadIdx.x * kScanItems;
-    uint64_t v = 0;
+    uint64_t vals[kScanItems], v = 0;
+#pragma unroll
+    for (int k = 0; k < kScanItems; k++)  // branch-free loads, one wait
+        vals[k] = in[b0 + k < n ? b0 + k : n - 1];
 #pragma unroll
     for (int k = 0; k < kScanItems; k++)
-        if (b0 + k < n)
-            v += in[b0 + k];
+        v += (b0 + k < n) ? vals[k] : 0;
     uint64_t tot;
     block_exclusive_scan(v, wsum, tot);
     if (threadIdx.x == 0)
@@ -502,8 +504,11 @@ __global__ __launch_bounds__(kScanBlock) void scan_apply_kernel(const uint64_t *
     uint64_t vals[kScanItems];
     uint64_t v = 0;
 #pragma unroll
+    for (int k = 0; k < kScanItems; k++)  // branch-free loads, one wait
+        vals[k] = in[b0 + k < n ? b0 + k : n - 1];
+#pragma unroll
     for (int k = 0; k < kScanItems; k++) {
-        vals[k] = (b0 + k < n) ? in[b0 + k] : 0;
+        vals[k] = (b0 + k < n) ? vals[k] : 0;
         v += vals[k];
     }
     uint64_t tot;
@@ -786,11 +791,55 @@ hipError_t launch_zero_u32(void *p, uint64_t ndwords, hipStream_t st)
     return hipGetLastError();
 }
 
+// Small scans (a batch's segment counts, a small dedup's [digit][tile]
+// counts) in one block: one launch instead of three.  Only up to one pass of
+// the block: a single CU moves the 63K counts of a 1M-record dedup in 38 us
+// against 21 us for the three-kernel form (profiles/r02/scan_kernels.txt).
+constexpr int kScan1Items = 16;
+constexpr uint64_t kScan1Max = 1024ull * kScan1Items;
+
+__global__ __launch_bounds__(1024) void scan_single_kernel(const uint64_t *__restrict__ in, uint64_t n,
+                                                           uint64_t *__restrict__ out)
+{
+    __shared__ uint64_t wsum[1024 / 64];
+    uint64_t carry = 0;
+    for (uint64_t c0 = 0; c0 < n; c0 += 1024 * kScan1Items) {
+        const uint64_t b0 = c0 + (uint64_t)threadIdx.x * kScan1Items;
+        // branch-free loads (clamped index, masked value): all of a thread's
+        // loads leave together instead of one round trip per item
+        uint64_t vals[kScan1Items];
+        uint64_t v = 0;
+#pragma unroll
+        for (int k = 0; k < kScan1Items; k++)
+            vals[k] = in[b0 + k < n ? b0 + k : n - 1];
+#pragma unroll
+        for (int k = 0; k < kScan1Items; k++) {
+            vals[k] = (b0 + k < n) ? vals[k] : 0;
+            v += vals[k];
+        }
+        uint64_t tot;
+        uint64_t run = carry + block_exclusive_scan(v, wsum, tot);
+#pragma unroll
+        for (int k = 0; k < kScan1Items; k++) {
+            if (b0 + k < n)
+                out[b0 + k] = run;
+            run += vals[k];
+        }
+        carry += tot;
+    }
+    if (threadIdx.x == 0)
+        out[n] = carry;
+}
+
 hipError_t launch_exclusive_scan(const uint64_t *in, uint64_t n, uint64_t *out, uint64_t *bsum,
                                  hipStream_t st)
 {
     if (n == 0)
         return launch_zero_u32(out, 2, st);
+    if (n <= kScan1Max) {
+        scan_single_kernel<<<1, 1024, 0, st>>>(in, n, out);
+        return hipGetLastError();
+    }
     const uint64_t nb = (n + kScanTile - 1) / kScanTile;
     scan_reduce_kernel<<<(unsigned)nb, kScanBlock, 0, st>>>(in, n, bsum);
     scan_sums_kernel<<<1, kScanBlock, 0, st>>>(bsum, nb);
