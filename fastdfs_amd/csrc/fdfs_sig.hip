@@ -478,18 +478,32 @@ __global__ __launch_bounds__(kScanBlock) void scan_reduce_kernel(const uint64_t 
         bsum[blockIdx.x] = tot;
 }
 
-__global__ __launch_bounds__(kScanBlock) void scan_sums_kernel(uint64_t *__restrict__ bsum,
-                                                               uint64_t nb)
+// One block of 1024 threads, 4 sums per thread per pass (a 1.5K-sum scan is
+// one pass: 11.3 us with 256 threads and one sum per thread per pass).
+__global__ __launch_bounds__(1024) void scan_sums_kernel(uint64_t *__restrict__ bsum, uint64_t nb)
 {
-    __shared__ uint64_t wsum[kScanBlock / 64];
+    constexpr int kI = 4;
+    __shared__ uint64_t wsum[1024 / 64];
     uint64_t carry = 0;
-    for (uint64_t c0 = 0; c0 < nb; c0 += kScanBlock) {
-        const uint64_t i = c0 + threadIdx.x;
-        const uint64_t v = (i < nb) ? bsum[i] : 0;
+    for (uint64_t c0 = 0; c0 < nb; c0 += 1024 * kI) {
+        const uint64_t b0 = c0 + (uint64_t)threadIdx.x * kI;
+        uint64_t vals[kI], v = 0;
+#pragma unroll
+        for (int k = 0; k < kI; k++)
+            vals[k] = bsum[b0 + k < nb ? b0 + k : nb - 1];
+#pragma unroll
+        for (int k = 0; k < kI; k++) {
+            vals[k] = (b0 + k < nb) ? vals[k] : 0;
+            v += vals[k];
+        }
         uint64_t tot;
-        const uint64_t ex = block_exclusive_scan(v, wsum, tot);
-        if (i < nb)
-            bsum[i] = carry + ex;
+        uint64_t run = carry + block_exclusive_scan(v, wsum, tot);
+#pragma unroll
+        for (int k = 0; k < kI; k++) {
+            if (b0 + k < nb)
+                bsum[b0 + k] = run;
+            run += vals[k];
+        }
         carry += tot;
     }
 }
@@ -842,7 +856,7 @@ hipError_t launch_exclusive_scan(const uint64_t *in, uint64_t n, uint64_t *out, 
     }
     const uint64_t nb = (n + kScanTile - 1) / kScanTile;
     scan_reduce_kernel<<<(unsigned)nb, kScanBlock, 0, st>>>(in, n, bsum);
-    scan_sums_kernel<<<1, kScanBlock, 0, st>>>(bsum, nb);
+    scan_sums_kernel<<<1, 1024, 0, st>>>(bsum, nb);
     scan_apply_kernel<<<(unsigned)nb, kScanBlock, 0, st>>>(in, n, bsum, out);
     return hipGetLastError();
 }
