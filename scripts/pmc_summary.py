@@ -13,17 +13,21 @@ import sys
 from collections import defaultdict
 
 
-def load(root):
-    acc = defaultdict(lambda: defaultdict(float))
-    disp = defaultdict(set)
+def load(root, how="mean"):
+    """Per kernel and counter: the mean over its dispatches, or (how="max")
+    the largest dispatch's value (config 3's bench also runs the MD5 kernel
+    on its largest file alone for the chain floor; those one-file dispatches
+    would halve a mean)."""
+    per = defaultdict(lambda: defaultdict(lambda: defaultdict(float)))
     for f in glob.glob(os.path.join(root, "**", "*counter_collection.csv"), recursive=True):
         for row in csv.DictReader(open(f)):
-            k = row["Kernel_Name"]
-            acc[k][row["Counter_Name"]] += float(row["Counter_Value"])
-            disp[(k, row["Counter_Name"])].add(row["Dispatch_Id"])
+            per[row["Kernel_Name"]][row["Counter_Name"]][row["Dispatch_Id"]] += float(row["Counter_Value"])
     out = {}
-    for k, cs in acc.items():
-        out[k] = {c: v / max(1, len(disp[(k, c)])) for c, v in cs.items()}
+    for k, cs in per.items():
+        if how == "max":
+            out[k] = {c: max(d.values()) for c, d in cs.items()}
+        else:
+            out[k] = {c: sum(d.values()) / max(1, len(d)) for c, d in cs.items()}
     return out
 
 

@@ -14,7 +14,7 @@ sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
 from pmc_summary import load  # noqa: E402
 
 BENCH_KERNEL = {"c2": ("sig_hash_kernel<true, 0, 0, false", "sig_hash_kernel<SAR>"),
-                "c3": ("md5_stage_kernel<true>", "md5_stage_kernel<SAR>"),
+                "c3": ("md5_stage_kernel<true", "md5_stage_kernel<SAR>"),
                 "c4": ("crc_seg_kernel<true, 2>", "crc_seg_kernel<SAR,2>")}
 
 
@@ -75,7 +75,7 @@ def main(src, dst):
         for kind in ("fetch", "write"):
             if not os.path.isdir(os.path.join(src, f"{kind}_{c}")):
                 continue  # no PMC pass for this config in this run: keep the committed one
-            d = load(os.path.join(src, f"{kind}_{c}"))
+            d = load(os.path.join(src, f"{kind}_{c}"), "max" if c == "c3" else "mean")
             with open(os.path.join(dst, f"pmc_{kind}_{c}.txt"), "w") as out:
                 for k, v in d.items():
                     if "fdfs::" in k:
