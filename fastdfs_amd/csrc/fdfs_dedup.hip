@@ -329,8 +329,12 @@ __global__ __launch_bounds__(256) void dp_chunks_kernel(const uint64_t *__restri
 
 // K3b: for every non-empty (digit, tile) run, the chunks of that bucket whose
 // first position falls inside it start at that tile.
+// Each chunk also gets its descriptor {P0 lo, P0 hi, m, b | last << 31}
+// (first position, entry count, bucket, last chunk of its bucket), so that
+// dp_split starts with one round of independent loads.
 __global__ void dp_chunk_ta_kernel(const uint64_t *__restrict__ off1, uint64_t tiles, uint64_t ncnt,
-                                   const uint32_t *__restrict__ cb, uint32_t *__restrict__ chunk_ta)
+                                   const uint32_t *__restrict__ cb, uint32_t *__restrict__ chunk_ta,
+                                   uint4 *__restrict__ chunk_hd)
 {
     for (uint64_t idx = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; idx < ncnt;
          idx += (uint64_t)gridDim.x * blockDim.x) {
@@ -338,9 +342,14 @@ __global__ void dp_chunk_ta_kernel(const uint64_t *__restrict__ off1, uint64_t t
         if (o2 <= o)
             continue;
         const uint64_t b = idx / tiles, t = idx - b * tiles;
-        const uint64_t bs = off1[b * tiles];
-        for (uint64_t k = (o - bs + kDpChunk - 1) / kDpChunk; bs + k * kDpChunk < o2; k++)
+        const uint64_t bs = off1[b * tiles], be = off1[(b + 1) * tiles];
+        for (uint64_t k = (o - bs + kDpChunk - 1) / kDpChunk; bs + k * kDpChunk < o2; k++) {
+            const uint64_t P0 = bs + k * kDpChunk;
+            const uint64_t m = be - P0 < (uint64_t)kDpChunk ? be - P0 : (uint64_t)kDpChunk;
+            const uint32_t last = P0 + kDpChunk >= be ? 1u : 0u;
             chunk_ta[cb[b] + k] = (uint32_t)t;
+            chunk_hd[cb[b] + k] = make_uint4((uint32_t)P0, (uint32_t)(P0 >> 32), (uint32_t)m, (uint32_t)b | last << 31);
+        }
     }
 }
 
@@ -358,7 +367,7 @@ template <int NB>
 __global__ __launch_bounds__(kDpSplitThreads) void dp_split_kernel(
     const uint64_t *__restrict__ ent1, int d1, int d2, uint64_t tiles, const uint64_t *__restrict__ off1,
     const uint32_t *__restrict__ loc1, const uint32_t *__restrict__ cb, const uint32_t *__restrict__ chunk_ta,
-    uint64_t *__restrict__ ent2, uint16_t *__restrict__ cdo)
+    const uint4 *__restrict__ chunk_hd, uint64_t *__restrict__ ent2, uint16_t *__restrict__ cdo)
 {
     constexpr int NT = kDpSplitThreads;
     constexpr int PER = NB / NT;
@@ -368,24 +377,23 @@ __global__ __launch_bounds__(kDpSplitThreads) void dp_split_kernel(
     __shared__ uint32_t cl[NB];        // chunk digit starts
     __shared__ uint32_t wsum[NT / 64];
     __shared__ int32_t wmax[NT / 64];
-    __shared__ uint32_t sbk;
     const uint32_t nb1 = 1u << d1, nd2 = 1u << d2;
     const uint32_t g = blockIdx.x;
-    if (g >= cb[nb1])  // past the last chunk (the grid is a bound)
+    // one round of independent loads: the chunk count, this chunk's
+    // descriptor and tile range (read before the bound check; unused past it)
+    const uint32_t nch = cb[nb1];
+    const uint4 hd = chunk_hd[g];
+    const uint32_t ta = chunk_ta[g], tn = chunk_ta[g + 1 < gridDim.x ? g + 1 : g];
+    if (g >= nch)  // past the last chunk (the grid is a bound)
         return;
-    if (threadIdx.x < nb1 && cb[threadIdx.x] <= g && g < cb[threadIdx.x + 1])
-        sbk = threadIdx.x;
-    for (uint32_t k = threadIdx.x; k < nd2; k += NT)
-        cc[k] = 0;
-    __syncthreads();
-    const uint32_t b = sbk;
+    const uint32_t b = hd.w & 0x7FFFFFFFu;
+    const uint64_t P0 = (uint64_t)hd.x | (uint64_t)hd.y << 32;
+    const uint32_t m = hd.z;
+    const uint32_t tb = (hd.w >> 31) ? (uint32_t)(tiles - 1) : tn;
     const uint64_t *ob = off1 + (uint64_t)b * tiles;
     const uint32_t *lb = loc1 + (uint64_t)b * tiles;
-    const uint64_t bs = ob[0], be = ob[tiles];
-    const uint64_t P0 = bs + (uint64_t)(g - cb[b]) * kDpChunk;
-    const uint32_t m = (uint32_t)((be - P0) < (uint64_t)kDpChunk ? (be - P0) : (uint64_t)kDpChunk);
-    const uint32_t ta = chunk_ta[g];
-    const uint32_t tb = (g + 1 < cb[b + 1]) ? chunk_ta[g + 1] : (uint32_t)(tiles - 1);
+    for (uint32_t k = threadIdx.x; k < nd2; k += NT)
+        cc[k] = 0;
     for (uint32_t i = threadIdx.x; i < m; i += NT)
         buf[i] = kDpNoMark;
     __syncthreads();
@@ -863,7 +871,8 @@ uint64_t dedup_ws_bytes(uint64_t n)
     const DpPlan pl = dp_plan(n);
     const uint64_t ncnt = pl.ncnt();
     return al(8 * n) + al(8 * n) + al(8 * (ncnt + 1)) + al(8 * (ncnt + 1)) + al(8 * scan_workspace_elems(ncnt)) +
-           al(4 * ncnt) + al(4 * ((1ull << pl.d1) + 1)) + al(4 * pl.chunks) + al((2 * pl.chunks) << pl.d2) +
+           al(4 * ncnt) + al(4 * ((1ull << pl.d1) + 1)) + al(4 * pl.chunks) + al(16 * pl.chunks) +
+           al((2 * pl.chunks) << pl.d2) +
            al(16 * n) + al(16 * n) + al(8 * n) + al(4 * (pl.nparts() + 1));
 }
 
@@ -897,6 +906,7 @@ hipError_t launch_dedup_group(const uint8_t *sig, uint32_t sig_stride, const uin
     uint32_t *loc1 = reinterpret_cast<uint32_t *>(take(4 * ncnt));
     uint32_t *cb = reinterpret_cast<uint32_t *>(take(4 * ((1ull << pl.d1) + 1)));
     uint32_t *chunk_ta = reinterpret_cast<uint32_t *>(take(4 * pl.chunks));
+    uint4 *chunk_hd = reinterpret_cast<uint4 *>(take(16 * pl.chunks));
     uint16_t *cdo = reinterpret_cast<uint16_t *>(take((2 * pl.chunks) << pl.d2));
     uint64_t *gword = reinterpret_cast<uint64_t *>(take(16 * n));  // oversized-partition tables
     uint64_t *gmin = reinterpret_cast<uint64_t *>(take(16 * n));
@@ -911,13 +921,13 @@ hipError_t launch_dedup_group(const uint8_t *sig, uint32_t sig_stride, const uin
     if ((e = launch_exclusive_scan(cnt1, ncnt, off1, bsum, st)) != hipSuccess)
         return e;
     dp_chunks_kernel<<<1, 256, 0, st>>>(off1, pl.d1, pl.tiles, cb, slow);
-    dp_chunk_ta_kernel<<<grid_for(ncnt, 256), 256, 0, st>>>(off1, pl.tiles, ncnt, cb, chunk_ta);
+    dp_chunk_ta_kernel<<<grid_for(ncnt, 256), 256, 0, st>>>(off1, pl.tiles, ncnt, cb, chunk_ta, chunk_hd);
     if (pl.d2 <= 10)
         dp_split_kernel<1024><<<(unsigned)pl.chunks, kDpSplitThreads, 0, st>>>(ent1, pl.d1, pl.d2, pl.tiles, off1,
-                                                                              loc1, cb, chunk_ta, ent2, cdo);
+                                                                              loc1, cb, chunk_ta, chunk_hd, ent2, cdo);
     else
         dp_split_kernel<1 << kDpMaxD2><<<(unsigned)pl.chunks, kDpSplitThreads, 0, st>>>(
-            ent1, pl.d1, pl.d2, pl.tiles, off1, loc1, cb, chunk_ta, ent2, cdo);
+            ent1, pl.d1, pl.d2, pl.tiles, off1, loc1, cb, chunk_ta, chunk_hd, ent2, cdo);
     const int gmode = !gidx_stride ? GM_INDEX
                       : (gidx == reinterpret_cast<const uint64_t *>(sig + 24) && 8 * gidx_stride == sig_stride)
                           ? GM_ROW
