@@ -51,6 +51,7 @@ EXPORTS = (
     "fdfs_gpu_final_batch",
     "fdfs_gpu_crc_combine",
     "fdfs_gpu_dedup_global",
+    "fdfs_gpu_dedup_global_local",
     "fdfs_gpu_comm_unique_id",
     "fdfs_gpu_comm_init",
     "fdfs_gpu_comm_destroy",
@@ -156,6 +157,8 @@ def load() -> ctypes.CDLL:
     L.fdfs_gpu_crc_combine.argtypes = [vp, vp, vp, vp, u32, vp, vp]
     L.fdfs_gpu_dedup_global.restype = i32
     L.fdfs_gpu_dedup_global.argtypes = [vp, vp, vp, vp, u64, vp, vp, vp]
+    L.fdfs_gpu_dedup_global_local.restype = i32
+    L.fdfs_gpu_dedup_global_local.argtypes = [vp, i32, vp, vp, vp, vp, vp, vp]
     L.fdfs_gpu_comm_unique_id.restype = i32
     L.fdfs_gpu_comm_unique_id.argtypes = [ctypes.c_char_p]
     L.fdfs_gpu_comm_init.restype = i32

@@ -286,12 +286,39 @@ class Context:
         grouped across every rank of `comm` over RCCL; (rep int64[n], ref
         int32[n]) for this rank's records (collective: all ranks call)."""
         n = _check_sig(sig, gidx)
+        if gidx is None and comm.world > 1 and n:
+            raise ValueError("dedup_global over more than one rank needs each record's global ingest index")
         rep = torch.empty(n, dtype=torch.int64, device=sig.device)
         ref = torch.empty(n, dtype=torch.int32, device=sig.device)
         self._rc(self._L.fdfs_gpu_dedup_global(self._h, comm.handle, sig.data_ptr(), _ptr(gidx), n,
                                                rep.data_ptr(), ref.data_ptr(), _stream_handle(stream)),
                  "fdfs_gpu_dedup_global")
         return rep, ref
+
+    def dedup_global_local(self, sigs: list, gidxs: list, stream=None):
+        """fdfs_gpu_dedup_global_local: len(sigs) VIRTUAL ranks on this
+        device, rank p holding sigs[p] (uint8[n_p, 24]) with global ingest
+        indices gidxs[p] (int64[n_p]); the RCCL form's bucket, exchange plan,
+        group and answer routing with every segment moved by a device copy.
+        Returns [(rep int64[n_p], ref int32[n_p])] per rank (synchronous)."""
+        nr = len(sigs)
+        if not 1 <= nr <= 64 or len(gidxs) != nr:
+            raise ValueError("1..64 ranks, one gidx tensor per rank")
+        outs = []
+        for s, g in zip(sigs, gidxs):
+            n = _check_sig(s, g)
+            if g is None and nr > 1 and n:
+                raise ValueError("more than one rank needs each record's global ingest index")
+            outs.append((torch.empty(n, dtype=torch.int64, device=s.device),
+                         torch.empty(n, dtype=torch.int32, device=s.device)))
+        P = ctypes.c_void_p * nr
+        U = ctypes.c_uint64 * nr
+        self._rc(self._L.fdfs_gpu_dedup_global_local(
+            self._h, nr, P(*[s.data_ptr() for s in sigs]),
+            P(*[None if g is None else g.data_ptr() for g in gidxs]), U(*[s.shape[0] for s in sigs]),
+            P(*[o[0].data_ptr() for o in outs]), P(*[o[1].data_ptr() for o in outs]),
+            _stream_handle(stream)), "fdfs_gpu_dedup_global_local")
+        return outs
 
     def dedup_bucket(self, sig: torch.Tensor, gidx: torch.Tensor | None, nranks: int, stream=None):
         """Pack {sig, gidx} rows by owner rank: (rows uint8[n,32], counts int64[nranks], row_of int64[n])."""

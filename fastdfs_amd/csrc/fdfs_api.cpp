@@ -49,11 +49,14 @@ struct fdfs_gpu_ctx {
     hipEvent_t ws_ev = nullptr;
     hipStream_t ws_st = nullptr;
     bool ws_rec = false;
-    // fdfs_gpu_dedup_global: exchange buffers (ordered like ws) and the
-    // pinned per-peer row counts {send[64], recv[64]}
+    // fdfs_gpu_dedup_global: exchange buffers (ordered like ws), and the
+    // announcement words every rank all-gathers before the row exchange
+    // (device: this rank's, then all ranks'; host: tail staging, all ranks',
+    // the agreement flag), allocated at open so that no rank can fail before
+    // its first collective
     void *xa = nullptr, *xb = nullptr;
     size_t xa_bytes = 0, xb_bytes = 0;
-    uint64_t *hcounts = nullptr;
+    uint64_t *dann = nullptr, *hann = nullptr;
 };
 
 namespace {
@@ -149,6 +152,13 @@ fdfs::BigCrcWs carve_big(const fdfs_gpu_ctx *ctx, Carve &cv, uint32_t n)
 }
 
 size_t dedup_ws_bytes(uint64_t n) { return fdfs::dedup_ws_bytes(n) + align_up(8 * 64); }
+
+// fdfs_gpu_dedup_global announcement: rank p's row count per owner (nranks
+// words), then kAnnTail words {owner-side room, workspace room, errno}.
+constexpr int kAnnTail = 3;
+constexpr size_t kAnnMax = 64 + kAnnTail;                   // words of one announcement
+constexpr size_t kAnnDevWords = kAnnMax + 64 * kAnnMax + 8;  // own, all ranks', agreement flag
+constexpr size_t kAnnHostWords = 64 * kAnnTail + 64 * kAnnMax + 8;  // tails, all ranks', flag
 
 bool capturing(hipStream_t st)
 {
@@ -318,10 +328,18 @@ int fdfs_gpu_open(int device, unsigned flags, fdfs_gpu_ctx **out)
         e = hipMalloc(&ctx->d_tabs, sizeof(fdfs::DevTables));
     if (e == hipSuccess)
         e = hipMemcpy(ctx->d_tabs, h, sizeof(fdfs::DevTables), hipMemcpyHostToDevice);
+    if (e == hipSuccess)
+        e = hipMalloc(reinterpret_cast<void **>(&ctx->dann), 8 * kAnnDevWords);
+    if (e == hipSuccess)
+        e = hipHostMalloc(reinterpret_cast<void **>(&ctx->hann), 8 * kAnnHostWords, 0);
     delete h;
     if (e != hipSuccess) {
         if (ctx->d_tabs)
             (void)hipFree(ctx->d_tabs);
+        if (ctx->dann)
+            (void)hipFree(ctx->dann);
+        if (ctx->hann)
+            (void)hipHostFree(ctx->hann);
         if (ctx->ws_ev)
             (void)hipEventDestroy(ctx->ws_ev);
         if (ctx->side)
@@ -355,8 +373,10 @@ int fdfs_gpu_close(fdfs_gpu_ctx *ctx)
         (void)hipFree(ctx->xa);
     if (ctx->xb)
         (void)hipFree(ctx->xb);
-    if (ctx->hcounts)
-        (void)hipHostFree(ctx->hcounts);
+    if (ctx->dann)
+        (void)hipFree(ctx->dann);
+    if (ctx->hann)
+        (void)hipHostFree(ctx->hann);
     for (auto &r : ctx->recs) {
         (void)hipEventDestroy(r.a);
         (void)hipEventDestroy(r.b);
@@ -1020,49 +1040,268 @@ int fdfs_gpu_comm_destroy(void *comm)
     return ncclCommDestroy(static_cast<ncclComm_t>(comm)) == ncclSuccess ? 0 : EIO;
 }
 
-// One exchange: rank p receives from every rank the rows addressed to it.
-// send/recv: per-peer element counts (elements of `elem` bytes) whose
-// prefix sums place the peers' segments in sbuf / rbuf.
-static int exchange(fdfs_gpu_ctx *ctx, ncclComm_t c, int nranks, int me, const char *sbuf, const uint64_t *send,
-                    char *rbuf, const uint64_t *recv, size_t elem, hipStream_t st)
-{
-    uint64_t so = 0, ro = 0;
-    uint64_t soff[64], roff[64];
-    for (int p = 0; p < nranks; p++) {
-        soff[p] = so;
-        roff[p] = ro;
-        so += send[p];
-        ro += recv[p];
+// fdfs_gpu_dedup_global is two parts, so that its multi-rank logic also runs
+// on one GPU (fdfs_gpu_dedup_global_local):
+//  * the exchange plan (DgPlan), derived identically on every rank from all
+//    ranks' announcements, all-gathered in one collective: each rank's row
+//    count per owner, the room of its owner-side buffers and any local error.
+//    From it every (src, dst) segment's count and its offsets on both sides,
+//    each owner's row count, and the common outcome: an error on any rank is
+//    every rank's error, returned before any row moves, so no rank is left
+//    waiting in a send or receive;
+//  * the transport: one rank of an RCCL communicator (ncclAllGather, grouped
+//    ncclSend / ncclRecv, the rank's own segment by a device copy), or N
+//    virtual ranks in one process on one device (every segment a
+//    hipMemcpyAsync).
+// Bucket, group, answer pack and answer gather are the same kernels for both.
+
+extern "C++" {
+
+struct DgPlan {
+    int nranks = 0;
+    uint64_t cnt[64][64];  // cnt[p][q]: rows rank p sends to owner q
+    uint64_t m[64];        // rows owner q groups
+    int err = 0, err_rank = -1;
+    bool grow = false;     // an owner's buffers must grow: the ranks agree on the outcome first
+    // where p's rows for owner q start among p's rows (and where q's answers
+    // for them land in p's answer buffer)
+    uint64_t soff(int p, int q) const
+    {
+        uint64_t s = 0;
+        for (int k = 0; k < q; k++)
+            s += cnt[p][k];
+        return s;
     }
-    if (send[me] && hipMemcpyAsync(rbuf + roff[me] * elem, sbuf + soff[me] * elem, send[me] * elem,
-                                   hipMemcpyDeviceToDevice, st) != hipSuccess)
-        return fail(ctx, hipGetLastError(), "exchange self copy");
-    if (nranks == 1)
+    // where p's rows start among owner q's received rows (and q's answers to p)
+    uint64_t roff(int q, int p) const
+    {
+        uint64_t s = 0;
+        for (int k = 0; k < p; k++)
+            s += cnt[k][q];
+        return s;
+    }
+};
+
+static size_t dg_a_bytes(uint64_t n)
+{
+    return align_up(32 * n) + align_up(8 * n) + align_up(16 * n) + align_up(8 * 64);
+}
+
+static size_t dg_b_bytes(uint64_t m)
+{
+    return align_up(32 * m) + align_up(8 * m) + align_up(4 * m) + align_up(16 * m);
+}
+
+// ann: nranks announcements of nranks + kAnnTail words, rank p's at p.
+static void dg_plan(const uint64_t *ann, int nranks, DgPlan &pl)
+{
+    const size_t w = (size_t)nranks + kAnnTail;
+    pl.nranks = nranks;
+    for (int q = 0; q < nranks; q++)
+        pl.m[q] = 0;
+    for (int p = 0; p < nranks; p++) {
+        const uint64_t *a = ann + p * w;
+        for (int q = 0; q < nranks; q++) {
+            pl.cnt[p][q] = a[q];
+            pl.m[q] += a[q];
+        }
+        if (a[nranks + 2] && !pl.err) {
+            pl.err = (int)a[nranks + 2];
+            pl.err_rank = p;
+        }
+    }
+    for (int q = 0; q < nranks && !pl.err; q++)
+        if (pl.m[q] >= 0xFFFFFFFFull) {  // the owner's group takes a uint32 record count
+            pl.err = EINVAL;
+            pl.err_rank = q;
+        }
+    for (int q = 0; q < nranks && !pl.err; q++) {
+        const uint64_t *a = ann + q * w;
+        if (dg_b_bytes(pl.m[q]) > a[nranks] || dedup_ws_bytes(pl.m[q]) > a[nranks + 1])
+            pl.grow = true;
+    }
+}
+
+// Every segment of one exchange.  Forward: rows from rank p to owner q, p's
+// rows at soff(p, q) -> q's received rows at roff(q, p).  Back: the answers
+// from owner q to rank p, q's at roff(q, p) -> p's at soff(p, q).
+struct DgSeg {
+    int src, dst;
+    uint64_t soff, doff, count;  // elements
+};
+
+template <typename F>
+static int dg_segments(const DgPlan &pl, bool back, F &&f)
+{
+    for (int p = 0; p < pl.nranks; p++)
+        for (int q = 0; q < pl.nranks; q++) {
+            const uint64_t c = pl.cnt[p][q];
+            if (!c)
+                continue;
+            const uint64_t a = pl.soff(p, q), b = pl.roff(q, p);
+            const int rc = back ? f(DgSeg{q, p, b, a, c}) : f(DgSeg{p, q, a, b, c});
+            if (rc)
+                return rc;
+        }
+    return 0;
+}
+
+// One rank's side: its records and the buffers of both directions.
+struct DgSide {
+    const uint8_t *sig = nullptr;
+    const uint64_t *gidx = nullptr;
+    uint64_t n = 0;
+    uint64_t *rep_out = nullptr;
+    uint32_t *ref_out = nullptr;
+    uint8_t *rows = nullptr;     // [n] 32-byte rows grouped by owner
+    uint64_t *row_of = nullptr;  // [n] row of each record
+    uint64_t *back = nullptr;    // [n] {rep, ref} answers, in row order
+    uint64_t *cursor = nullptr;  // [64] bucket cursors
+    uint64_t m = 0;              // rows this rank groups as owner
+    uint8_t *rows_in = nullptr;  // [m]
+    uint64_t *rep_in = nullptr;  // [m]
+    uint32_t *ref_in = nullptr;  // [m]
+    uint64_t *ans = nullptr;     // [m] {rep, ref} for the way back
+};
+
+static void dg_carve_a(DgSide &s, void *mem)
+{
+    Carve c{static_cast<char *>(mem)};
+    s.rows = c.take<uint8_t>(32 * s.n);
+    s.row_of = c.take<uint64_t>(s.n);
+    s.back = c.take<uint64_t>(2 * s.n);
+    s.cursor = c.take<uint64_t>(64);
+}
+
+static void dg_carve_b(DgSide &s, void *mem, uint64_t m)
+{
+    Carve c{static_cast<char *>(mem)};
+    s.m = m;
+    s.rows_in = c.take<uint8_t>(32 * m);
+    s.rep_in = c.take<uint64_t>(m);
+    s.ref_in = c.take<uint32_t>(m);
+    s.ans = c.take<uint64_t>(2 * m);
+}
+
+// Argument check of one rank's share (0 or EINVAL).
+static int dg_check(const uint8_t *sig, const uint64_t *gidx, uint64_t n, const uint64_t *rep_out,
+                    const uint32_t *ref_out, int nranks)
+{
+    if (n >= 0xFFFFFFFFull)
+        return EINVAL;
+    if (n && (!sig || !rep_out || !ref_out))
+        return EINVAL;
+    // without ingest indices every rank would number its records 0..n-1 and
+    // the owners' class minimum would mix records of different ranks
+    if (n && !gidx && nranks > 1)
+        return EINVAL;
+    if ((reinterpret_cast<uintptr_t>(sig) | reinterpret_cast<uintptr_t>(gidx) |
+         reinterpret_cast<uintptr_t>(rep_out)) & 7)
+        return EINVAL;
+    return 0;
+}
+
+// Phase 1: rows by owner; the counts are the first nranks words of `ann`.
+static hipError_t dg_bucket(fdfs_gpu_ctx *ctx, DgSide &s, int nranks, uint64_t *ann, hipStream_t st)
+{
+    hipEvent_t a, b;
+    timing_pair(ctx, FDFS_KERNEL_BUCKET, a, b);
+    return fdfs::launch_dedup_bucket(s.sig, s.gidx, s.n, (uint32_t)nranks, s.rows, ann, s.cursor, s.row_of, st, a,
+                                     b);
+}
+
+// The announcement's tail {owner-side room, workspace room, errno}, staged
+// in pinned memory (`h`, untouched until the stream has copied it).
+static hipError_t dg_announce(uint64_t *ann_tail, uint64_t *h, uint64_t b_room, uint64_t ws_room, int err,
+                              hipStream_t st)
+{
+    h[0] = b_room;
+    h[1] = ws_room;
+    h[2] = (uint64_t)err;
+    return hipMemcpyAsync(ann_tail, h, 8 * kAnnTail, hipMemcpyHostToDevice, st);
+}
+
+// Phase 3: the owner groups its rows (min gidx from the rows' own word 3),
+// answers packed for the way back.
+static hipError_t dg_group(fdfs_gpu_ctx *ctx, DgSide &s, hipStream_t st)
+{
+    hipEvent_t a, b;
+    timing_pair(ctx, FDFS_KERNEL_DEDUP, a, b);
+    hipError_t e = fdfs::launch_dedup_group(s.rows_in, 32, reinterpret_cast<const uint64_t *>(s.rows_in + 24), 4, s.m,
+                                            ctx->ws, s.rep_in, s.ref_in, st, a, b);
+    if (e == hipSuccess)
+        e = fdfs::launch_answer_pack(s.rep_in, s.ref_in, s.m, s.ans, st);
+    return e;
+}
+
+// Phase 5: the answers into record order.
+static hipError_t dg_gather(DgSide &s, hipStream_t st)
+{
+    return fdfs::launch_answer_gather(s.back, s.row_of, s.n, s.rep_out, s.ref_out, st);
+}
+
+// RCCL transport of one exchange for rank `me`: its own segment by a device
+// copy, the others by one group of sends and receives.
+static int dg_nccl_exchange(fdfs_gpu_ctx *ctx, ncclComm_t c, int me, const DgPlan &pl, bool back, const void *sbuf,
+                            void *rbuf, size_t elem, hipStream_t st)
+{
+    const char *sb = static_cast<const char *>(sbuf);
+    char *rb = static_cast<char *>(rbuf);
+    hipError_t e = hipSuccess;
+    int rc = dg_segments(pl, back, [&](const DgSeg &g) -> int {
+        if (g.src != me || g.dst != me)
+            return 0;
+        e = hipMemcpyAsync(rb + g.doff * elem, sb + g.soff * elem, g.count * elem, hipMemcpyDeviceToDevice, st);
+        return e == hipSuccess ? 0 : EIO;
+    });
+    if (rc)
+        return fail(ctx, e, "exchange self copy");
+    if (pl.nranks == 1)
         return 0;
     ncclResult_t r = ncclGroupStart();
-    for (int p = 0; p < nranks && r == ncclSuccess; p++) {
-        if (p == me)
-            continue;
-        if (send[p])
-            r = ncclSend(sbuf + soff[p] * elem, send[p] * elem, ncclUint8, p, c, st);
-        if (r == ncclSuccess && recv[p])
-            r = ncclRecv(rbuf + roff[p] * elem, recv[p] * elem, ncclUint8, p, c, st);
-    }
+    if (r != ncclSuccess)
+        return nccl_fail(ctx, r, "ncclGroupStart");
+    rc = dg_segments(pl, back, [&](const DgSeg &g) -> int {
+        if (g.src == me && g.dst != me)
+            r = ncclSend(sb + g.soff * elem, g.count * elem, ncclUint8, g.dst, c, st);
+        else if (g.dst == me && g.src != me)
+            r = ncclRecv(rb + g.doff * elem, g.count * elem, ncclUint8, g.src, c, st);
+        return r == ncclSuccess ? 0 : EIO;
+    });
     const ncclResult_t r2 = ncclGroupEnd();
-    if (r != ncclSuccess || r2 != ncclSuccess)
+    if (rc || r2 != ncclSuccess)
         return nccl_fail(ctx, r != ncclSuccess ? r : r2, "exchange");
     return 0;
 }
 
+// In-process transport: every rank's buffers are on this device.
+static int dg_local_exchange(fdfs_gpu_ctx *ctx, const DgPlan &pl, bool back, const std::vector<const char *> &sbuf,
+                             const std::vector<char *> &rbuf, size_t elem, hipStream_t st)
+{
+    hipError_t e = hipSuccess;
+    const int rc = dg_segments(pl, back, [&](const DgSeg &g) -> int {
+        e = hipMemcpyAsync(rbuf[g.dst] + g.doff * elem, sbuf[g.src] + g.soff * elem, g.count * elem,
+                           hipMemcpyDeviceToDevice, st);
+        return e == hipSuccess ? 0 : EIO;
+    });
+    return rc ? fail(ctx, e, "local exchange copy") : 0;
+}
+
+static int dg_plan_error(fdfs_gpu_ctx *ctx, const DgPlan &pl, int me)
+{
+    if (pl.err_rank != me || pl.err == EINVAL)
+        std::snprintf(ctx->err, sizeof(ctx->err), "dedup_global: rank %d failed: %s", pl.err_rank,
+                      pl.err == EINVAL ? "invalid arguments or over 2^32-2 rows for one owner"
+                                       : pl.err == ENOMEM ? "out of memory" : "HIP error");
+    return pl.err;
+}
+
+}  // extern "C++"
+
 int fdfs_gpu_dedup_global(fdfs_gpu_ctx *ctx, void *comm, const uint8_t *sig, const uint64_t *gidx,
                           uint64_t n, uint64_t *rep_out, uint32_t *ref_out, void *stream)
 {
-    if (!ctx || !comm || n >= 0xFFFFFFFFull)
-        return EINVAL;
-    if (n && (!sig || !rep_out || !ref_out))
-        return EINVAL;
-    if ((reinterpret_cast<uintptr_t>(sig) | reinterpret_cast<uintptr_t>(gidx) |
-         reinterpret_cast<uintptr_t>(rep_out)) & 7)
+    if (!ctx || !comm)
         return EINVAL;
     ncclComm_t c = static_cast<ncclComm_t>(comm);
     int nranks = 0, me = 0;
@@ -1074,66 +1313,175 @@ int fdfs_gpu_dedup_global(fdfs_gpu_ctx *ctx, void *comm, const uint8_t *sig, con
     if (!g.ok)
         return ENODEV;
     hipStream_t st = reinterpret_cast<hipStream_t>(stream);
-    if (!ctx->hcounts && hipHostMalloc(reinterpret_cast<void **>(&ctx->hcounts), 2 * 64 * 8, 0) != hipSuccess)
-        return ENOMEM;
-    // this rank's side: rows by owner, their positions, the answers coming back
-    const size_t a_bytes = align_up(32 * n) + align_up(8 * n) + align_up(16 * n) + 3 * align_up(8 * 64);
-    int rc = ensure_buf(ctx, &ctx->xa, &ctx->xa_bytes, a_bytes, st);
-    if (rc)
-        return rc;
+    // A local error is announced, not returned: every rank takes part in the
+    // all-gather and all of them return it together.
+    int err = dg_check(sig, gidx, n, rep_out, ref_out, nranks);
+    if (!err)
+        err = ensure_buf(ctx, &ctx->xa, &ctx->xa_bytes, dg_a_bytes(n), st);
     WsScope wsc(ctx, st);
-    Carve ca{static_cast<char *>(ctx->xa)};
-    uint8_t *rows = ca.take<uint8_t>(32 * n);
-    uint64_t *row_of = ca.take<uint64_t>(n);
-    uint64_t *back = ca.take<uint64_t>(2 * n);
-    uint64_t *counts = ca.take<uint64_t>(64);  // send counts; recv counts follow
-    uint64_t *rcounts = ca.take<uint64_t>(64);
-    uint64_t *cursor = ca.take<uint64_t>(64);
-    hipEvent_t a, b;
-    timing_pair(ctx, FDFS_KERNEL_BUCKET, a, b);
-    hipError_t e = fdfs::launch_dedup_bucket(sig, gidx, n, (uint32_t)nranks, rows, counts, cursor, row_of, st, a, b);
-    if (e != hipSuccess)
-        return fail(ctx, e, "dedup_global bucket");
-    // 1. row counts to their owners (one u64 per peer), then to the host:
-    //    the only host synchronisation (the row exchange needs the sizes)
-    ncclResult_t r = ncclAllToAll(counts, rcounts, 1, ncclUint64, c, st);
-    if (r != ncclSuccess)
-        return nccl_fail(ctx, r, "ncclAllToAll counts");
-    if ((e = hipMemcpyAsync(ctx->hcounts, counts, 2 * 64 * 8, hipMemcpyDeviceToHost, st)) != hipSuccess ||
-        (e = hipStreamSynchronize(st)) != hipSuccess)
-        return fail(ctx, e, "dedup_global counts");
-    uint64_t send[64], recv[64], m = 0;
-    for (int p = 0; p < nranks; p++) {
-        send[p] = ctx->hcounts[p];
-        recv[p] = ctx->hcounts[64 + p];
-        m += recv[p];
+    const size_t w = (size_t)nranks + kAnnTail;
+    uint64_t *ann = ctx->dann, *all = ctx->dann + kAnnMax, *dflag = ctx->dann + kAnnMax + 64 * kAnnMax;
+    uint64_t *htail = ctx->hann, *hall = ctx->hann + 64 * kAnnTail, *hflag = hall + 64 * kAnnMax;
+    DgSide s;
+    s.sig = sig;
+    s.gidx = gidx;
+    s.n = n;
+    s.rep_out = rep_out;
+    s.ref_out = ref_out;
+    hipError_t e;
+    if (!err) {
+        dg_carve_a(s, ctx->xa);
+        if ((e = dg_bucket(ctx, s, nranks, ann, st)) != hipSuccess)
+            err = fail(ctx, e, "dedup_global bucket");
     }
-    if (m >= 0xFFFFFFFFull)
-        return EINVAL;
-    // the owner's side: received rows, their answers (packed for the way back)
-    const size_t b_bytes = align_up(32 * m) + align_up(8 * m) + align_up(4 * m) + align_up(16 * m);
-    if ((rc = ensure_buf(ctx, &ctx->xb, &ctx->xb_bytes, b_bytes, st)) ||
-        (rc = ensure_ws(ctx, dedup_ws_bytes(m), st)))
+    if (err && (e = fdfs::launch_zero_u32(ann, 2ull * nranks, st)) != hipSuccess)
+        return fail(ctx, e, "dedup_global announce");  // the device is gone; so is the exchange
+    if ((e = dg_announce(ann + nranks, htail, ctx->xb_bytes, ctx->ws_bytes, err, st)) != hipSuccess)
+        return fail(ctx, e, "dedup_global announce");
+    // 1. every rank's announcement to every rank, then to the host: the one
+    //    host synchronisation (the row exchange is sized by it)
+    ncclResult_t r = ncclAllGather(ann, all, w, ncclUint64, c, st);
+    if (r != ncclSuccess)
+        return nccl_fail(ctx, r, "ncclAllGather announcements");
+    if ((e = hipMemcpyAsync(hall, all, 8 * w * nranks, hipMemcpyDeviceToHost, st)) != hipSuccess ||
+        (e = hipStreamSynchronize(st)) != hipSuccess)
+        return fail(ctx, e, "dedup_global announcements");
+    DgPlan pl;
+    dg_plan(hall, nranks, pl);
+    if (pl.err)
+        return dg_plan_error(ctx, pl, me);
+    if (pl.grow) {
+        // some owner must grow its buffers: each grows its own, and the ranks
+        // agree on the outcome (max over ranks) before any row moves
+        int gerr = ensure_buf(ctx, &ctx->xb, &ctx->xb_bytes, dg_b_bytes(pl.m[me]), st);
+        if (!gerr)
+            gerr = ensure_ws(ctx, dedup_ws_bytes(pl.m[me]), st);
+        hflag[0] = (uint64_t)gerr;
+        if ((e = hipMemcpyAsync(dflag, hflag, 8, hipMemcpyHostToDevice, st)) != hipSuccess)
+            return fail(ctx, e, "dedup_global agreement");
+        if ((r = ncclAllReduce(dflag, dflag, 1, ncclUint64, ncclMax, c, st)) != ncclSuccess)
+            return nccl_fail(ctx, r, "ncclAllReduce agreement");
+        if ((e = hipMemcpyAsync(hflag, dflag, 8, hipMemcpyDeviceToHost, st)) != hipSuccess ||
+            (e = hipStreamSynchronize(st)) != hipSuccess)
+            return fail(ctx, e, "dedup_global agreement");
+        if (hflag[0]) {
+            if (!gerr)
+                std::snprintf(ctx->err, sizeof(ctx->err), "dedup_global: another rank could not grow its buffers");
+            return gerr ? gerr : (int)hflag[0];
+        }
+    }
+    dg_carve_b(s, ctx->xb, pl.m[me]);
+    int rc;
+    // 2. rows to their owners over xGMI, 3. group, 4. answers back, 5. gather
+    if ((rc = dg_nccl_exchange(ctx, c, me, pl, false, s.rows, s.rows_in, 32, st)))
         return rc;
-    Carve cb{static_cast<char *>(ctx->xb)};
-    uint8_t *rows_in = cb.take<uint8_t>(32 * m);
-    uint64_t *rep_in = cb.take<uint64_t>(m);
-    uint32_t *ref_in = cb.take<uint32_t>(m);
-    uint64_t *ans = cb.take<uint64_t>(2 * m);
-    // 2. rows to their owners over xGMI, 3. group, 4. answers back
-    if ((rc = exchange(ctx, c, nranks, me, reinterpret_cast<const char *>(rows), send,
-                       reinterpret_cast<char *>(rows_in), recv, 32, st)))
-        return rc;
-    timing_pair(ctx, FDFS_KERNEL_DEDUP, a, b);
-    if ((e = fdfs::launch_dedup_group(rows_in, 32, reinterpret_cast<const uint64_t *>(rows_in + 24), 4, m, ctx->ws,
-                                      rep_in, ref_in, st, a, b)) != hipSuccess ||
-        (e = fdfs::launch_answer_pack(rep_in, ref_in, m, ans, st)) != hipSuccess)
+    if ((e = dg_group(ctx, s, st)) != hipSuccess)
         return fail(ctx, e, "dedup_global group");
-    if ((rc = exchange(ctx, c, nranks, me, reinterpret_cast<const char *>(ans), recv,
-                       reinterpret_cast<char *>(back), send, 16, st)))
+    if ((rc = dg_nccl_exchange(ctx, c, me, pl, true, s.ans, s.back, 16, st)))
         return rc;
-    e = fdfs::launch_answer_gather(back, row_of, n, rep_out, ref_out, st);
+    e = dg_gather(s, st);
     return e == hipSuccess ? 0 : fail(ctx, e, "dedup_global gather");
+}
+
+int fdfs_gpu_dedup_global_local(fdfs_gpu_ctx *ctx, int nranks, const uint8_t *const *sig,
+                                const uint64_t *const *gidx, const uint64_t *n, uint64_t *const *rep_out,
+                                uint32_t *const *ref_out, void *stream)
+{
+    if (!ctx || nranks < 1 || nranks > 64 || !sig || !n || !rep_out || !ref_out || (nranks > 1 && !gidx))
+        return EINVAL;
+    for (int p = 0; p < nranks; p++)
+        if (dg_check(sig[p], gidx ? gidx[p] : nullptr, n[p], rep_out[p], ref_out[p], nranks))
+            return EINVAL;
+    std::lock_guard<std::recursive_mutex> lk(ctx->mu);
+    DeviceGuard g(ctx->device);
+    if (!g.ok)
+        return ENODEV;
+    hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+    if (capturing(st)) {
+        std::snprintf(ctx->err, sizeof(ctx->err), "dedup_global_local synchronises; not capturable");
+        return EINVAL;
+    }
+    WsScope wsc(ctx, st);
+    const size_t w = (size_t)nranks + kAnnTail;
+    uint64_t *all = ctx->dann + kAnnMax;
+    uint64_t *htail = ctx->hann, *hall = ctx->hann + 64 * kAnnTail;
+    std::vector<DgSide> s(nranks);
+    size_t abytes = 0;
+    for (int p = 0; p < nranks; p++)
+        abytes += dg_a_bytes(n[p]);
+    void *amem = nullptr, *bmem = nullptr;
+    hipError_t e = hipMalloc(&amem, abytes);
+    if (e != hipSuccess) {
+        std::snprintf(ctx->err, sizeof(ctx->err), "hipMalloc(%zu): %s", abytes, hipGetErrorString(e));
+        return ENOMEM;
+    }
+    int rc = 0;
+    DgPlan pl;
+    size_t done = 0;
+    for (int p = 0; p < nranks && !rc; p++) {
+        s[p].sig = sig[p];
+        s[p].gidx = gidx ? gidx[p] : nullptr;
+        s[p].n = n[p];
+        s[p].rep_out = rep_out[p];
+        s[p].ref_out = ref_out[p];
+        dg_carve_a(s[p], static_cast<char *>(amem) + done);
+        done += dg_a_bytes(n[p]);
+        // 1. every virtual rank's bucket and announcement (no owner-side
+        //    buffers yet: room 0, so the plan always grows them below)
+        if ((e = dg_bucket(ctx, s[p], nranks, all + p * w, st)) != hipSuccess ||
+            (e = dg_announce(all + p * w + nranks, htail + kAnnTail * p, 0, ctx->ws_bytes, 0, st)) != hipSuccess)
+            rc = fail(ctx, e, "dedup_global_local bucket");
+    }
+    if (!rc && ((e = hipMemcpyAsync(hall, all, 8 * w * nranks, hipMemcpyDeviceToHost, st)) != hipSuccess ||
+                (e = hipStreamSynchronize(st)) != hipSuccess))
+        rc = fail(ctx, e, "dedup_global_local announcements");
+    if (!rc) {
+        dg_plan(hall, nranks, pl);
+        rc = pl.err ? dg_plan_error(ctx, pl, -1) : 0;
+    }
+    size_t bbytes = 0, wsb = 0;
+    for (int q = 0; q < nranks && !rc; q++) {
+        bbytes += dg_b_bytes(pl.m[q]);
+        wsb = std::max(wsb, dedup_ws_bytes(pl.m[q]));
+    }
+    if (!rc && (e = hipMalloc(&bmem, bbytes)) != hipSuccess) {
+        std::snprintf(ctx->err, sizeof(ctx->err), "hipMalloc(%zu): %s", bbytes, hipGetErrorString(e));
+        rc = ENOMEM;
+    }
+    if (!rc)
+        rc = ensure_ws(ctx, wsb, st);
+    if (!rc) {
+        std::vector<const char *> rows(nranks), ans(nranks);
+        std::vector<char *> rows_in(nranks), back(nranks);
+        done = 0;
+        for (int q = 0; q < nranks; q++) {
+            dg_carve_b(s[q], static_cast<char *>(bmem) + done, pl.m[q]);
+            done += dg_b_bytes(pl.m[q]);
+            rows[q] = reinterpret_cast<const char *>(s[q].rows);
+            rows_in[q] = reinterpret_cast<char *>(s[q].rows_in);
+            ans[q] = reinterpret_cast<const char *>(s[q].ans);
+            back[q] = reinterpret_cast<char *>(s[q].back);
+        }
+        // 2. rows to their owners, 3. each owner's group (one workspace,
+        //    stream-ordered), 4. answers back, 5. gathers
+        rc = dg_local_exchange(ctx, pl, false, rows, rows_in, 32, st);
+        for (int q = 0; q < nranks && !rc; q++)
+            if ((e = dg_group(ctx, s[q], st)) != hipSuccess)
+                rc = fail(ctx, e, "dedup_global_local group");
+        if (!rc)
+            rc = dg_local_exchange(ctx, pl, true, ans, back, 16, st);
+        for (int p = 0; p < nranks && !rc; p++)
+            if ((e = dg_gather(s[p], st)) != hipSuccess)
+                rc = fail(ctx, e, "dedup_global_local gather");
+    }
+    // the buffers are freed only once the stream is done with them
+    e = hipStreamSynchronize(st);
+    if (!rc && e != hipSuccess)
+        rc = fail(ctx, e, "dedup_global_local");
+    (void)hipFree(amem);
+    if (bmem)
+        (void)hipFree(bmem);
+    return rc;
 }
 
 // ---- formats that consume the CRC, FastDHT routing, scrub ----

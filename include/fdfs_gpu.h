@@ -237,19 +237,39 @@ int fdfs_gpu_index_stats(fdfs_gpu_index *index, uint64_t *classes, uint64_t *rec
 
 /* Multi-GPU dedup in one call, over RCCL (xGMI between the GPUs of a node):
  * one process per GPU, each holding its share of the ingest (sig, gidx: the
- * files' global ingest indices); every rank calls it with its share and gets
- * rep_out / ref_out for its own records, identical to fdfs_gpu_dedup over
- * the concatenated ingest.  Inside: bucket by owner rank (the FastDHT key
- * partition, storage/fdht_client/fdht_client.c:301-305, as a GPU bucket),
- * ncclAllToAll of the per-peer row counts, grouped ncclSend/ncclRecv of the
- * 32-byte rows, the owner's group, and the {rep, ref} answers sent back the
- * same way.  The one host synchronisation is the count exchange (the row
- * exchange is sized by it).  comm: an ncclComm_t (RCCL) of the ranks taking
- * part, each rank's communicator on this context's device.  Replaces the
- * per-file fdht_get_ex1 / fdht_set_ex / fdht_inc_ex round trips
+ * files' global ingest indices, required when the communicator has more
+ * than one rank); every rank calls it with its share and gets rep_out /
+ * ref_out for its own records, identical to fdfs_gpu_dedup over the
+ * concatenated ingest.  Inside: bucket by owner rank (the FastDHT key
+ * partition, storage/fdht_client/fdht_client.c:301-305, as a GPU bucket);
+ * one ncclAllGather of every rank's announcement (rows per owner, the room
+ * of its owner-side buffers, any local error), from which every rank derives
+ * the same exchange plan; grouped ncclSend/ncclRecv of the 32-byte rows; the
+ * owner's group; the {rep, ref} answers sent back the same way.  The one
+ * host synchronisation is the announcement (the row exchange is sized by
+ * it), plus one small all-reduce when some owner's buffers must grow.
+ * Errors: an argument error or allocation failure on ANY rank is returned by
+ * EVERY rank (EINVAL / ENOMEM; fdfs_gpu_last_error names the rank) before
+ * any row moves, so no rank is left waiting.  EIO after that point (a failed
+ * launch or RCCL call) leaves the communicator unusable: abort it.
+ * comm: an ncclComm_t (RCCL) of the ranks taking part, each rank's
+ * communicator on this context's device.  Replaces the per-file
+ * fdht_get_ex1 / fdht_set_ex / fdht_inc_ex round trips
  * (storage/storage_service.c:2652,2714,2734,2984) for bulk ingest. */
 int fdfs_gpu_dedup_global(fdfs_gpu_ctx *ctx, void *comm, const uint8_t *sig, const uint64_t *gidx,
                           uint64_t n, uint64_t *rep_out, uint32_t *ref_out, void *stream);
+
+/* fdfs_gpu_dedup_global for `nranks` VIRTUAL ranks in this process, all on
+ * this context's device: rank p's share is sig[p], gidx[p], n[p] -> rep_out[p],
+ * ref_out[p] (host arrays of nranks device pointers / counts).  It runs the
+ * same bucket, exchange plan, group and answer-gather code as the RCCL form;
+ * every (src, dst) segment moves by hipMemcpyAsync where RCCL would send it.
+ * This is how the multi-rank offsets and answer routing are checked on one
+ * GPU (tests/test_gpu_dedup.py), and a one-process fallback for a caller
+ * that holds every share.  Synchronous; allocates its exchange buffers. */
+int fdfs_gpu_dedup_global_local(fdfs_gpu_ctx *ctx, int nranks, const uint8_t *const *sig,
+                                const uint64_t *const *gidx, const uint64_t *n, uint64_t *const *rep_out,
+                                uint32_t *const *ref_out, void *stream);
 
 /* Convenience RCCL communicator setup for callers without one: rank 0 gets
  * a 128-byte id (ncclGetUniqueId) and sends it to the others by any means;

@@ -76,18 +76,52 @@ def test_config3_full_batch(oracle, ctxs):
     torch.cuda.empty_cache()
 
 
-def test_config5_bench_set(oracle, ctxs):
+C5_TOTAL = 100_000_000
+
+
+@pytest.fixture(scope="module")
+def c5_oracle(oracle):
+    """The oracle's sequential-semantics answers for the bench's config-5
+    set (computed once for the tests below)."""
+    sig, _ = C.c5_signatures(C5_TOTAL, 1, 0, "cuda")
+    sig_np = sig.cpu().numpy()
+    del sig
+    orep, oref = oracle.dedup(sig_np, nthreads=16)
+    del sig_np
+    return orep.astype(np.int64), oref.astype(np.int32)
+
+
+def test_config5_bench_set(c5_oracle, ctxs):
     """The bench's config-5 set (100M signatures, 10 % duplicates) on one
     GPU: every record's class source and class size equal the oracle's."""
     torch.cuda.empty_cache()
-    total = 100_000_000
-    sig, gidx = C.c5_signatures(total, 1, 0, "cuda")
+    orep, oref = c5_oracle
+    sig, gidx = C.c5_signatures(C5_TOTAL, 1, 0, "cuda")
     rep, ref = ctxs[0].dedup(sig)
     torch.cuda.synchronize()
-    sig_np = sig.cpu().numpy()
     del sig, gidx
-    orep, oref = oracle.dedup(sig_np, nthreads=16)
-    assert np.array_equal(rep.cpu().numpy(), orep.astype(np.int64))
-    assert np.array_equal(ref.cpu().numpy(), oref.astype(np.int32))
-    assert int(oref.max()) > 1 and (oref > 1).sum() > total // 20
+    assert np.array_equal(rep.cpu().numpy(), orep)
+    assert np.array_equal(ref.cpu().numpy(), oref)
+    assert int(oref.max()) > 1 and (oref > 1).sum() > C5_TOTAL // 20
+    torch.cuda.empty_cache()
+
+
+@pytest.mark.parametrize("world", [2, 3, 8])
+def test_config5_dedup_global_ranks(c5_oracle, ctxs, world):
+    """The multi-GPU dedup's own code (fdfs_gpu_dedup_global: bucket,
+    announcement plan, exchange offsets, owner groups, answer routing) at
+    world 2, 3 and 8 on the bench's 100M config-5 set, each rank's share
+    exactly as bench.py --gpus N splits it (C.c5_signatures), the ranks
+    virtual on this GPU with every (src, dst) segment a device copy where
+    RCCL would send it: every rank's answers equal the oracle's over the
+    concatenation."""
+    torch.cuda.empty_cache()
+    orep, oref = c5_oracle
+    shares = [C.c5_signatures(C5_TOTAL, world, r, "cuda") for r in range(world)]
+    outs = ctxs[0].dedup_global_local([s for s, _ in shares], [g for _, g in shares])
+    for r, ((_, g), (rep, ref)) in enumerate(zip(shares, outs)):
+        lo, hi = int(g[0]), int(g[-1]) + 1
+        assert np.array_equal(rep.cpu().numpy(), orep[lo:hi]), (world, r)
+        assert np.array_equal(ref.cpu().numpy(), oref[lo:hi]), (world, r)
+    del shares, outs
     torch.cuda.empty_cache()

@@ -252,6 +252,52 @@ def test_dedup_global_c_abi_one_rank(oracle, ctx):
         dist.destroy_process_group()
 
 
+@pytest.mark.parametrize("nranks", [1, 2, 3, 8, 64])
+def test_dedup_global_local_vs_oracle(oracle, ctx, nranks):
+    """fdfs_gpu_dedup_global's own code path (bucket, announcement plan,
+    per-(src, dst) offsets, owner groups, answer routing) for nranks virtual
+    ranks on this GPU, segments moved by device copies where RCCL would send
+    them.  Shares of uneven size (one empty), duplicates across ranks,
+    ingest indices with gaps: every rank's answers equal the oracle's over
+    the concatenation."""
+    n = 60_000
+    sig = _sigs(n, 35_000, 100 + nranks)
+    gidx = np.cumsum(np.random.default_rng(nranks).integers(1, 5, n)).astype(np.int64)
+    cuts = np.sort(np.random.default_rng(7 * nranks).choice(np.arange(1, n), nranks - 1, replace=False)) \
+        if nranks > 1 else np.array([], np.int64)
+    bounds = [0] + list(cuts) + [n]
+    if nranks > 2:
+        bounds[2] = bounds[1]  # rank 1 holds nothing
+    sig_t, g_t = torch.from_numpy(sig).cuda(), torch.from_numpy(gidx).cuda()
+    shares = [(sig_t[bounds[p]:bounds[p + 1]].contiguous(), g_t[bounds[p]:bounds[p + 1]].contiguous())
+              for p in range(nranks)]
+    outs = ctx.dedup_global_local([s for s, _ in shares], [g for _, g in shares])
+    orep, oref = oracle.dedup(sig)
+    for p in range(nranks):
+        lo, hi = bounds[p], bounds[p + 1]
+        rep, ref = outs[p]
+        assert np.array_equal(rep.cpu().numpy(), gidx[orep[lo:hi].astype(np.int64)]), p
+        assert np.array_equal(ref.cpu().numpy(), oref[lo:hi].astype(np.int32)), p
+
+
+def test_dedup_global_needs_gidx_over_ranks(ctx):
+    """without ingest indices, records of different ranks share
+    numbers and the class minimum would pick another rank's record.  More
+    than one rank without gidx is EINVAL (C) / ValueError (Python)."""
+    import ctypes
+    import errno
+    sig = torch.zeros((10, 24), dtype=torch.uint8, device="cuda")
+    with pytest.raises(ValueError):
+        ctx.dedup_global_local([sig, sig], [None, None])
+    L = ctx._L
+    rep = torch.empty(10, dtype=torch.int64, device="cuda")
+    ref = torch.empty(10, dtype=torch.int32, device="cuda")
+    P, U = ctypes.c_void_p * 2, ctypes.c_uint64 * 2
+    rc = L.fdfs_gpu_dedup_global_local(ctx._h, 2, P(sig.data_ptr(), sig.data_ptr()), P(None, None), U(10, 10),
+                                       P(rep.data_ptr(), rep.data_ptr()), P(ref.data_ptr(), ref.data_ptr()), None)
+    assert rc == errno.EINVAL
+
+
 @pytest.mark.parametrize("nbatch", [1, 2, 5])
 def test_incremental_index_matches_sequential_ingest(oracle, ctx, nbatch):
     """fdfs_gpu_index: a stream ingested in k batches.  After batch j every
