@@ -59,6 +59,7 @@ EXPORTS = (
     "fdfs_gpu_index_destroy",
     "fdfs_gpu_index_ingest",
     "fdfs_gpu_index_stats",
+    "fdfs_gpu_index_slots",
 )
 COMM_ID_BYTES = 128
 FILE_STATE_SIZE = 128  # sizeof(fdfs_gpu_file_state)
@@ -173,5 +174,7 @@ def load() -> ctypes.CDLL:
     L.fdfs_gpu_index_ingest.argtypes = [vp, vp, vp, vp, u64, vp, vp, vp]
     L.fdfs_gpu_index_stats.restype = i32
     L.fdfs_gpu_index_stats.argtypes = [vp, ctypes.POINTER(u64), ctypes.POINTER(u64), ctypes.POINTER(u64)]
+    L.fdfs_gpu_index_slots.restype = i32
+    L.fdfs_gpu_index_slots.argtypes = [vp, ctypes.POINTER(u64)]
     _lib = L
     return L

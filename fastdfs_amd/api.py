@@ -530,7 +530,11 @@ class DedupIndex:
         rc = self.ctx._L.fdfs_gpu_index_stats(self._h, ctypes.byref(cl), ctypes.byref(rec), ctypes.byref(un))
         if rc:
             raise FdfsGpuError(rc, "fdfs_gpu_index_stats")
-        return {"classes": cl.value, "records": rec.value, "unplaced": un.value}
+        sl = ctypes.c_uint64()
+        rc = self.ctx._L.fdfs_gpu_index_slots(self._h, ctypes.byref(sl))
+        if rc:
+            raise FdfsGpuError(rc, "fdfs_gpu_index_slots")
+        return {"classes": cl.value, "records": rec.value, "unplaced": un.value, "slots": sl.value}
 
     def close(self):
         if getattr(self, "_h", None):

@@ -509,8 +509,10 @@ int fdfs_gpu_state_init(fdfs_gpu_ctx *ctx, fdfs_gpu_file_state *states, uint32_t
     return e == hipSuccess ? 0 : fail(ctx, e, "state_init launch");
 }
 
-int fdfs_gpu_update_batch(fdfs_gpu_ctx *ctx, const fdfs_gpu_batch *chunks, const uint32_t *state_idx,
-                          int method, fdfs_gpu_file_state *states, void *stream)
+// check: the public entry's duplicate-state_idx check (one small kernel and
+// a host synchronisation); sig_batch_host's windows are unique by plan.
+static int update_batch(fdfs_gpu_ctx *ctx, const fdfs_gpu_batch *chunks, const uint32_t *state_idx, int method,
+                        fdfs_gpu_file_state *states, void *stream, bool check)
 {
     if (!ctx || !chunks)
         return EINVAL;
@@ -528,13 +530,31 @@ int fdfs_gpu_update_batch(fdfs_gpu_ctx *ctx, const fdfs_gpu_batch *chunks, const
     if (!g.ok)
         return ENODEV;
     hipStream_t st = reinterpret_cast<hipStream_t>(stream);
-    int rc = ensure_ws(ctx, sig_ws_bytes(n) + align_up(4ull * n), st);
+    const size_t tbytes = check && state_idx ? align_up(4ull * fdfs::sidx_table_size(n)) : 0;
+    int rc = ensure_ws(ctx, std::max(sig_ws_bytes(n) + align_up(4ull * n), tbytes), st);
     if (rc)
         return rc;
     WsScope wsc(ctx, st);
+    hipError_t e;
+    if (tbytes && !capturing(st)) {
+        // the contract (a state at most once per call) checked before any
+        // state is touched: the table is scratch in the workspace the
+        // kernels below then overwrite
+        uint32_t *dflag = reinterpret_cast<uint32_t *>(ctx->dann + kAnnMax + 64 * kAnnMax + 1);
+        volatile uint32_t *hflag = reinterpret_cast<uint32_t *>(ctx->hann + 64 * kAnnTail + 64 * kAnnMax + 1);
+        if ((e = fdfs::launch_sidx_check(state_idx, n, static_cast<uint32_t *>(ctx->ws), dflag, st)) != hipSuccess ||
+            (e = hipMemcpyAsync(const_cast<uint32_t *>(hflag), dflag, 4, hipMemcpyDeviceToHost, st)) != hipSuccess ||
+            (e = hipStreamSynchronize(st)) != hipSuccess)
+            return fail(ctx, e, "update_batch state_idx check");
+        if (*hflag) {
+            std::snprintf(ctx->err, sizeof(ctx->err), "update_batch: %s",
+                          (*hflag & 1) ? "a state index appears more than once in one call"
+                                       : "state index 0xFFFFFFFF");
+            return EINVAL;
+        }
+    }
     Carve cv{static_cast<char *>(ctx->ws)};
     const uint8_t *base = static_cast<const uint8_t *>(chunks->base);
-    hipError_t e;
     if (method == FDFS_SIG_CRC_ONLY) {
         // per-chunk CRC by the segmented kernel, then carried onto the state
         uint32_t *tmp = cv.take<uint32_t>(n);
@@ -558,6 +578,12 @@ int fdfs_gpu_update_batch(fdfs_gpu_ctx *ctx, const fdfs_gpu_batch *chunks, const
                                   st, a, b);
     }
     return e == hipSuccess ? 0 : fail(ctx, e, "update_batch launch");
+}
+
+int fdfs_gpu_update_batch(fdfs_gpu_ctx *ctx, const fdfs_gpu_batch *chunks, const uint32_t *state_idx,
+                          int method, fdfs_gpu_file_state *states, void *stream)
+{
+    return update_batch(ctx, chunks, state_idx, method, states, stream, true);
 }
 
 int fdfs_gpu_final_batch(fdfs_gpu_ctx *ctx, const fdfs_gpu_file_state *states,
@@ -747,8 +773,8 @@ int fdfs_gpu_sig_batch_host(fdfs_gpu_ctx *ctx, const fdfs_gpu_batch *hb, int met
             break;
         fdfs_gpu_batch b{d_data, reinterpret_cast<const uint64_t *>(d_meta),
                          reinterpret_cast<const uint64_t *>(d_meta + align_up(8ull * maxp)), m};
-        rc = fdfs_gpu_update_batch(ctx, &b, reinterpret_cast<const uint32_t *>(d_meta + 2 * align_up(8ull * maxp)),
-                                   method, states, cs);
+        rc = update_batch(ctx, &b, reinterpret_cast<const uint32_t *>(d_meta + 2 * align_up(8ull * maxp)), method,
+                          states, cs, false);  // one piece per file per window by plan
         if (rc == 0)
             e = hipEventRecord(done[k & 1], cs);
     }
@@ -866,9 +892,32 @@ struct fdfs_gpu_index {
     fdfs::IndexTable t{};
     void *mem = nullptr;
     uint64_t records = 0;  // records ingested so far (the implicit ingest index base)
+    uint64_t bound = 0;    // upper bound of the classes in the table (exact after a read-back)
     hipEvent_t ev = nullptr;
     bool used = false;
+    // ingest, stats and destroy of one index are serialised here (after the
+    // calling context's mutex, never before it)
+    std::mutex mu;
 };
+
+// The table keeps load <= 3/4.
+static uint64_t index_capacity(uint64_t slots) { return slots / 4 * 3; }
+
+static size_t index_bytes(uint64_t slots)
+{
+    return align_up(24 * slots) + align_up(8 * slots) + align_up(4 * slots) + align_up(4 * slots) + align_up(8 * 4);
+}
+
+static void index_carve(fdfs::IndexTable &t, void *mem, uint64_t slots)
+{
+    Carve cv{static_cast<char *>(mem)};
+    t.slots = slots;
+    t.keys = cv.take<uint8_t>(24 * slots);
+    t.rep = cv.take<uint64_t>(slots);
+    t.ref = cv.take<uint32_t>(slots);
+    t.state = cv.take<uint32_t>(slots);
+    t.counters = cv.take<uint64_t>(4);
+}
 
 int fdfs_gpu_index_create(fdfs_gpu_ctx *ctx, uint64_t max_classes, fdfs_gpu_index **out)
 {
@@ -880,27 +929,20 @@ int fdfs_gpu_index_create(fdfs_gpu_ctx *ctx, uint64_t max_classes, fdfs_gpu_inde
     if (!g.ok)
         return ENODEV;
     uint64_t slots = 1024;
-    while (slots * 3 / 4 < max_classes)  // load factor <= 0.75
+    while (index_capacity(slots) < max_classes)
         slots <<= 1;
     auto *ix = new (std::nothrow) fdfs_gpu_index;
     if (!ix)
         return ENOMEM;
     ix->device = ctx->device;
-    const size_t bytes = align_up(24 * slots) + align_up(8 * slots) + align_up(4 * slots) + align_up(4 * slots) +
-                         align_up(8 * 4);
+    const size_t bytes = index_bytes(slots);
     hipError_t e = hipMalloc(&ix->mem, bytes);
     if (e != hipSuccess) {
         delete ix;
         std::snprintf(ctx->err, sizeof(ctx->err), "hipMalloc(%zu): %s", bytes, hipGetErrorString(e));
         return ENOMEM;
     }
-    Carve cv{static_cast<char *>(ix->mem)};
-    ix->t.slots = slots;
-    ix->t.keys = cv.take<uint8_t>(24 * slots);
-    ix->t.rep = cv.take<uint64_t>(slots);
-    ix->t.ref = cv.take<uint32_t>(slots);
-    ix->t.state = cv.take<uint32_t>(slots);
-    ix->t.counters = cv.take<uint64_t>(4);
+    index_carve(ix->t, ix->mem, slots);
     if ((e = hipEventCreateWithFlags(&ix->ev, hipEventDisableTiming)) == hipSuccess &&
         (e = hipMemset(ix->t.counters, 0, 32)) == hipSuccess &&
         (e = fdfs::launch_index_clear(ix->t.state, slots, nullptr)) == hipSuccess)
@@ -920,12 +962,66 @@ int fdfs_gpu_index_destroy(fdfs_gpu_index *ix)
 {
     if (!ix)
         return EINVAL;
-    DeviceGuard g(ix->device);
-    if (ix->used)
-        (void)hipEventSynchronize(ix->ev);
-    (void)hipFree(ix->mem);
-    (void)hipEventDestroy(ix->ev);
+    {
+        std::lock_guard<std::mutex> lk(ix->mu);  // waits for an ingest in progress
+        DeviceGuard g(ix->device);
+        if (ix->used)
+            (void)hipEventSynchronize(ix->ev);
+        (void)hipFree(ix->mem);
+        (void)hipEventDestroy(ix->ev);
+    }
     delete ix;
+    return 0;
+}
+
+// Make room for `n` more classes: read back the exact class count (a sync
+// on the index's last ingest) when the running bound says the batch might
+// not fit, and if it still might, grow the table (twice the slots until it
+// fits) and rehash every class into it.  On failure the index is unchanged.
+static int index_make_room(fdfs_gpu_ctx *ctx, fdfs_gpu_index *ix, uint64_t n, hipStream_t st)
+{
+    if (ix->bound + n <= index_capacity(ix->t.slots))
+        return 0;
+    if (capturing(st)) {
+        std::snprintf(ctx->err, sizeof(ctx->err), "index growth needed during stream capture");
+        return ENOSPC;
+    }
+    uint64_t c[4] = {0, 0, 0, 0};
+    hipError_t e = ix->used ? hipEventSynchronize(ix->ev) : hipSuccess;
+    if (e == hipSuccess)
+        e = hipMemcpy(c, ix->t.counters, sizeof(c), hipMemcpyDeviceToHost);
+    if (e != hipSuccess)
+        return fail(ctx, e, "index class count");
+    ix->bound = c[0];
+    if (ix->bound + n <= index_capacity(ix->t.slots))
+        return 0;
+    uint64_t slots = ix->t.slots;
+    while (index_capacity(slots) < ix->bound + n) {
+        if (slots >= (1ull << 41))
+            return ENOMEM;
+        slots <<= 1;
+    }
+    void *mem = nullptr;
+    const size_t bytes = index_bytes(slots);
+    if ((e = hipMalloc(&mem, bytes)) != hipSuccess) {
+        std::snprintf(ctx->err, sizeof(ctx->err), "index growth to %llu slots: hipMalloc(%zu): %s",
+                      (unsigned long long)slots, bytes, hipGetErrorString(e));
+        return ENOMEM;
+    }
+    fdfs::IndexTable t{};
+    index_carve(t, mem, slots);
+    if ((e = fdfs::launch_index_clear(t.state, slots, st)) == hipSuccess &&
+        (e = hipMemcpyAsync(t.counters, ix->t.counters, 32, hipMemcpyDeviceToDevice, st)) == hipSuccess &&
+        (e = fdfs::launch_index_rehash(ix->t, t, st)) == hipSuccess)
+        e = hipStreamSynchronize(st);
+    if (e != hipSuccess) {
+        (void)hipStreamSynchronize(st);
+        (void)hipFree(mem);
+        return fail(ctx, e, "index growth");
+    }
+    (void)hipFree(ix->mem);
+    ix->mem = mem;
+    ix->t = t;
     return 0;
 }
 
@@ -942,6 +1038,7 @@ int fdfs_gpu_index_ingest(fdfs_gpu_ctx *ctx, fdfs_gpu_index *ix, const uint8_t *
          reinterpret_cast<uintptr_t>(rep_out)) & 7)
         return EINVAL;
     std::lock_guard<std::recursive_mutex> lk(ctx->mu);
+    std::lock_guard<std::mutex> lki(ix->mu);
     DeviceGuard g(ctx->device);
     if (!g.ok)
         return ENODEV;
@@ -954,6 +1051,9 @@ int fdfs_gpu_index_ingest(fdfs_gpu_ctx *ctx, fdfs_gpu_index *ix, const uint8_t *
     // successive ingests into one index are ordered whatever their streams
     if (ix->used && !capturing(st))
         (void)hipStreamWaitEvent(st, ix->ev, 0);
+    // every class of the batch finds a slot: the table grows first if needed
+    if ((rc = index_make_room(ctx, ix, n, st)))
+        return rc;
     Carve cv{static_cast<char *>(ctx->ws) + dws};
     uint64_t *rep_pos = cv.take<uint64_t>(n);
     uint32_t *ref_b = cv.take<uint32_t>(n);
@@ -970,6 +1070,7 @@ int fdfs_gpu_index_ingest(fdfs_gpu_ctx *ctx, fdfs_gpu_index *ix, const uint8_t *
     if (e != hipSuccess)
         return fail(ctx, e, "index_ingest");
     ix->records += n;
+    ix->bound += n;
     if (!capturing(st) && hipEventRecord(ix->ev, st) == hipSuccess)
         ix->used = true;
     return 0;
@@ -979,18 +1080,29 @@ int fdfs_gpu_index_stats(fdfs_gpu_index *ix, uint64_t *classes, uint64_t *record
 {
     if (!ix)
         return EINVAL;
+    std::lock_guard<std::mutex> lk(ix->mu);
     DeviceGuard g(ix->device);
     uint64_t c[4] = {0, 0, 0, 0};
     if (ix->used && hipEventSynchronize(ix->ev) != hipSuccess)
         return EIO;
     if (hipMemcpy(c, ix->t.counters, sizeof(c), hipMemcpyDeviceToHost) != hipSuccess)
         return EIO;
+    ix->bound = c[0];
     if (classes)
         *classes = c[0];
     if (records)
         *records = ix->records;
     if (unplaced)
         *unplaced = c[2];
+    return 0;
+}
+
+int fdfs_gpu_index_slots(fdfs_gpu_index *ix, uint64_t *slots)
+{
+    if (!ix || !slots)
+        return EINVAL;
+    std::lock_guard<std::mutex> lk(ix->mu);
+    *slots = ix->t.slots;
     return 0;
 }
 

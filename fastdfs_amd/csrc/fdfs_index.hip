@@ -120,6 +120,42 @@ __global__ void index_answer_kernel(const uint64_t *__restrict__ rep_pos, uint64
     }
 }
 
+// Growth: every full slot of the old table into the new one (distinct keys,
+// no concurrent reader: a claim is one CAS, then the fields).
+__global__ void index_rehash_kernel(const uint8_t *__restrict__ okeys, const uint64_t *__restrict__ orep,
+                                    const uint32_t *__restrict__ oref, const uint32_t *__restrict__ ostate,
+                                    uint64_t oslots, uint8_t *__restrict__ keys, uint64_t *__restrict__ vrep,
+                                    uint32_t *__restrict__ vref, uint32_t *__restrict__ state, uint64_t slots)
+{
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < oslots;
+         i += (uint64_t)gridDim.x * blockDim.x) {
+        if (ostate[i] != kIxFull)
+            continue;
+        const uint64_t *k = reinterpret_cast<const uint64_t *>(okeys + 24 * i);
+        const uint64_t a = k[0], b = k[1], c = k[2];
+        uint64_t slot = ix_hash(a, b, c) & (slots - 1);
+        for (;;) {
+            if (atomicCAS(&state[slot], kIxEmpty, kIxFull) == kIxEmpty)
+                break;
+            slot = (slot + 1) & (slots - 1);
+        }
+        uint64_t *d = reinterpret_cast<uint64_t *>(keys + 24 * slot);
+        d[0] = a;
+        d[1] = b;
+        d[2] = c;
+        vrep[slot] = orep[i];
+        vref[slot] = oref[i];
+    }
+}
+
+hipError_t launch_index_rehash(const IndexTable &from, const IndexTable &to, hipStream_t st)
+{
+    const uint64_t g = (from.slots + 255) / 256;
+    index_rehash_kernel<<<(unsigned)(g < 16384 ? g : 16384), 256, 0, st>>>(
+        from.keys, from.rep, from.ref, from.state, from.slots, to.keys, to.rep, to.ref, to.state, to.slots);
+    return hipGetLastError();
+}
+
 hipError_t launch_index_clear(uint32_t *state, uint64_t slots, hipStream_t st)
 {
     index_clear_kernel<<<4096, 256, 0, st>>>(state, slots);

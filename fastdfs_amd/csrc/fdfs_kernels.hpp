@@ -82,6 +82,10 @@ hipError_t launch_final(int method, const fdfs_gpu_file_state *states, const uin
                         hipStream_t st);
 hipError_t launch_crc_combine(const uint32_t *a, const uint32_t *b, const uint64_t *len_b, uint32_t n,
                               uint32_t *out, const DevTables *tabs, hipStream_t st);
+// Duplicate state indices of an update batch: *flag = 1 duplicate, 2 the
+// reserved value ~0 (table: sidx_table_size(n) u32 of scratch).
+uint32_t sidx_table_size(uint32_t n);
+hipError_t launch_sidx_check(const uint32_t *sidx, uint32_t n, uint32_t *table, uint32_t *flag, hipStream_t st);
 int crc_seg_blocks_per_cu();
 int crc_table_mode();
 
@@ -130,6 +134,7 @@ struct IndexTable {
     uint64_t *counters;   // [4]: classes, -, unplaced classes (table full), -
 };
 hipError_t launch_index_clear(uint32_t *state, uint64_t slots, hipStream_t st);
+hipError_t launch_index_rehash(const IndexTable &from, const IndexTable &to, hipStream_t st);
 hipError_t launch_index_ingest(const uint8_t *sig, const uint64_t *gidx, uint64_t gbase, uint64_t n,
                                const uint64_t *rep_pos, const uint32_t *ref_b, const IndexTable &t,
                                uint64_t *res_rep, uint32_t *res_ref, uint64_t *rep_out, uint32_t *ref_out,

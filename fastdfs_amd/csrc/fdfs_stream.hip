@@ -113,6 +113,59 @@ __global__ void crc_combine_kernel(const uint32_t *__restrict__ a, const uint32_
 
 static unsigned blocks(uint32_t n) { return (n + 255) / 256; }
 
+// fdfs_gpu_update_batch's contract check: a state index may appear at most
+// once per call (two chunks on one state would race).  Open addressing on
+// `size` (a power of two >= 2n) u32 slots, pre-filled with ~0: a claim that
+// meets its own value is a duplicate.  flag |= 1 on a duplicate, 2 on the
+// reserved value ~0.
+__global__ void sidx_fill_kernel(uint32_t *__restrict__ table, uint32_t size)
+{
+    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < size; i += gridDim.x * blockDim.x)
+        table[i] = ~0u;
+}
+
+__global__ void sidx_dup_kernel(const uint32_t *__restrict__ sidx, uint32_t n, uint32_t *__restrict__ table,
+                                uint32_t size, uint32_t *__restrict__ flag)
+{
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n)
+        return;
+    const uint32_t v = sidx[i];
+    if (v == ~0u) {
+        atomicOr(flag, 2u);
+        return;
+    }
+    for (uint32_t h = (v * 0x9E3779B1u) & (size - 1);; h = (h + 1) & (size - 1)) {
+        const uint32_t cur = atomicCAS(&table[h], ~0u, v);
+        if (cur == ~0u)
+            return;
+        if (cur == v) {
+            atomicOr(flag, 1u);
+            return;
+        }
+    }
+}
+
+uint32_t sidx_table_size(uint32_t n)
+{
+    uint32_t s = 64;
+    while (s < 2ull * n && s < (1u << 31))
+        s <<= 1;
+    return s;
+}
+
+hipError_t launch_sidx_check(const uint32_t *sidx, uint32_t n, uint32_t *table, uint32_t *flag, hipStream_t st)
+{
+    const uint32_t size = sidx_table_size(n);
+    const uint32_t g = (size + 255) / 256;
+    sidx_fill_kernel<<<g < 4096 ? g : 4096, 256, 0, st>>>(table, size);
+    hipError_t e = launch_zero_u32(flag, 1, st);
+    if (e != hipSuccess)
+        return e;
+    sidx_dup_kernel<<<blocks(n), 256, 0, st>>>(sidx, n, table, size, flag);
+    return hipGetLastError();
+}
+
 hipError_t launch_state_init(fdfs_gpu_file_state *states, uint32_t n, hipStream_t st)
 {
     state_init_kernel<<<blocks(n), 256, 0, st>>>(states, n);

@@ -4,8 +4,9 @@
  * Same usage, output ("%u\n" of CRC32_FINAL(CRC32_ex(...)),
  * client/fdfs_crc32.c:97-101) and error convention (message + errno exit
  * status, client/fdfs_crc32.c:37-45).  Several files may be given: one CRC
- * per line, in argument order.  Set FDFS_UNSIGNED_HASH=1 in the environment
- * for the logical-shift variant.
+ * per line, in argument order.  A leading -u selects the logical-shift
+ * (zlib) variant; the default is the signed-int CRC32_ex libfastcommon
+ * declares.  No environment variable changes a result.
  *
  * Like the reference, which reads each file in 512 KiB chunks and carries
  * the CRC32_ex value from chunk to chunk (client/fdfs_crc32.c:70-93), the
@@ -59,8 +60,14 @@ struct slot {
 
 int main(int argc, char *argv[])
 {
+    int unsigned_hash = 0;
+    if (argc >= 2 && strcmp(argv[1], "-u") == 0) {
+        unsigned_hash = 1;
+        argv++;
+        argc--;
+    }
     if (argc < 2) {
-        printf("Usage: %s <filename> [filename ...]\n", argv[0]);
+        printf("Usage: %s [-u] <filename> [filename ...]\n", argv[0]);
         return 1;
     }
     const uint32_t n = (uint32_t)(argc - 1);
@@ -76,9 +83,8 @@ int main(int argc, char *argv[])
     }
     /* the device first: without a GPU this fails loudly (ENODEV), there is
      * no CPU path */
-    const char *u = getenv("FDFS_UNSIGNED_HASH");
     fdfs_gpu_ctx *ctx = NULL;
-    int rc = fdfs_gpu_open(0, (u && *u == '1') ? FDFS_GPU_FLAG_UNSIGNED_HASH : 0, &ctx);
+    int rc = fdfs_gpu_open(0, unsigned_hash ? FDFS_GPU_FLAG_UNSIGNED_HASH : 0, &ctx);
     if (rc) {
         printf("fdfs_gpu_open fail, errno: %d, error info: %s\n", rc, strerror(rc));
         return rc;

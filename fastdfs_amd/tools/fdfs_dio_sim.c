@@ -25,8 +25,8 @@
  * Output, one line per file in argument order: the CRC32 ("%u", as
  * fdfs_crc32 prints it), then for -m hash / -m md5 the 24-byte signature in
  * hex.  A summary goes to stderr.  Errors: message + errno exit status, as
- * client/fdfs_crc32.c does.  FDFS_UNSIGNED_HASH=1 selects the logical-shift
- * hash variant.
+ * client/fdfs_crc32.c does.  -u selects the logical-shift hash variant
+ * (no environment variable changes a result).
  */
 #include <errno.h>
 #include <fcntl.h>
@@ -81,8 +81,8 @@ int main(int argc, char *argv[])
     uint64_t buff = 256u << 10; /* buff_size = 256KB, conf/storage.conf:52 */
     uint64_t hdr = 25;          /* proto header (10) + upload fields (15) in the first buffer */
     uint32_t jobs = 1024;
-    int opt;
-    while ((opt = getopt(argc, argv, "m:c:H:j:")) != -1) {
+    int opt, unsigned_hash = 0;
+    while ((opt = getopt(argc, argv, "um:c:H:j:")) != -1) {
         if (opt == 'm')
             method = !strcmp(optarg, "crc") ? FDFS_SIG_CRC_ONLY : !strcmp(optarg, "md5") ? FDFS_SIG_MD5 : FDFS_SIG_HASH;
         else if (opt == 'c')
@@ -91,11 +91,13 @@ int main(int argc, char *argv[])
             hdr = strtoull(optarg, NULL, 10);
         else if (opt == 'j')
             jobs = (uint32_t)strtoul(optarg, NULL, 10);
+        else if (opt == 'u')
+            unsigned_hash = 1;
         else
             optind = argc + 1;
     }
     if (optind >= argc || buff == 0 || hdr >= buff || jobs == 0) {
-        printf("Usage: %s [-m crc|hash|md5] [-c buff_size] [-H header_bytes] [-j uploads] <filename> ...\n",
+        printf("Usage: %s [-u] [-m crc|hash|md5] [-c buff_size] [-H header_bytes] [-j uploads] <filename> ...\n",
                argv[0]);
         return 1;
     }
@@ -119,9 +121,8 @@ int main(int argc, char *argv[])
 
     /* the device first: without a GPU this fails loudly (ENODEV), there is
      * no CPU path */
-    const char *u = getenv("FDFS_UNSIGNED_HASH");
     fdfs_gpu_ctx *ctx = NULL;
-    int rc = fdfs_gpu_open(0, (u && *u == '1') ? FDFS_GPU_FLAG_UNSIGNED_HASH : 0, &ctx);
+    int rc = fdfs_gpu_open(0, unsigned_hash ? FDFS_GPU_FLAG_UNSIGNED_HASH : 0, &ctx);
     if (rc) {
         printf("fdfs_gpu_open fail, errno: %d, error info: %s\n", rc, strerror(rc));
         return rc;

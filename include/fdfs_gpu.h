@@ -164,8 +164,12 @@ int fdfs_gpu_state_init(fdfs_gpu_ctx *ctx, fdfs_gpu_file_state *states, uint32_t
  * states[state_idx ? state_idx[i] : i]: CRC32_ex always (as uploads do,
  * storage/storage_service.c:4533), CALC_HASH_CODES4 for FDFS_SIG_HASH,
  * my_md5_update for FDFS_SIG_MD5.  A state may appear at most once per call
- * (the daemon has one chunk of an upload in flight at a time); chunks may
- * start at any byte and have any length, including 0. */
+ * (the daemon has one chunk of an upload in flight at a time): with
+ * state_idx given, the call checks this first (one small kernel and a host
+ * synchronisation) and returns EINVAL without touching any state on a
+ * repeated index or the reserved index 0xFFFFFFFF (inside a stream capture
+ * the check is skipped and the contract is the caller's).  Chunks may start
+ * at any byte and have any length, including 0. */
 int fdfs_gpu_update_batch(fdfs_gpu_ctx *ctx, const fdfs_gpu_batch *chunks, const uint32_t *state_idx,
                           int method, fdfs_gpu_file_state *states, void *stream);
 
@@ -221,11 +225,19 @@ int fdfs_gpu_dedup_group(fdfs_gpu_ctx *ctx, const uint8_t *records, uint64_t n,
  * record rep_out = the ingest index of the first file EVER ingested with its
  * signature (an earlier batch's source stays the source) and ref_out = the
  * class size once this batch is in.  After k batches the answers equal
- * fdfs_gpu_dedup over the concatenation of all k.  max_classes bounds the
- * distinct signatures (the table keeps load <= 3/4, 40 bytes per slot);
- * classes that find no slot are answered within their batch and counted in
- * fdfs_gpu_index_stats' unplaced (synchronous; waits for the last ingest).
- * Ingests into one index are ordered whatever their streams. */
+ * fdfs_gpu_dedup over the concatenation of all k.  max_classes sizes the
+ * table (load <= 3/4, 40 bytes per slot); it is not a limit: when a batch
+ * might not fit (a host-side bound of the classes so far plus the batch's
+ * records, refined by reading back the exact count, one synchronisation),
+ * the table grows to twice its slots until it fits and every class is
+ * rehashed into it, before the batch is grouped.  So every class of every
+ * batch is placed: no answer is ever given "within its batch only".  If the
+ * growth cannot be allocated, ingest returns ENOMEM and the index is
+ * unchanged (the batch was not ingested; ENOSPC if growth is needed inside a
+ * stream capture).  fdfs_gpu_index_stats is synchronous (waits for the last
+ * ingest); unplaced stays 0.  Ingests into one index are ordered whatever
+ * their streams; ingest, stats, slots and destroy of one index may be called
+ * from any thread (the index has its own lock). */
 typedef struct fdfs_gpu_index fdfs_gpu_index;
 int fdfs_gpu_index_create(fdfs_gpu_ctx *ctx, uint64_t max_classes, fdfs_gpu_index **out);
 int fdfs_gpu_index_destroy(fdfs_gpu_index *index);
@@ -234,6 +246,8 @@ int fdfs_gpu_index_ingest(fdfs_gpu_ctx *ctx, fdfs_gpu_index *index, const uint8_
                           void *stream);
 int fdfs_gpu_index_stats(fdfs_gpu_index *index, uint64_t *classes, uint64_t *records,
                          uint64_t *unplaced);
+/* The table's current slot count (grows as above). */
+int fdfs_gpu_index_slots(fdfs_gpu_index *index, uint64_t *slots);
 
 /* Multi-GPU dedup in one call, over RCCL (xGMI between the GPUs of a node):
  * one process per GPU, each holding its share of the ingest (sig, gidx: the

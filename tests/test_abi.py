@@ -114,3 +114,13 @@ def test_stream_api_argument_errors():
     assert L.fdfs_gpu_update_batch(None, None, None, 0, None, None) == errno.EINVAL
     assert L.fdfs_gpu_final_batch(None, None, None, 1, 0, None, None, None, None) == errno.EINVAL
     assert L.fdfs_gpu_crc_combine(None, None, None, None, 1, None, None) == errno.EINVAL
+
+
+def test_tools_read_no_environment():
+    """The drop-in C tools select the hash variant by a -u flag, never by an
+    environment variable: neither imports getenv."""
+    for tool in ("fdfs_crc32_gpu", "fdfs_dio_sim"):
+        path = os.path.join(os.path.dirname(_lib.LIB_PATH), tool)
+        out = subprocess.run(["nm", "-D", "--undefined-only", path], capture_output=True, text=True,
+                             check=True).stdout
+        assert not re.search(r"\b(secure_)?getenv\b", out), tool

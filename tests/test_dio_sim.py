@@ -85,8 +85,8 @@ def test_uploads_vs_oracle(tmp_path, oracle, method, variant):
     sizes = [0, 1, buff - hdr - 1, buff - hdr, buff - hdr + 1, 2 * buff - hdr, 2 * buff - hdr + 63, 0,
              5 * buff + 7] + list(rng.integers(0, 400_000, 12))
     paths, bufs = _write(tmp_path, sizes, 80 + method)
-    r = _run(["-m", METHOD[method], "-c", str(buff), "-H", str(hdr), "-j", "5"] + paths,
-             env={"FDFS_UNSIGNED_HASH": str(variant)})
+    r = _run((["-u"] if variant else []) + ["-m", METHOD[method], "-c", str(buff), "-H", str(hdr), "-j", "5"]
+             + paths)
     assert r.returncode == 0, r.stdout + r.stderr
     crc, sig = _parse(r.stdout, method)
     for i, b in enumerate(bufs):

@@ -5,7 +5,10 @@
 * config 3: the bench's 100K photo files (~262 GB resident), a sample from
   every size decile against the oracle and hashlib;
 * config 5: the bench's own 100M-signature set on one GPU against the
-  oracle's sequential-semantics dedup.
+  oracle's sequential-semantics dedup, and through the multi-GPU dedup's
+  code at world 2, 3 and 8;
+* signatures of the largest files: MD5 past 512 MiB (a 64-bit bit count)
+  and of 1 GiB, one-shot and chunked; HASH of a file past 4 GiB.
 """
 import hashlib
 
@@ -124,4 +127,62 @@ def test_config5_dedup_global_ranks(c5_oracle, ctxs, world):
         assert np.array_equal(rep.cpu().numpy(), orep[lo:hi]), (world, r)
         assert np.array_equal(ref.cpu().numpy(), oref[lo:hi]), (world, r)
     del shares, outs
+    torch.cuda.empty_cache()
+
+
+@pytest.mark.parametrize("size", [(512 << 20) + 13, 1 << 30])
+def test_md5_big_files(oracle, ctxs, size):
+    """MD5 signature (file_signature_method=md5, storage/storage_dio.c:480,
+    512) of files whose bit count passes 2^32 (its high word non-zero,
+    RFC 1321 3.2): one-shot, and through update_batch in 256 KiB (the
+    daemon's buff_size) and 64 MiB chunks, against the oracle and hashlib."""
+    torch.cuda.empty_cache()
+    data = torch.empty(size + 64, dtype=torch.uint8, device="cuda")
+    C.fill_random(data, size & 0xFFFF)
+    host = data[:size].cpu().numpy()
+    oc, osig, _ = oracle.dio_file(host, 2, 0)
+    assert osig[8:] == hashlib.md5(host.tobytes()).digest()
+    del host
+    ctx = ctxs[0]
+    offs = torch.tensor([0], dtype=torch.int64, device="cuda")
+    crc, sig, _ = ctx.sig_batch(data, offs, torch.tensor([size], dtype=torch.int64, device="cuda"), method=2)
+    torch.cuda.synchronize()
+    assert int(crc.cpu().numpy().view(np.uint32)[0]) == oc
+    assert sig.cpu().numpy()[0].tobytes() == osig
+    for chunk in (256 << 10, 64 << 20):
+        states = ctx.new_states(1)
+        for p in range(0, size, chunk):
+            c = min(chunk, size - p)
+            ctx.update_batch(states, data, torch.tensor([p], dtype=torch.int64, device="cuda"),
+                             torch.tensor([c], dtype=torch.int64, device="cuda"), method=2, check_bounds=False)
+        crc, sig, _ = ctx.final_batch(states, method=2)
+        torch.cuda.synchronize()
+        assert int(crc.cpu().numpy().view(np.uint32)[0]) == oc, chunk
+        assert sig.cpu().numpy()[0].tobytes() == osig, chunk
+        bits = int(states.cpu().numpy()[0, 36:44].view(np.uint64)[0])
+        assert bits == 8 * size
+    del data
+    torch.cuda.empty_cache()
+
+
+def test_hash_file_past_4gib(oracle, ctxs):
+    """HASH signature of a (4 GiB + 7 B) file: the ELF lane's 64-bit
+    lengths, the big-file offload (segmented CRC + polynomial kernels) and
+    the be64 size field, against the oracle (CRC32_ex + CALC_HASH_CODES4 in
+    256 KiB chunks, storage/storage_dio.c:465-477)."""
+    torch.cuda.empty_cache()
+    size = (4 << 30) + 7
+    data = torch.empty(size + 64, dtype=torch.uint8, device="cuda")
+    C.fill_random(data, 4747)
+    crc, sig, codes = ctxs[0].sig_batch(data, torch.tensor([0], dtype=torch.int64, device="cuda"),
+                                        torch.tensor([size], dtype=torch.int64, device="cuda"), method=1,
+                                        want_codes=True)
+    torch.cuda.synchronize()
+    host = data[:size].cpu().numpy()
+    del data
+    oc, osig, ocodes = oracle.dio_file(host, 1, 0)
+    assert int(crc.cpu().numpy().view(np.uint32)[0]) == oc
+    assert sig.cpu().numpy()[0].tobytes() == osig
+    assert [int(x) for x in codes.cpu().numpy()[0]] == ocodes
+    assert int.from_bytes(osig[:8], "big") == size
     torch.cuda.empty_cache()

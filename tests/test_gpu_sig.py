@@ -250,8 +250,9 @@ def test_offload_regime_boundary(oracle, ctxs, extra):
 def test_md5_staged_multiwave(oracle, ctxs):
     """MD5 method over several waves of the staged kernel: files of 0 B to
     1.2 MiB in one aligned batch (lanes finish at different rounds, partial
-    last rounds, a ragged last wave), plus one byte-misaligned file that
-    sends its wave down the lane-serial load path."""
+    last rounds, a ragged last wave), plus one byte-misaligned file: the
+    staged cooperative loads read every file's stream at its own byte
+    offset, so it takes the same path as the aligned ones."""
     rng = np.random.default_rng(31)
     sizes = np.concatenate([rng.integers(0, 300, 70), rng.integers(300, 70000, 150),
                             rng.integers(1 << 18, 1_200_000, 113)])

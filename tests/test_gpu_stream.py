@@ -340,3 +340,34 @@ def test_two_streams_one_context(oracle):
         t.join()
     ctx.close()
     assert not errors, errors
+
+
+@pytest.mark.parametrize("method", [0, 1, 2])
+def test_update_rejects_repeated_state(ctxs, method):
+    """include/fdfs_gpu.h: a state may appear at most once per update call
+    (storage/storage_nio.h:96 -- one chunk of an upload in flight at a time).
+    A repeated index, or the reserved 0xFFFFFFFF, is EINVAL before any state
+    is touched; a permutation passes."""
+    import errno
+    from fastdfs_amd import FdfsGpuError
+    ctx = ctxs[0]
+    n = 5000
+    states = ctx.new_states(n)
+    before = states.clone()
+    data = torch.randint(0, 256, (n * 100,), dtype=torch.uint8, device="cuda")
+    offs = torch.arange(n, dtype=torch.int64, device="cuda") * 100
+    sizes = torch.full((n,), 100, dtype=torch.int64, device="cuda")
+    for bad in ([3, 3], [0, 4999], None):
+        idx = torch.randperm(n, device="cuda").to(torch.int32)
+        if bad is None:
+            idx[77] = -1  # 0xFFFFFFFF
+        else:
+            idx[bad[1]] = idx[bad[0]]
+        with pytest.raises(FdfsGpuError) as ei:
+            ctx.update_batch(states, data, offs, sizes, method=method, state_idx=idx, check_bounds=False)
+        assert ei.value.errno == errno.EINVAL
+        assert torch.equal(states, before)
+    ctx.update_batch(states, data, offs, sizes, method=method,
+                     state_idx=torch.randperm(n, device="cuda").to(torch.int32))
+    torch.cuda.synchronize()
+    assert not torch.equal(states, before)

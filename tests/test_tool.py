@@ -62,7 +62,7 @@ def test_corpus_files(tmp_path, corpus, kat, unsigned):
     empty.write_bytes(b"")
     check = tmp_path / "check"
     check.write_bytes(b"123456789")
-    r = _run(paths + [str(empty), str(check)], env={"FDFS_UNSIGNED_HASH": "1" if unsigned else "0"})
+    r = _run((["-u"] if unsigned else []) + paths + [str(empty), str(check)])
     assert r.returncode == 0, r.stdout
     got = [int(x) for x in r.stdout.split()]
     key = "crc_unsigned" if unsigned else "crc_signed"
