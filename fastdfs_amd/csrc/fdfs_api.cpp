@@ -190,6 +190,32 @@ struct WsScope {
     ~WsScope() { ws_leave(ctx, st); }
 };
 
+// The lane path's device error word (fdfs::kLaneErrWord) reaches the host
+// through a pinned word: copied after every lane launch, checked at the
+// start of the context's next call, which then fails with EIO.
+uint32_t *lane_err_host(fdfs_gpu_ctx *ctx)
+{
+    return reinterpret_cast<uint32_t *>(ctx->hann + 64 * kAnnTail + 64 * kAnnMax + 2);
+}
+
+hipError_t lane_err_note(fdfs_gpu_ctx *ctx, const uint32_t *hist, hipStream_t st)
+{
+    return hipMemcpyAsync(lane_err_host(ctx), hist + fdfs::kLaneErrWord, 4, hipMemcpyDeviceToHost, st);
+}
+
+int lane_err_check(fdfs_gpu_ctx *ctx)
+{
+    volatile uint32_t *h = lane_err_host(ctx);
+    const uint32_t v = *h;
+    if (!v)
+        return 0;
+    *h = 0;
+    std::snprintf(ctx->err, sizeof(ctx->err),
+                  "an earlier signature call on this context found its size binning inconsistent "
+                  "(device error word 0x%x): its outputs are invalid", v);
+    return EIO;
+}
+
 // Grow a context-owned device buffer (like ensure_ws: the last call that
 // used the context's buffers must be done before the old one is freed).
 int ensure_buf(fdfs_gpu_ctx *ctx, void **buf, size_t *have, size_t bytes, hipStream_t st)
@@ -459,6 +485,8 @@ int fdfs_gpu_sig_batch(fdfs_gpu_ctx *ctx, const fdfs_gpu_batch *batch, int metho
     if (!batch->base || !batch->offset || !batch->size || !crc_out)
         return EINVAL;
     std::lock_guard<std::recursive_mutex> lk(ctx->mu);
+    if (int rc0 = lane_err_check(ctx))
+        return rc0;
     DeviceGuard g(ctx->device);
     if (!g.ok)
         return ENODEV;
@@ -487,6 +515,8 @@ int fdfs_gpu_sig_batch(fdfs_gpu_ctx *ctx, const fdfs_gpu_batch *batch, int metho
         e = fdfs::launch_sig_lane(ctx->sar, method, base, batch->offset, batch->size, n, hist,
                                   order, &big, ctx->d_tabs, crc_out, sig_out, codes_out, nullptr, nullptr,
                                   ctx->seg_grid, st, a, b);
+        if (e == hipSuccess)
+            e = lane_err_note(ctx, hist, st);
     }
     return e == hipSuccess ? 0 : fail(ctx, e, "sig_batch launch");
 }
@@ -526,6 +556,8 @@ static int update_batch(fdfs_gpu_ctx *ctx, const fdfs_gpu_batch *chunks, const u
     if (reinterpret_cast<uintptr_t>(states) & 15)
         return EINVAL;
     std::lock_guard<std::recursive_mutex> lk(ctx->mu);
+    if (int rc0 = lane_err_check(ctx))
+        return rc0;
     DeviceGuard g(ctx->device);
     if (!g.ok)
         return ENODEV;
@@ -576,6 +608,8 @@ static int update_batch(fdfs_gpu_ctx *ctx, const fdfs_gpu_batch *chunks, const u
         e = fdfs::launch_sig_lane(ctx->sar, method, base, chunks->offset, chunks->size, n, hist, order, &big,
                                   ctx->d_tabs, nullptr, nullptr, nullptr, states, state_idx, ctx->seg_grid,
                                   st, a, b);
+        if (e == hipSuccess)
+            e = lane_err_note(ctx, hist, st);
     }
     return e == hipSuccess ? 0 : fail(ctx, e, "update_batch launch");
 }
@@ -602,6 +636,8 @@ int fdfs_gpu_final_batch(fdfs_gpu_ctx *ctx, const fdfs_gpu_file_state *states,
         reinterpret_cast<uintptr_t>(codes_out) & 15)
         return EINVAL;
     std::lock_guard<std::recursive_mutex> lk(ctx->mu);
+    if (int rc0 = lane_err_check(ctx))
+        return rc0;
     DeviceGuard g(ctx->device);
     if (!g.ok)
         return ENODEV;
@@ -828,6 +864,8 @@ static int dedup_common(fdfs_gpu_ctx *ctx, const uint8_t *sig, uint32_t stride,
          reinterpret_cast<uintptr_t>(rep_out)) & 7)
         return EINVAL;
     std::lock_guard<std::recursive_mutex> lk(ctx->mu);
+    if (int rc0 = lane_err_check(ctx))
+        return rc0;
     DeviceGuard g(ctx->device);
     if (!g.ok)
         return ENODEV;

@@ -78,12 +78,14 @@ __device__ __forceinline__ void h4_lane(const uint32_t *sD, const Rep8Lane &R8, 
 }
 
 // (a & m) ^ 0x80808080 in one VALU op (v_bitop3_b32, truth table 0x6A):
-// the b - 128 int8 operand of a lane, zero data past the file's end.
+// the b - 128 int8 operand of a lane, zero data past the file's end.  A
+// builtin, not an asm statement: its result feeds the MFMA's A operand
+// directly, and only an instruction hipcc can see gets the VALU-write ->
+// MFMA-read wait states padded (round 2's asm form left one state where two
+// are required; tests/test_isa.py checks the shipped code object).
 __device__ __forceinline__ uint32_t and_xor80(uint32_t a, uint32_t m)
 {
-    uint32_t r;
-    asm("v_bitop3_b32 %0, %1, %2, %3 bitop3:0x6a" : "=v"(r) : "v"(a), "v"(m), "s"(0x80808080u));
-    return r;
+    return __builtin_amdgcn_bitop3_b32(a, m, 0x80808080u, 0x6a);
 }
 
 // Quad transpose of one dword position: lane j of a lane quad holds r_k =
@@ -150,11 +152,15 @@ __global__ __launch_bounds__(TM == 2 ? 1024 : kHashBlock) void sig_hash_kernel(
     if (wave0 >= n)  // whole wave past the batch (wave-uniform: MFMAs below need every lane)
         return;
     const uint32_t i = wave0 + lane;
-    const bool valid = i < n;
+    bool valid = i < n;
     const uint32_t K16 = TM == 2 ? tabs->t.K8 : tabs->t.K16;
     const Rep8Lane R8 = rep8_lane(lane);
     const uint8_t *safe = reinterpret_cast<const uint8_t *>(tabs);  // >= 128 readable bytes
-    const uint32_t f = valid ? order[i] : 0;
+    uint32_t f = valid ? order[i] : 0;
+    if (f >= n) {  // a stale order entry (the binning flagged it): no file
+        valid = false;
+        f = 0;
+    }
     const uint64_t L = valid ? sizes[f] : 0;
     const uint8_t *p = valid ? base + offs[f] : safe;
     uint32_t c = 0xFFFFFFFFu;  // CRC32_XINIT (storage/storage_service.c:7149)
@@ -560,14 +566,23 @@ hipError_t launch_sig_hash(bool sar, const uint8_t *base, const uint64_t *offs,
 #endif
     const unsigned blk = (tm == 2 && !states) ? 1024 : kHashBlock;
     const unsigned grid = (n + blk - 1) / blk;
+#ifdef FDFS_PROBES
+#define HASH_LAUNCH_TM2(S, M)                                                                            \
+    else if (tm == 2)                                                                                    \
+        sig_hash_kernel<S, 2, M, false, false><<<grid, blk, 0, st>>>(base, offs, sizes, order, n, tabs, big_min, \
+                                                                     crc_out, sig_out, codes_out, nullptr, nullptr);
+#else
+// the rotated-table form (TM 2, VGPR accumulators) exists in the probe
+// build only: the production library holds AGPR-accumulator kernels alone
+// (tests/test_isa.py)
+#define HASH_LAUNCH_TM2(S, M)
+#endif
 #define HASH_LAUNCH(S, M)                                                                                \
     do {                                                                                                 \
         if (states)                                                                                      \
             sig_hash_kernel<S, 0, M, true, true><<<grid, blk, 0, st>>>(base, offs, sizes, order, n, tabs, big_min, \
                                                                  crc_out, sig_out, codes_out, states, sidx); \
-        else if (tm == 2)                                                                                \
-            sig_hash_kernel<S, 2, M, false, false><<<grid, blk, 0, st>>>(base, offs, sizes, order, n, tabs, big_min, \
-                                                                  crc_out, sig_out, codes_out, nullptr, nullptr); \
+        HASH_LAUNCH_TM2(S, M)                                                                            \
         else if (ql)                                                                                     \
             sig_hash_kernel<S, 0, M, false, true><<<grid, blk, 0, st>>>(base, offs, sizes, order, n, tabs, big_min, \
                                                                   crc_out, sig_out, codes_out, nullptr, nullptr); \
@@ -587,6 +602,7 @@ hipError_t launch_sig_hash(bool sar, const uint8_t *base, const uint64_t *offs,
     else
         HASH_LAUNCH(false, 0);
 #undef HASH_LAUNCH
+#undef HASH_LAUNCH_TM2
     return hipGetLastError();
 }
 

@@ -12,7 +12,13 @@ struct DevTables;
 constexpr uint64_t kSegBytes = 64 * 1024;  // CRC segment owned by one wave
 constexpr int kSegBlock = 512;             // threads per crc_seg_kernel workgroup
 constexpr int kSizeBins = 2048;            // size bins of the lane-path counting sort
-constexpr int kLaneWsDwords = 2 * kSizeBins + 64;  // size-bin histogram + cursors + MD5 chunk queue
+constexpr int kLaneWsDwords = 2 * kSizeBins + 64;  // size-bin histogram + cursors + MD5 chunk queue + error word
+// Lane-path error word (zeroed with the histogram at every launch): bit 0 =
+// the size binning placed a file outside [0, n) or read a file index >= n
+// (a histogram that was not zero before counting); such files are skipped,
+// never read or written out of bounds.  The API copies it to the host after
+// the launch and fails the context's next call with EIO.
+constexpr int kLaneErrWord = 2 * kSizeBins + 32;
 
 // signature path (fdfs_sig.hip)
 uint64_t scan_workspace_elems(uint64_t n);

@@ -145,8 +145,12 @@ __global__ __launch_bounds__(64 * kMd5Waves) void md5_stage_kernel(
     for (; chunk < nw;) {
     const uint32_t wave0 = chunk * 64;
     const uint32_t i = wave0 + lane;
-    const bool valid = i < n;
-    const uint32_t f = valid ? order[i] : 0;
+    bool valid = i < n;
+    uint32_t f = valid ? order[i] : 0;
+    if (f >= n) {  // a stale order entry (the binning flagged it): no file
+        valid = false;
+        f = 0;
+    }
     const uint64_t L = valid ? sizes[f] : 0;
     const uint8_t *p = valid ? base + offs[f] : safe;
     const bool small = L < big_min;  // else the CRC comes from crc_seg_kernel

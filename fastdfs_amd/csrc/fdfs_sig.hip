@@ -398,7 +398,7 @@ constexpr int kBinItems = 8;
 
 __global__ __launch_bounds__(1024) void bin_scatter_kernel(const uint64_t *__restrict__ sizes,
                                                            uint32_t n, uint32_t *__restrict__ cursor,
-                                                           uint32_t *__restrict__ order)
+                                                           uint32_t *__restrict__ order, uint32_t *__restrict__ err)
 {
     __shared__ uint32_t cnt[kSizeBins];
     __shared__ uint32_t bas[kSizeBins];
@@ -424,8 +424,15 @@ __global__ __launch_bounds__(1024) void bin_scatter_kernel(const uint64_t *__res
 #pragma unroll
     for (int k = 0; k < kBinItems; k++) {
         const uint32_t i = i0 + k * blockDim.x;
-        if (i < n)
-            order[bas[bin[k]] + rank[k]] = i;
+        if (i < n) {
+            // a histogram that held counts before this batch's shifts the
+            // cursors: a position past n is an error, never a store
+            const uint32_t pos = bas[bin[k]] + rank[k];
+            if (pos < n)
+                order[pos] = i;
+            else
+                atomicOr(err, 1u);
+        }
     }
 }
 
@@ -581,7 +588,8 @@ __global__ __launch_bounds__(1024) void big_plan_kernel(
     const uint64_t *__restrict__ offs, const uint64_t *__restrict__ sizes, uint32_t n, int method,
     uint32_t lat_files, uint32_t md5_bin, uint32_t *__restrict__ nbig_out, uint64_t *__restrict__ big_min,
     uint64_t *__restrict__ boffs, uint64_t *__restrict__ bsizes,
-    uint64_t *__restrict__ seg_first, uint32_t *__restrict__ bcrc, uint32_t *__restrict__ bpoly)
+    uint64_t *__restrict__ seg_first, uint32_t *__restrict__ bcrc, uint32_t *__restrict__ bpoly,
+    uint32_t *__restrict__ err)
 {
     static_assert(kSizeBins == 2 * 1024, "two bins per thread");
     __shared__ uint32_t wsum[16];
@@ -694,8 +702,11 @@ __global__ __launch_bounds__(1024) void big_plan_kernel(
         uint64_t ns = 0;
         if (i < nbig) {
             const uint32_t f = order[i];
-            const uint64_t L = sizes[f];
-            boffs[i] = offs[f];
+            const bool ok = f < n;  // a stale order entry: skipped (an empty file) and flagged
+            if (!ok)
+                atomicOr(err, 1u);
+            const uint64_t L = ok ? sizes[f] : 0;
+            boffs[i] = ok ? offs[f] : 0;
             bsizes[i] = L;
             bcrc[i] = 0;  // crc_seg_kernel accumulates multi-segment files by XOR
             bpoly[2ull * i] = 0;  // poly_seg_kernel adds segment contributions
@@ -730,13 +741,15 @@ __global__ __launch_bounds__(1024) void big_plan_kernel(
 // After the lane kernel: the big files' segmented CRC, simple_hash and
 // Time33 into crc_out, their signature fields and codes[0], [2], [3].
 __global__ void big_patch_kernel(const uint32_t *__restrict__ nbig, const uint32_t *__restrict__ order,
-                                 const uint32_t *__restrict__ bcrc, const uint32_t *__restrict__ bpoly,
+                                 uint32_t n, const uint32_t *__restrict__ bcrc, const uint32_t *__restrict__ bpoly,
                                  bool md5, uint32_t *__restrict__ crc_out, uint8_t *__restrict__ sig_out,
                                  int32_t *__restrict__ codes_out)
 {
     const uint32_t nb = *nbig;
     for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < nb; i += gridDim.x * blockDim.x) {
         const uint32_t f = order[i], c = bcrc[i], s = bpoly[2ull * i], t = bpoly[2ull * i + 1];
+        if (f >= n)  // flagged by big_plan_kernel
+            continue;
         crc_out[f] = c;
         if (md5)  // the signature and codes hold the MD5 digest
             continue;
@@ -760,7 +773,7 @@ __global__ void big_patch_kernel(const uint32_t *__restrict__ nbig, const uint32
 // CRC32_ex(d, X) = FINAL-form crc ^ ~0 ^ M^|d| (X ^ ~0) and
 // h(d, X) = M^|d| X + h(d, 0) for simple_hash / Time33 (orders divide 2^30).
 __global__ void big_patch_state_kernel(const uint32_t *__restrict__ nbig, const uint32_t *__restrict__ order,
-                                       const uint32_t *__restrict__ bcrc, const uint32_t *__restrict__ bpoly,
+                                       uint32_t n, const uint32_t *__restrict__ bcrc, const uint32_t *__restrict__ bpoly,
                                        const uint64_t *__restrict__ sizes, const uint32_t *__restrict__ sidx,
                                        bool md5, fdfs_gpu_file_state *__restrict__ states,
                                        const DevTables *__restrict__ tabs)
@@ -768,6 +781,8 @@ __global__ void big_patch_state_kernel(const uint32_t *__restrict__ nbig, const 
     const uint32_t nb = *nbig;
     for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < nb; i += gridDim.x * blockDim.x) {
         const uint32_t f = order[i];
+        if (f >= n)  // flagged by big_plan_kernel
+            continue;
         const uint64_t L = sizes[f];
         fdfs_gpu_file_state *fs = states + (sidx ? sidx[f] : f);
         const uint32_t c = bcrc[i] ^ 0xFFFFFFFFu ^ advance_bytes(tabs->t, ~(uint32_t)fs->crc32, L);
@@ -800,6 +815,18 @@ hipError_t launch_zero_u32(void *p, uint64_t ndwords, hipStream_t st)
 {
     if (ndwords == 0)
         return hipSuccess;
+#ifdef FDFS_PROBES
+    // measurement build only: FDFS_GPU_MEMSET=1 restores round 2's
+    // hipMemsetAsync zeroing (scripts/graph_memset_probe.py dumps the
+    // captured graph it makes)
+    static int ms = -1;
+    if (ms < 0) {
+        const char *ev = getenv("FDFS_GPU_MEMSET");
+        ms = (ev && ev[0] == '1') ? 1 : 0;
+    }
+    if (ms)
+        return hipMemsetAsync(p, 0, 4 * ndwords, st);
+#endif
     uint64_t g = (ndwords + 255) / 256;
     zero_u32_kernel<<<(unsigned)(g < 4096 ? g : 4096), 256, 0, st>>>(static_cast<uint32_t *>(p), ndwords);
     return hipGetLastError();
@@ -881,12 +908,13 @@ hipError_t launch_sig_lane(bool sar, int method, const uint8_t *base, const uint
     const unsigned hb = (n + 1023) / 1024, sb = (n + 1024 * kBinItems - 1) / (1024 * kBinItems);
     bin_hist_kernel<<<hb < 128 ? hb : 128, 1024, 0, st>>>(sizes, n, hist);
     bin_scan_kernel<<<1, 1024, 0, st>>>(hist, cursor);
-    bin_scatter_kernel<<<sb, 1024, 0, st>>>(sizes, n, cursor, order);
+    uint32_t *err = hist + kLaneErrWord;
+    bin_scatter_kernel<<<sb, 1024, 0, st>>>(sizes, n, cursor, order, err);
     const bool offload = big != nullptr;
     if (offload) {  // CRC (HASH: simple_hash, Time33 too) of the files >= T by the segmented kernels, first
         big_plan_kernel<<<1, 1024, 0, st>>>(hist, order, offs, sizes, n, method, big->lat_files, big->md5_bin,
                                             big->nbig, big->big_min, big->offs, big->sizes, big->seg_first,
-                                            big->crc, big->poly);
+                                            big->crc, big->poly, err);
         hipStream_t ss = st;
         if (big->side) {  // fork: the segmented passes beside the lane kernel
             if ((e = hipEventRecord(big->fork, st)) != hipSuccess ||
@@ -917,10 +945,10 @@ hipError_t launch_sig_lane(bool sar, int method, const uint8_t *base, const uint
     if (offload && big->side && (e = hipStreamWaitEvent(st, big->join, 0)) != hipSuccess)
         return e;
     if (offload && states)
-        big_patch_state_kernel<<<256, 256, 0, st>>>(big->nbig, order, big->crc, big->poly, sizes, sidx,
+        big_patch_state_kernel<<<256, 256, 0, st>>>(big->nbig, order, n, big->crc, big->poly, sizes, sidx,
                                                     method == 2, states, tabs);
     else if (offload)
-        big_patch_kernel<<<256, 256, 0, st>>>(big->nbig, order, big->crc, big->poly, method == 2, crc_out,
+        big_patch_kernel<<<256, 256, 0, st>>>(big->nbig, order, n, big->crc, big->poly, method == 2, crc_out,
                                               sig_out, codes_out);
     return hipGetLastError();
 }
