@@ -564,13 +564,16 @@ hipError_t launch_sig_hash(bool sar, const uint8_t *base, const uint64_t *offs,
 #else
     constexpr int ql = 1;
 #endif
-    const unsigned blk = (tm == 2 && !states) ? 1024 : kHashBlock;
+    const unsigned blk = (tm >= 2 && !states) ? 1024 : kHashBlock;
     const unsigned grid = (n + blk - 1) / blk;
 #ifdef FDFS_PROBES
 #define HASH_LAUNCH_TM2(S, M)                                                                            \
     else if (tm == 2)                                                                                    \
         sig_hash_kernel<S, 2, M, false, false><<<grid, blk, 0, st>>>(base, offs, sizes, order, n, tabs, big_min, \
-                                                                     crc_out, sig_out, codes_out, nullptr, nullptr);
+                                                                     crc_out, sig_out, codes_out, nullptr, nullptr); \
+    else if (tm == 3)                                                                                    \
+        sig_hash_kernel<S, 2, M, false, true><<<grid, blk, 0, st>>>(base, offs, sizes, order, n, tabs, big_min, \
+                                                                    crc_out, sig_out, codes_out, nullptr, nullptr);
 #else
 // the rotated-table form (TM 2, VGPR accumulators) exists in the probe
 // build only: the production library holds AGPR-accumulator kernels alone

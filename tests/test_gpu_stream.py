@@ -357,7 +357,7 @@ def test_update_rejects_repeated_state(ctxs, method):
     data = torch.randint(0, 256, (n * 100,), dtype=torch.uint8, device="cuda")
     offs = torch.arange(n, dtype=torch.int64, device="cuda") * 100
     sizes = torch.full((n,), 100, dtype=torch.int64, device="cuda")
-    for bad in ([3, 3], [0, 4999], None):
+    for bad in ([3, 4], [0, 4999], None):
         idx = torch.randperm(n, device="cuda").to(torch.int32)
         if bad is None:
             idx[77] = -1  # 0xFFFFFFFF
