@@ -16,6 +16,8 @@ LIB_PATH = os.path.join(_HERE, "lib", "libfdfs_gpu.so")
 # environment.
 if os.environ.get("FDFS_GPU_PROBE_LIB") == "1":
     LIB_PATH = os.path.join(_HERE, "lib", "probes", "libfdfs_gpu.so")
+elif os.environ.get("FDFS_GPU_PROBE_LIB") == "ab":  # `make ab`: the previous form of a kernel, for A/B runs
+    LIB_PATH = os.path.join(_HERE, "lib", "ab", "libfdfs_gpu.so")
 HEADER_PATH = os.path.join(os.path.dirname(_HERE), "include", "fdfs_gpu.h")
 
 SIG_CRC_ONLY = 0

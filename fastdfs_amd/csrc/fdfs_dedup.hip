@@ -103,18 +103,28 @@ constexpr int kDpSplitThreads = 1024;
 constexpr int kDpSplitPer = 8;
 constexpr int kDpChunk = kDpSplitThreads * kDpSplitPer;  // entries per K4 chunk
 static_assert(kDpChunk < 65536, "chunk digit starts are u16");
-constexpr int kDpSlotsLog = 12;  // LDS table: 4096 slots (80 KB, two workgroups per CU)
+// LDS table of the group kernel: 2048 slots (40 KB) for partitions of up to
+// 1024 records (mean <= 768), four 512-thread workgroups per CU.  The group
+// is latency-bound (a chain of dependent global round trips per partition),
+// so what sets its rate is the number of partitions in flight per CU: four
+// half-size ones instead of round 2's two 4096-slot / 1024-thread ones, the
+// same 32 waves per CU.  FDFS_DP_TABLE_LOG=12 builds the round-2 form
+// (`make ab`, the A/B library).
+#ifndef FDFS_DP_TABLE_LOG
+#define FDFS_DP_TABLE_LOG 11
+#endif
+constexpr int kDpSlotsLog = FDFS_DP_TABLE_LOG;
 constexpr int kDpSlots = 1 << kDpSlotsLog;
 // Records per partition grouped in LDS: two entries per thread of the
-// 1024-thread group.  At three (cap 3072) the per-thread arrays of the
-// confirmation phase went past the 64 VGPRs of two workgroups per CU and
-// hipcc spilled them to scratch, serialising the three entries' row loads
-// into three round trips.  dp_plan keeps the mean partition at <= 1536
-// records, so a uniform key spread stays far below the cap; larger
-// partitions (heavy duplication, adversarial keys) take dp_group_slow.
+// group.  At three the per-thread arrays of the confirmation phase went past
+// the 64 VGPRs of 32 waves per CU and hipcc spilled them to scratch,
+// serialising the three entries' row loads into three round trips.
+// dp_plan keeps the mean partition at <= 3/4 of the cap, ~9 sigma below it
+// for uniform keys; larger partitions (heavy duplication, adversarial keys)
+// take dp_group_slow.
 constexpr uint32_t kDpCap = kDpSlots / 2;
 constexpr uint64_t kDpEmpty = ~0ull;
-constexpr int kDpGroupThreads = 1024;
+constexpr int kDpGroupThreads = kDpSlots / 4;
 constexpr int kDpRuns = kDpGroupThreads;  // chunk runs per K5 gather batch (one per thread)
 
 struct DpPlan {
@@ -127,8 +137,8 @@ struct DpPlan {
 
 DpPlan dp_plan(uint64_t n)
 {
-    int p = 1;  // partitions of ~1.5K records: mean n / 2^p <= 1536 (kDpCap = 2048)
-    while (p < kDpMaxD1 + kDpMaxD2 && (n >> p) > 1536)
+    int p = 1;  // partitions of mean n / 2^p <= 3/4 of kDpCap
+    while (p < kDpMaxD1 + kDpMaxD2 && (n >> p) > kDpCap / 4 * 3)
         p++;
     DpPlan pl;
     pl.d1 = p < kDpMaxD1 ? p : kDpMaxD1;
@@ -587,7 +597,7 @@ __device__ __forceinline__ uint64_t dp_src(uint32_t l, uint32_t nk, const uint32
 // members gets all k indices and a singleton reads none.
 constexpr int kDpEpt = (kDpCap + kDpGroupThreads - 1) / kDpGroupThreads;  // entries per thread
 
-struct DpLds {  // dp_group_kernel's LDS table (80 KB: two workgroups per CU)
+struct DpLds {  // dp_group_kernel's LDS table (20 B per slot: 40 KB, four workgroups per CU)
     uint64_t word[kDpSlots];
     uint64_t mn[kDpSlots];
     uint32_t cn[kDpSlots];
