@@ -128,6 +128,29 @@ __device__ __forceinline__ uint32_t chain16(const uint32_t *__restrict__ D, uint
     return r;
 }
 
+// chain16 in two halves (probe build, sig_hash_kernel MODE 3): the 16
+// lookups, then -- after other work has hidden their LDS latency -- the XOR
+// tree.
+__device__ __forceinline__ void chain16_issue(const uint32_t *__restrict__ D, uint32_t c, uint4 w,
+                                              uint32_t (&v)[16])
+{
+    const uint32_t x = c ^ w.x;
+    const uint32_t wd[4] = {x, w.y, w.z, w.w};
+#pragma unroll
+    for (int j = 0; j < 16; j++)
+        v[j] = D[j * 256 + ((wd[j >> 2] >> (8 * (j & 3))) & 0xFFu)];
+}
+
+template <bool SAR>
+__device__ __forceinline__ uint32_t chain16_finish(const uint32_t (&v)[16], uint32_t c, uint32_t K16)
+{
+    uint32_t r = xor3(xor3(v[0], v[1], v[2]), xor3(v[3], v[4], v[5]), xor3(v[6], v[7], v[8]));
+    r = xor3(r, xor3(v[9], v[10], v[11]), xor3(v[12], v[13], v[14])) ^ v[15];
+    if (SAR)
+        r ^= (uint32_t)((int32_t)c >> 31) & K16;
+    return r;
+}
+
 // Linear map given as 4 byte tables (LDS, [4][256]).
 __device__ __forceinline__ uint32_t apply4(const uint32_t *__restrict__ A, uint32_t v)
 {

@@ -127,8 +127,16 @@ __device__ __forceinline__ void quad_transpose(uint32_t &r0, uint32_t &r1, uint3
 // INIT_HASH_CODES4 and writes it back unfinalised; every step above is a
 // recurrence from whatever state it starts in (the polynomial planes start
 // from the lane's running value), so nothing else changes.
+// Four waves per SIMD (128 registers) is part of the design (DESIGN.md
+// 4.2): asked for explicitly, so that a variant over the budget spills
+// rather than silently dropping to three.
+#ifdef FDFS_AB_ROUND2  // `make ab`: the round-2 form
+#define HASH_WPE
+#else
+#define HASH_WPE __attribute__((amdgpu_waves_per_eu(4)))
+#endif
 template <bool SAR, int TM, int MODE, bool ST, bool QL>
-__global__ __launch_bounds__(TM == 2 ? 1024 : kHashBlock) void sig_hash_kernel(
+__global__ __launch_bounds__(TM == 2 ? 1024 : kHashBlock) HASH_WPE void sig_hash_kernel(
     const uint8_t *__restrict__ base, const uint64_t *__restrict__ offs,
     const uint64_t *__restrict__ sizes, const uint32_t *__restrict__ order, uint32_t n,
     const DevTables *__restrict__ tabs, const uint64_t *__restrict__ big_min_p,
@@ -271,7 +279,30 @@ __global__ __launch_bounds__(TM == 2 ? 1024 : kHashBlock) void sig_hash_kernel(
                         c ^= aq.x ^ aq.y ^ aq.z ^ aq.w;
                     continue;
                 }
-                if (ok) {
+                if constexpr (MODE == 3 && TM == 0) {  // PROBE: CRC lookups, ELF, then the CRC XOR tree
+                    if (ok) {
+                        uint32_t v[16];
+                        if (small)
+                            chain16_issue(sD, c, aq, v);
+                        __builtin_amdgcn_sched_barrier(0);
+                        elf_word4<SAR, false>(aq.x, e);
+                        elf_word4<SAR, false>(aq.y, e);
+                        elf_word4<SAR, false>(aq.z, e);
+                        elf_word4<SAR, true>(aq.w, e);
+                        __builtin_amdgcn_sched_barrier(0);
+                        if (small)
+                            c = chain16_finish<SAR>(v, c, K16);
+                    }
+                } else if constexpr (MODE == 4) {  // PROBE: ELF in the 3-op chain form
+                    if (ok) {
+                        if (small)
+                            c = crc16<SAR, TM>(sD, R8, K16, c, aq);
+                        elf_word4_chain<SAR, false>(aq.x, e);
+                        elf_word4_chain<SAR, false>(aq.y, e);
+                        elf_word4_chain<SAR, false>(aq.z, e);
+                        elf_word4_chain<SAR, true>(aq.w, e);
+                    }
+                } else if (ok) {
                     if (small)
                         c = crc16<SAR, TM>(sD, R8, K16, c, aq);
                     elf_word4<SAR, false>(aq.x, e);
@@ -540,7 +571,8 @@ hipError_t launch_sig_hash(bool sar, const uint8_t *base, const uint64_t *offs,
 {
 #ifdef FDFS_PROBES
     // measurement build only (make probes): FDFS_GPU_HASH_MODE 1 = loads
-    // only, 2 = compute only (wrong results); FDFS_GPU_HASH_TM CRC table form
+    // only, 2 = compute only (wrong results), 3 = CRC lookups / ELF / CRC
+    // XOR tree in that order, 4 = ELF in the 3-op chain form; FDFS_GPU_HASH_TM CRC table form
     // 0 = slice-by-16 bytes, 2 = rotated rep8
     static int mode = -1;
     if (mode < 0) {
@@ -598,6 +630,10 @@ hipError_t launch_sig_hash(bool sar, const uint8_t *base, const uint64_t *offs,
         HASH_LAUNCH(true, 1);
     else if (mode == 2)
         HASH_LAUNCH(true, 2);
+    else if (mode == 3)
+        HASH_LAUNCH(true, 3);
+    else if (mode == 4)
+        HASH_LAUNCH(true, 4);
     else
 #endif
     if (sar)
