@@ -127,16 +127,12 @@ __device__ __forceinline__ void quad_transpose(uint32_t &r0, uint32_t &r1, uint3
 // INIT_HASH_CODES4 and writes it back unfinalised; every step above is a
 // recurrence from whatever state it starts in (the polynomial planes start
 // from the lane's running value), so nothing else changes.
-// Four waves per SIMD (128 registers) is part of the design (DESIGN.md
-// 4.2): asked for explicitly, so that a variant over the budget spills
-// rather than silently dropping to three.
-#ifdef FDFS_AB_ROUND2  // `make ab`: the round-2 form
-#define HASH_WPE
-#else
-#define HASH_WPE __attribute__((amdgpu_waves_per_eu(4)))
-#endif
+// Occupancy: the production instantiations fit four waves per SIMD (128
+// registers) with AGPR accumulators as compiled.  Asking for four waves
+// explicitly made hipcc move the ST form's accumulators to VGPRs (caught by
+// tests/test_isa.py), so only the probe variant MODE 4 asks for it.
 template <bool SAR, int TM, int MODE, bool ST, bool QL>
-__global__ __launch_bounds__(TM == 2 ? 1024 : kHashBlock) HASH_WPE void sig_hash_kernel(
+__global__ __launch_bounds__(TM == 2 ? 1024 : kHashBlock) __attribute__((amdgpu_waves_per_eu(MODE == 4 ? 4 : 1))) void sig_hash_kernel(
     const uint8_t *__restrict__ base, const uint64_t *__restrict__ offs,
     const uint64_t *__restrict__ sizes, const uint32_t *__restrict__ order, uint32_t n,
     const DevTables *__restrict__ tabs, const uint64_t *__restrict__ big_min_p,
