@@ -132,7 +132,7 @@ __device__ __forceinline__ void quad_transpose(uint32_t &r0, uint32_t &r1, uint3
 // explicitly made hipcc move the ST form's accumulators to VGPRs (caught by
 // tests/test_isa.py), so only the probe variant MODE 4 asks for it.
 template <bool SAR, int TM, int MODE, bool ST, bool QL>
-__global__ __launch_bounds__(TM == 2 ? 1024 : kHashBlock) __attribute__((amdgpu_waves_per_eu(MODE == 4 ? 4 : 1))) void sig_hash_kernel(
+__global__ __launch_bounds__(TM == 2 || MODE == 5 ? 1024 : kHashBlock) __attribute__((amdgpu_waves_per_eu(MODE == 4 ? 4 : 1))) void sig_hash_kernel(
     const uint8_t *__restrict__ base, const uint64_t *__restrict__ offs,
     const uint64_t *__restrict__ sizes, const uint32_t *__restrict__ order, uint32_t n,
     const DevTables *__restrict__ tabs, const uint64_t *__restrict__ big_min_p,
@@ -568,7 +568,8 @@ hipError_t launch_sig_hash(bool sar, const uint8_t *base, const uint64_t *offs,
 #ifdef FDFS_PROBES
     // measurement build only (make probes): FDFS_GPU_HASH_MODE 1 = loads
     // only, 2 = compute only (wrong results), 3 = CRC lookups / ELF / CRC
-    // XOR tree in that order, 4 = ELF in the 3-op chain form; FDFS_GPU_HASH_TM CRC table form
+    // XOR tree in that order, 4 = ELF in the 3-op chain form, 5 = production
+    // code in 1024-thread workgroups; FDFS_GPU_HASH_TM CRC table form
     // 0 = slice-by-16 bytes, 2 = rotated rep8
     static int mode = -1;
     if (mode < 0) {
@@ -581,7 +582,7 @@ hipError_t launch_sig_hash(bool sar, const uint8_t *base, const uint64_t *offs,
         tm = ev ? atoi(ev) : 0;
     }
 #else
-    constexpr int tm = 0;
+    [[maybe_unused]] constexpr int tm = 0;
 #endif
 #ifdef FDFS_PROBES
     static int ql = -1;  // FDFS_GPU_HASH_QUAD=0: round-2 lane-per-file loads
@@ -592,7 +593,11 @@ hipError_t launch_sig_hash(bool sar, const uint8_t *base, const uint64_t *offs,
 #else
     constexpr int ql = 1;
 #endif
-    const unsigned blk = (tm >= 2 && !states) ? 1024 : kHashBlock;
+#ifdef FDFS_PROBES
+    const unsigned blk = ((tm >= 2 || mode == 5) && !states) ? 1024 : kHashBlock;
+#else
+    const unsigned blk = kHashBlock;
+#endif
     const unsigned grid = (n + blk - 1) / blk;
 #ifdef FDFS_PROBES
 #define HASH_LAUNCH_TM2(S, M)                                                                            \
@@ -630,6 +635,8 @@ hipError_t launch_sig_hash(bool sar, const uint8_t *base, const uint64_t *offs,
         HASH_LAUNCH(true, 3);
     else if (mode == 4)
         HASH_LAUNCH(true, 4);
+    else if (mode == 5)  // production code in 1024-thread workgroups (the TM 2/3 block size)
+        HASH_LAUNCH(true, 5);
     else
 #endif
     if (sar)
