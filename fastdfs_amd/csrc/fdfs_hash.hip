@@ -141,14 +141,21 @@ __global__ __launch_bounds__(TM == 2 || MODE == 5 ? 1024 : kHashBlock) __attribu
 {
     __shared__ uint32_t sD[TM == 2 ? kRep8Dwords : 16 * 256];
     __shared__ uint32_t sT[256];
-    __shared__ uint4 sB[2 * 8 * 64];
+    // SV vectors per step: 8 (one 128-byte line) or, probe MODE 6, 4 (half
+    // a line: two 16-VGPR load sets instead of two of 32, and only B's last
+    // four vectors in LDS)
+    constexpr int SV = MODE == 6 ? 4 : 8;
+    constexpr uint32_t SB = 16 * SV;  // bytes per step
+    __shared__ uint4 sB[2 * SV * 64];
     if constexpr (TM == 2)
         lds_fill_rep8(sD, &tabs->t.D[0][0]);
     else
         lds_fill(sD, &tabs->t.D[0][0], 16 * 256);
     lds_fill(sT, tabs->t.T, 256);
-    lds_fill(reinterpret_cast<uint32_t *>(sB), reinterpret_cast<const uint32_t *>(&tabs->pm.B[0][0][0][0]),
-             2 * 8 * 64 * 4);
+#pragma unroll
+    for (int h = 0; h < 2; h++)
+        lds_fill(reinterpret_cast<uint32_t *>(sB + h * SV * 64),
+                 reinterpret_cast<const uint32_t *>(&tabs->pm.B[h][8 - SV][0][0]), SV * 64 * 4);
     __syncthreads();
 
     const int lane = threadIdx.x & 63;
@@ -200,14 +207,14 @@ __global__ __launch_bounds__(TM == 2 || MODE == 5 ? 1024 : kHashBlock) __attribu
     }
     const uint4 *v = reinterpret_cast<const uint4 *>(p + head);
     const uint64_t nvec = (L - head) >> 4;
-    uint64_t lead = ((128u - ((uintptr_t)v & 127u)) & 127u) >> 4;
+    uint64_t lead = ((SB - ((uintptr_t)v & (SB - 1))) & (SB - 1)) >> 4;
     if (lead > nvec)
         lead = nvec;
     for (uint64_t j = 0; j < lead; j++)
         h4_lane<SAR, TM>(sD, R8, K16, v[j], small, c, e, s, t);
 
-    // whole 128-byte lines: the wave steps in lockstep to its longest file
-    const uint32_t nsteps = (uint32_t)((nvec - lead) >> 3);
+    // whole steps: the wave steps in lockstep to its longest file
+    const uint32_t nsteps = (uint32_t)((nvec - lead) / SV);
     uint32_t nmax = nsteps;
 #pragma unroll
     for (int o = 32; o; o >>= 1) {
@@ -215,10 +222,13 @@ __global__ __launch_bounds__(TM == 2 || MODE == 5 ? 1024 : kHashBlock) __attribu
         nmax = y > nmax ? y : nmax;
     }
     if (nmax) {
-        const uint32_t m31 = tabs->pm.m128[0], m33 = tabs->pm.m128[1];
+        const uint32_t m31 = SV == 8 ? tabs->pm.m128[0] : tabs->pm.m64[0];
+        const uint32_t m33 = SV == 8 ? tabs->pm.m128[1] : tabs->pm.m64[1];
         const int col = lane & 15, j = col & 3, g = col >> 2;
-        const i32x4 k31 = {tabs->pm.K[0][j], tabs->pm.K[0][j], tabs->pm.K[0][j], tabs->pm.K[0][j]};
-        const i32x4 k33 = {tabs->pm.K[1][j], tabs->pm.K[1][j], tabs->pm.K[1][j], tabs->pm.K[1][j]};
+        const int32_t kk31 = SV == 8 ? tabs->pm.K[0][j] : tabs->pm.K64[0][j];
+        const int32_t kk33 = SV == 8 ? tabs->pm.K[1][j] : tabs->pm.K64[1][j];
+        const i32x4 k31 = {kk31, kk31, kk31, kk31};
+        const i32x4 k33 = {kk33, kk33, kk33, kk33};
         // accumulator element r of this lane: plane j of the file in lane
         // 16 g + 4 (lane >> 4) + r; plane 0 starts from the lane-serial state
         i32x4 C31, C33;
@@ -239,7 +249,7 @@ __global__ __launch_bounds__(TM == 2 || MODE == 5 ? 1024 : kHashBlock) __attribu
         // QL: the step's pieces arrive quad-interleaved (issue_q below) and
         // are transposed back to their files' lanes, one half line at a time
         // just before its four vectors are hashed.
-        auto qtr = [](u32x4 (&a)[8], int h) {
+        auto qtr = [](u32x4 (&a)[SV], int h) {
 #pragma unroll
             for (int d = 0; d < 4; d++) {
                 uint32_t r0 = a[4 * h + 0][d], r1 = a[4 * h + 1][d], r2 = a[4 * h + 2][d], r3 = a[4 * h + 3][d];
@@ -250,7 +260,7 @@ __global__ __launch_bounds__(TM == 2 || MODE == 5 ? 1024 : kHashBlock) __attribu
                 a[4 * h + 3][d] = r3;
             }
         };
-        auto step = [&](u32x4 (&a)[8], bool ok) {
+        auto step = [&](u32x4 (&a)[SV], bool ok) {
             const bool mon = __any(ok && small);
             nexec += mon ? 1u : 0u;
 #pragma unroll
@@ -261,7 +271,7 @@ __global__ __launch_bounds__(TM == 2 || MODE == 5 ? 1024 : kHashBlock) __attribu
                 C33[r] = (int)((uint32_t)C33[r] * m33) + k33[r];
             }
 #pragma unroll
-            for (int q = 0; q < 8; q++) {
+            for (int q = 0; q < SV; q++) {
                 if constexpr (QL && MODE != 1) {
                     if ((q & 3) == 0) {
                         __builtin_amdgcn_sched_barrier(0);
@@ -312,7 +322,8 @@ __global__ __launch_bounds__(TM == 2 || MODE == 5 ? 1024 : kHashBlock) __attribu
                 const uint32_t msk = ok ? 0xFFFFFFFFu : 0u;
                 const i32x4 A = {(int)and_xor80(aq.x, msk), (int)and_xor80(aq.y, msk),
                                  (int)and_xor80(aq.z, msk), (int)and_xor80(aq.w, msk)};
-                const uint4 b31 = sB[(0 * 8 + q) * 64 + lane], b33 = sB[(1 * 8 + q) * 64 + lane];
+                // the step's vector q carries coefficients M^(SB-1-pos): B's vectors 8 - SV + q
+                const uint4 b31 = sB[(0 * SV + q) * 64 + lane], b33 = sB[(1 * SV + q) * 64 + lane];
                 const i32x4 B31 = {(int)b31.x, (int)b31.y, (int)b31.z, (int)b31.w};
                 const i32x4 B33 = {(int)b33.x, (int)b33.y, (int)b33.z, (int)b33.w};
                 C31 = __builtin_amdgcn_mfma_i32_16x16x64_i8(A, B31, C31, 0, 0, 0);
@@ -323,11 +334,11 @@ __global__ __launch_bounds__(TM == 2 || MODE == 5 ? 1024 : kHashBlock) __attribu
         // register sets, asm loads (hipcc would sink plain loads to their
         // use), issued unconditionally (past-the-end steps read `safe`) so no
         // register an asm load is still writing is ever copied.
-        u32x4 RA[8], RB[8];
-        auto issue = [&](u32x4 (&R)[8], uint32_t stp) {
-            const uint8_t *ln = (MODE != 2 && stp < nsteps) ? reinterpret_cast<const uint8_t *>(w + 8 * (uint64_t)stp) : safe;
+        u32x4 RA[SV], RB[SV];
+        auto issue = [&](u32x4 (&R)[SV], uint32_t stp) {
+            const uint8_t *ln = (MODE != 2 && stp < nsteps) ? reinterpret_cast<const uint8_t *>(w + SV * (uint64_t)stp) : safe;
 #pragma unroll
-            for (int q = 0; q < 8; q++)
+            for (int q = 0; q < SV; q++)
                 asm volatile("global_load_dwordx4 %0, %1, off offset:%2" : "=v"(R[q]) : "v"(ln), "i"(16 * q) : "memory");
         };
         // Quad-cooperative form (QL): lane j of quad Q loads 16-byte piece
@@ -336,33 +347,43 @@ __global__ __launch_bounds__(TM == 2 || MODE == 5 ? 1024 : kHashBlock) __attribu
         // 16-byte pieces (4x fewer lines and pages per instruction; loads
         // alone 6.8 -> 6.0 ms on config 2, profiles/r02/hash_quad_ab.md).
         // The quad's line addresses are broadcast by DPP quad_perm.
-        auto issue_q = [&](u32x4 (&R)[8], uint32_t stp) {
-            const uint8_t *ln = (MODE != 2 && stp < nsteps) ? reinterpret_cast<const uint8_t *>(w + 8 * (uint64_t)stp) : safe;
+        auto issue_q = [&](u32x4 (&R)[SV], uint32_t stp) {
+            const uint8_t *ln = (MODE != 2 && stp < nsteps) ? reinterpret_cast<const uint8_t *>(w + SV * (uint64_t)stp) : safe;
             const uint64_t a = reinterpret_cast<uint64_t>(ln);
             const uint32_t lo = (uint32_t)a, hi = (uint32_t)(a >> 32);
-            auto ld = [&](u32x4 &R0, u32x4 &R1, uint32_t lk, uint32_t hk) {
+            auto ld = [&](int k, uint32_t lk, uint32_t hk) {
                 const uint8_t *pk = reinterpret_cast<const uint8_t *>(((uint64_t)hk << 32 | lk) + 16u * (lane & 3));
-                asm volatile("global_load_dwordx4 %0, %1, off offset:0" : "=v"(R0) : "v"(pk) : "memory");
-                asm volatile("global_load_dwordx4 %0, %1, off offset:64" : "=v"(R1) : "v"(pk) : "memory");
+                asm volatile("global_load_dwordx4 %0, %1, off offset:0" : "=v"(R[k]) : "v"(pk) : "memory");
+                if constexpr (SV == 8)
+                    asm volatile("global_load_dwordx4 %0, %1, off offset:64" : "=v"(R[k + 4]) : "v"(pk) : "memory");
             };
 #define QBC(K) (uint32_t) __builtin_amdgcn_mov_dpp((int)lo, 0x55 * K, 0xF, 0xF, false), \
                (uint32_t) __builtin_amdgcn_mov_dpp((int)hi, 0x55 * K, 0xF, 0xF, false)
-            ld(R[0], R[4], QBC(0));
-            ld(R[1], R[5], QBC(1));
-            ld(R[2], R[6], QBC(2));
-            ld(R[3], R[7], QBC(3));
+            ld(0, QBC(0));
+            ld(1, QBC(1));
+            ld(2, QBC(2));
+            ld(3, QBC(3));
 #undef QBC
         };
-        auto wait_older = [&](u32x4 (&R)[8]) {  // R is the older of the two sets in flight
-            asm volatile("s_waitcnt vmcnt(8)" : "+v"(R[0]), "+v"(R[1]), "+v"(R[2]), "+v"(R[3]) :: "memory");
-            asm volatile("" : "+v"(R[4]), "+v"(R[5]), "+v"(R[6]), "+v"(R[7]));
+        auto wait_older = [&](u32x4 (&R)[SV]) {  // R is the older of the two sets in flight
+            if constexpr (SV == 8) {
+                asm volatile("s_waitcnt vmcnt(8)" : "+v"(R[0]), "+v"(R[1]), "+v"(R[2]), "+v"(R[3]) :: "memory");
+                asm volatile("" : "+v"(R[4]), "+v"(R[5]), "+v"(R[6]), "+v"(R[7]));
+            } else {
+                asm volatile("s_waitcnt vmcnt(4)" : "+v"(R[0]), "+v"(R[1]), "+v"(R[2]), "+v"(R[3]) :: "memory");
+            }
         };
         auto drain = [&]() {
-            asm volatile("s_waitcnt vmcnt(0)"
-                         : "+v"(RA[0]), "+v"(RA[1]), "+v"(RA[2]), "+v"(RA[3]), "+v"(RA[4]), "+v"(RA[5]),
-                           "+v"(RA[6]), "+v"(RA[7]) :: "memory");
-            asm volatile("" : "+v"(RB[0]), "+v"(RB[1]), "+v"(RB[2]), "+v"(RB[3]), "+v"(RB[4]), "+v"(RB[5]),
-                              "+v"(RB[6]), "+v"(RB[7]));
+            if constexpr (SV == 8) {
+                asm volatile("s_waitcnt vmcnt(0)"
+                             : "+v"(RA[0]), "+v"(RA[1]), "+v"(RA[2]), "+v"(RA[3]), "+v"(RA[4]), "+v"(RA[5]),
+                               "+v"(RA[6]), "+v"(RA[7]) :: "memory");
+                asm volatile("" : "+v"(RB[0]), "+v"(RB[1]), "+v"(RB[2]), "+v"(RB[3]), "+v"(RB[4]), "+v"(RB[5]),
+                                  "+v"(RB[6]), "+v"(RB[7]));
+            } else {
+                asm volatile("s_waitcnt vmcnt(0)" : "+v"(RA[0]), "+v"(RA[1]), "+v"(RA[2]), "+v"(RA[3]) :: "memory");
+                asm volatile("" : "+v"(RB[0]), "+v"(RB[1]), "+v"(RB[2]), "+v"(RB[3]));
+            }
         };
         // Small lanes only ever end, so the steps where a lane below big_min
         // is still hashing are a prefix [0, nfull) of the wave's steps.  The
@@ -375,7 +396,7 @@ __global__ __launch_bounds__(TM == 2 || MODE == 5 ? 1024 : kHashBlock) __attribu
             nfull = y > nfull ? y : nfull;
         }
         if (nfull) {
-            auto iss = [&](u32x4 (&R)[8], uint32_t stp) {
+            auto iss = [&](u32x4 (&R)[SV], uint32_t stp) {
                 if constexpr (QL)
                     issue_q(R, stp);
                 else
@@ -393,11 +414,11 @@ __global__ __launch_bounds__(TM == 2 || MODE == 5 ? 1024 : kHashBlock) __attribu
             }
             drain();
         }
-        auto step_chain = [&](u32x4 (&a)[8], bool ok) {
+        auto step_chain = [&](u32x4 (&a)[SV], bool ok) {
             if (MODE == 1 || !ok)
                 return;
 #pragma unroll
-            for (int q = 0; q < 8; q++) {
+            for (int q = 0; q < SV; q++) {
                 elf_word4_chain<SAR, false>(a[q][0], e);
                 elf_word4_chain<SAR, false>(a[q][1], e);
                 elf_word4_chain<SAR, false>(a[q][2], e);
@@ -418,7 +439,7 @@ __global__ __launch_bounds__(TM == 2 || MODE == 5 ? 1024 : kHashBlock) __attribu
             drain();
         }
         // planes -> value: sum_j P_j << 8j over the lane quad (j = lane & 3),
-        // then back to the file's lane; undo the padded steps (M^-128 each)
+        // then back to the file's lane; undo the padded steps (M^-SB each)
         uint32_t s31 = 0, s33 = 0;
 #pragma unroll
         for (int r = 0; r < 4; r++) {
@@ -436,11 +457,11 @@ __global__ __launch_bounds__(TM == 2 || MODE == 5 ? 1024 : kHashBlock) __attribu
             }
         }
         const uint32_t pad = nexec - nsteps;  // (garbage for big-file lanes: patched)
-        s = s31 * pow_dev(tabs->pm.inv128[0], pad);
-        t = s33 * pow_dev(tabs->pm.inv128[1], pad);
+        s = s31 * pow_dev(SV == 8 ? tabs->pm.inv128[0] : tabs->pm.inv64[0], pad);
+        t = s33 * pow_dev(SV == 8 ? tabs->pm.inv128[1] : tabs->pm.inv64[1], pad);
     }
 
-    for (uint64_t jv = lead + 8 * (uint64_t)nsteps; jv < nvec; jv++)
+    for (uint64_t jv = lead + SV * (uint64_t)nsteps; jv < nvec; jv++)
         h4_lane<SAR, TM>(sD, R8, K16, v[jv], small, c, e, s, t);
     for (uint64_t k = head + (nvec << 4); k < L; k++) {  // the last (L - head) & 15 bytes
         const uint32_t b = p[k];
@@ -637,6 +658,8 @@ hipError_t launch_sig_hash(bool sar, const uint8_t *base, const uint64_t *offs,
         HASH_LAUNCH(true, 4);
     else if (mode == 5)  // production code in 1024-thread workgroups (the TM 2/3 block size)
         HASH_LAUNCH(true, 5);
+    else if (mode == 6)  // 64-byte steps: two 16-VGPR load sets
+        HASH_LAUNCH(true, 6);
     else
 #endif
     if (sar)

@@ -153,22 +153,29 @@ void build_poly_mfma_tables(PolyMfmaTables &t)
     std::memset(&t, 0, sizeof(t));
     const uint32_t M[2] = {31u, 33u};
     for (int h = 0; h < 2; h++) {
-        int64_t ksum[4] = {0, 0, 0, 0};
+        int64_t ksum[4] = {0, 0, 0, 0}, ksum64[4] = {0, 0, 0, 0};
         for (int pos = 0; pos < 128; pos++) {
             int d[4];
             digits4(pow_u32(M[h], 127 - pos), d);
-            for (int j = 0; j < 4; j++)
+            for (int j = 0; j < 4; j++) {
                 ksum[j] += d[j];
+                if (pos >= 64)
+                    ksum64[j] += d[j];
+            }
             const int q = pos >> 4, e = pos & 15;
             for (int lane = 0; lane < 64; lane++) {
                 const int col = lane & 15, kb = col >> 2, j = col & 3, g = lane >> 4;
                 t.B[h][q][lane][e] = (g == kb) ? (int8_t)d[j] : (int8_t)0;
             }
         }
-        for (int j = 0; j < 4; j++)
+        for (int j = 0; j < 4; j++) {
             t.K[h][j] = (int32_t)(uint32_t)(128 * ksum[j]);
+            t.K64[h][j] = (int32_t)(uint32_t)(128 * ksum64[j]);
+        }
         t.m128[h] = pow_u32(M[h], 128);
         t.inv128[h] = inv_u32(t.m128[h]);
+        t.m64[h] = pow_u32(M[h], 64);
+        t.inv64[h] = inv_u32(t.m64[h]);
     }
 }
 

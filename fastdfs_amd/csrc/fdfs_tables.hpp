@@ -39,6 +39,10 @@ struct PolyMfmaTables {
     int32_t K[2][4];         // per plane: 128 * sum over the step of the digits
     uint32_t m128[2];        // M^128 mod 2^32
     uint32_t inv128[2];      // M^-128 mod 2^32
+    // the same for 64-byte steps (vectors q = 4..7 of B: coefficients M^63..M^0)
+    int32_t K64[2][4];
+    uint32_t m64[2];
+    uint32_t inv64[2];
 };
 
 void build_poly_mfma_tables(PolyMfmaTables &t);
