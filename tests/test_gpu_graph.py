@@ -12,7 +12,11 @@ nothing is cached), and must equal the eager calls.
 History: with the lane path's size histogram cleared by hipMemsetAsync, the
 captured HASH batch + dedup replayed correctly once and faulted (illegal
 address) on the second replay; every zeroing in the library is now a
-kernel (launch_zero_u32), and the sequence replays exactly.
+kernel (launch_zero_u32), and the sequence replays exactly.  Round 3 showed
+why (profiles/r03/graph_*): the memset node is ordered
+and sized correctly, but its region is not zero on replays after the first,
+so the histogram is stale; the binning now clamps instead of storing out of
+bounds and the next call reports EIO.
 """
 import numpy as np
 import pytest
