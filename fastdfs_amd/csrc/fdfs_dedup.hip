@@ -371,6 +371,17 @@ __global__ void dp_chunk_ta_kernel(const uint64_t *__restrict__ off1, uint64_t t
 // then ranked by the d2 digit in LDS and the chunk goes back contiguously.
 constexpr int64_t kDpNoMark = INT64_MIN;
 
+// The position -> source buffer is stored swizzled: position i at
+// dp_sw(i), which permutes the 16-byte pairs inside each 64-byte row of 8
+// positions by bits 4-5 of i.  The max-scan reads a thread's own row with
+// 16-byte loads at a 64-byte stride; unswizzled, those rows land on the same
+// banks for every other lane (before: 119M of 177M LDS-active cycles were
+// bank conflicts, profiles/r03/dedup_pmc.txt), swizzled the 8 lanes of each
+// 128-byte LDS pass hit 8 distinct 16-byte bank groups.  Position-order
+// accesses (lane l at position base + l) stay conflict-free: the
+// permutation does not leave a row.
+__device__ __forceinline__ uint32_t dp_sw(uint32_t i) { return i ^ (((i >> 4) & 3u) << 1); }
+
 // NB: digit bins (1 << d2 <= NB); 1024 bins keep the LDS at 72 KB, two
 // workgroups per CU.
 template <int NB>
@@ -382,7 +393,8 @@ __global__ __launch_bounds__(kDpSplitThreads) void dp_split_kernel(
     constexpr int NT = kDpSplitThreads;
     constexpr int PER = NB / NT;
     static_assert(NB % NT == 0, "bins per thread");
-    __shared__ int64_t buf[kDpChunk];  // position -> source offset, then the digit-sorted chunk
+    static_assert(kDpSplitPer == 8, "one 64-byte row of positions per thread");
+    __shared__ int64_t buf[kDpChunk];  // position -> source offset (swizzled), then the digit-sorted chunk
     __shared__ uint32_t cc[NB];        // chunk digit counts
     __shared__ uint32_t cl[NB];        // chunk digit starts
     __shared__ uint32_t wsum[NT / 64];
@@ -405,39 +417,49 @@ __global__ __launch_bounds__(kDpSplitThreads) void dp_split_kernel(
     for (uint32_t k = threadIdx.x; k < nd2; k += NT)
         cc[k] = 0;
     for (uint32_t i = threadIdx.x; i < m; i += NT)
-        buf[i] = kDpNoMark;
+        buf[dp_sw(i)] = kDpNoMark;
     __syncthreads();
     for (uint32_t t = ta + threadIdx.x; t <= tb; t += NT) {
         const uint64_t o = ob[t], o2 = ob[t + 1];
         const uint64_t lo = o > P0 ? o : P0;
         const uint64_t hi = o2 < P0 + m ? o2 : P0 + m;
         if (lo < hi)
-            buf[lo - P0] = (int64_t)((uint64_t)t * kDpTile + lb[t]) - (int64_t)o;
+            buf[dp_sw((uint32_t)(lo - P0))] = (int64_t)((uint64_t)t * kDpTile + lb[t]) - (int64_t)o;
     }
     __syncthreads();
-    // carry each mark over its run: thread owns positions [i0, i0 + PER8)
+    // carry each mark over its run: thread owns positions [i0, i0 + 8), one
+    // row, read as four 16-byte pairs (pair j of the row sits at j ^ sw)
     const uint32_t i0 = threadIdx.x * kDpSplitPer;
+    const uint32_t sw = (threadIdx.x >> 1) & 3u;
+    uint4 *bufv = reinterpret_cast<uint4 *>(buf);
     int64_t bv[kDpSplitPer];
+#pragma unroll
+    for (int j = 0; j < kDpSplitPer / 2; j++) {
+        const uint4 v = bufv[threadIdx.x * 4 + (j ^ sw)];
+        bv[2 * j] = (int64_t)((uint64_t)v.x | (uint64_t)v.y << 32);
+        bv[2 * j + 1] = (int64_t)((uint64_t)v.z | (uint64_t)v.w << 32);
+    }
     int32_t lp = -1;
 #pragma unroll
     for (int q = 0; q < kDpSplitPer; q++)
-        if (i0 + q < m && buf[i0 + q] != kDpNoMark)
+        if (i0 + q < m && bv[q] != kDpNoMark)
             lp = (int32_t)(i0 + q);
-    int32_t cur = block_max_excl(lp, wmax);
+    const int32_t cur = block_max_excl(lp, wmax);
+    // the mark carried in from the threads before (position 0 is always
+    // marked, chunk_ta), then this row's own marks
+    int64_t val = cur >= 0 ? buf[dp_sw((uint32_t)cur)] : 0;
 #pragma unroll
     for (int q = 0; q < kDpSplitPer; q++) {
-        bv[q] = 0;
-        if (i0 + q < m) {
-            if (buf[i0 + q] != kDpNoMark)
-                cur = (int32_t)(i0 + q);
-            bv[q] = buf[cur];  // position 0 is always marked (chunk_ta)
-        }
+        if (bv[q] != kDpNoMark)
+            val = bv[q];
+        bv[q] = val;  // positions >= m: unused
     }
     __syncthreads();
 #pragma unroll
-    for (int q = 0; q < kDpSplitPer; q++)
-        if (i0 + q < m)
-            buf[i0 + q] = bv[q];
+    for (int j = 0; j < kDpSplitPer / 2; j++)
+        bufv[threadIdx.x * 4 + (j ^ sw)] =
+            make_uint4((uint32_t)bv[2 * j], (uint32_t)((uint64_t)bv[2 * j] >> 32), (uint32_t)bv[2 * j + 1],
+                       (uint32_t)((uint64_t)bv[2 * j + 1] >> 32));
     __syncthreads();
     const int sh = 64 - d1 - d2;  // d2 digit = (entry >> sh) & (nd2 - 1)
     uint64_t en[kDpSplitPer];
@@ -446,7 +468,7 @@ __global__ __launch_bounds__(kDpSplitThreads) void dp_split_kernel(
     for (int q = 0; q < kDpSplitPer; q++) {
         const uint32_t l = q * NT + threadIdx.x;
         if (l < m)
-            en[q] = ent1[(uint64_t)(buf[l] + (int64_t)(P0 + l))];
+            en[q] = ent1[(uint64_t)(buf[dp_sw(l)] + (int64_t)(P0 + l))];
     }
 #pragma unroll
     for (int q = 0; q < kDpSplitPer; q++) {
