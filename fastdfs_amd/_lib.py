@@ -54,6 +54,8 @@ EXPORTS = (
     "fdfs_gpu_crc_combine",
     "fdfs_gpu_dedup_global",
     "fdfs_gpu_dedup_global_local",
+    "fdfs_gpu_crc_batch_global",
+    "fdfs_gpu_crc_batch_global_local",
     "fdfs_gpu_comm_unique_id",
     "fdfs_gpu_comm_init",
     "fdfs_gpu_comm_destroy",
@@ -162,6 +164,10 @@ def load() -> ctypes.CDLL:
     L.fdfs_gpu_dedup_global.argtypes = [vp, vp, vp, vp, u64, vp, vp, vp]
     L.fdfs_gpu_dedup_global_local.restype = i32
     L.fdfs_gpu_dedup_global_local.argtypes = [vp, i32, vp, vp, vp, vp, vp, vp]
+    L.fdfs_gpu_crc_batch_global.restype = i32
+    L.fdfs_gpu_crc_batch_global.argtypes = [vp, vp, ctypes.POINTER(FdfsGpuBatch), vp, vp, vp, u64, vp, vp]
+    L.fdfs_gpu_crc_batch_global_local.restype = i32
+    L.fdfs_gpu_crc_batch_global_local.argtypes = [vp, i32, ctypes.POINTER(FdfsGpuBatch), vp, vp, vp, u64, vp, vp]
     L.fdfs_gpu_comm_unique_id.restype = i32
     L.fdfs_gpu_comm_unique_id.argtypes = [ctypes.c_char_p]
     L.fdfs_gpu_comm_init.restype = i32

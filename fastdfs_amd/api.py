@@ -320,6 +320,54 @@ class Context:
             _stream_handle(stream)), "fdfs_gpu_dedup_global_local")
         return outs
 
+    # ------------------------------------------------- split-file CRC (N GPUs)
+    @staticmethod
+    def _check_pieces(data, offsets, sizes, piece_file, piece_start):
+        n = _check_batch(data, offsets, sizes, True)
+        for t, name in ((piece_file, "piece_file"), (piece_start, "piece_start")):
+            _check_dev(t, name, torch.int64)
+            if t.numel() != n:
+                raise ValueError(f"{name} must have one entry per piece")
+        return n
+
+    def crc_batch_global(self, comm: "Comm", data: torch.Tensor, offsets: torch.Tensor, sizes: torch.Tensor,
+                         piece_file: torch.Tensor, piece_start: torch.Tensor, file_size: torch.Tensor,
+                         stream=None) -> torch.Tensor:
+        """fdfs_gpu_crc_batch_global: this rank holds pieces (bytes
+        data[offsets[i] : + sizes[i]] = file piece_file[i] from byte
+        piece_start[i]); file_size (int64[nfiles], equal on every rank).
+        Returns the CRC32 of every file (int32 bit patterns) on every rank
+        (collective: all ranks call)."""
+        n = self._check_pieces(data, offsets, sizes, piece_file, piece_start)
+        _check_dev(file_size, "file_size", torch.int64)
+        nf = file_size.numel()
+        crc = torch.empty(nf, dtype=torch.int32, device=file_size.device)
+        b = _lib.FdfsGpuBatch(data.data_ptr(), offsets.data_ptr(), sizes.data_ptr(), n)
+        self._rc(self._L.fdfs_gpu_crc_batch_global(self._h, comm.handle, ctypes.byref(b), piece_file.data_ptr(),
+                                                   piece_start.data_ptr(), file_size.data_ptr(), nf,
+                                                   crc.data_ptr(), _stream_handle(stream)),
+                 "fdfs_gpu_crc_batch_global")
+        return crc
+
+    def crc_batch_global_local(self, ranks: list, file_size: torch.Tensor, stream=None) -> torch.Tensor:
+        """fdfs_gpu_crc_batch_global_local: len(ranks) VIRTUAL ranks on this
+        device, ranks[p] = (data, offsets, sizes, piece_file, piece_start) as
+        crc_batch_global takes them.  Returns the files' CRC32s (synchronous)."""
+        nr = len(ranks)
+        if not 1 <= nr <= 64:
+            raise ValueError("1..64 ranks")
+        _check_dev(file_size, "file_size", torch.int64)
+        nf = file_size.numel()
+        B = _lib.FdfsGpuBatch * nr
+        P = ctypes.c_void_p * nr
+        bs = B(*[_lib.FdfsGpuBatch(d.data_ptr(), o.data_ptr(), s.data_ptr(), self._check_pieces(d, o, s, pf, ps))
+                 for d, o, s, pf, ps in ranks])
+        crc = torch.empty(nf, dtype=torch.int32, device=file_size.device)
+        self._rc(self._L.fdfs_gpu_crc_batch_global_local(
+            self._h, nr, bs, P(*[r[3].data_ptr() for r in ranks]), P(*[r[4].data_ptr() for r in ranks]),
+            file_size.data_ptr(), nf, crc.data_ptr(), _stream_handle(stream)), "fdfs_gpu_crc_batch_global_local")
+        return crc
+
     def dedup_bucket(self, sig: torch.Tensor, gidx: torch.Tensor | None, nranks: int, stream=None):
         """Pack {sig, gidx} rows by owner rank: (rows uint8[n,32], counts int64[nranks], row_of int64[n])."""
         n = _check_sig(sig, gidx)

@@ -1634,6 +1634,177 @@ int fdfs_gpu_dedup_global_local(fdfs_gpu_ctx *ctx, int nranks, const uint8_t *co
     return rc;
 }
 
+// ---- split-file CRC over N GPUs -------------------------------
+
+extern "C++" {
+
+static int cg_check(const fdfs_gpu_batch *pieces, const uint64_t *pfile, const uint64_t *pstart,
+                    const uint64_t *fsize, uint64_t nfiles, const uint32_t *crc_out)
+{
+    if (!pieces)
+        return EINVAL;
+    if (pieces->n && (!pieces->base || !pieces->offset || !pieces->size || !pfile || !pstart))
+        return EINVAL;
+    if (nfiles && (!fsize || !crc_out))
+        return EINVAL;
+    return 0;
+}
+
+// The segmented pass over one rank's pieces (their CRC32_ex from XINIT) and
+// the pieces' terms in that rank's block of `blk` (zeroed first).
+static size_t cg_ws_bytes(uint64_t np) { return align_up(4 * np) + sig_ws_bytes(np); }
+
+static hipError_t cg_pieces(fdfs_gpu_ctx *ctx, const fdfs_gpu_batch *pieces, const uint64_t *pfile,
+                            const uint64_t *pstart, const uint64_t *fsize, uint64_t nfiles, const fdfs::CrcParts &blk,
+                            uint32_t r, hipStream_t st)
+{
+    fdfs::CrcParts mine = blk;
+    mine.base = blk.base + r * blk.stride;
+    hipError_t e = fdfs::launch_zero_u32(mine.base, fdfs::CrcParts::block_bytes(nfiles) / 4, st);
+    const uint32_t np = pieces->n;
+    if (e != hipSuccess || !np)
+        return e;
+    Carve cv{static_cast<char *>(ctx->ws)};
+    uint32_t *crc = cv.take<uint32_t>(np);
+    uint64_t *nseg = cv.take<uint64_t>(np);
+    uint64_t *first = cv.take<uint64_t>((size_t)np + 1);
+    uint64_t *bsum = cv.take<uint64_t>(fdfs::scan_workspace_elems(np));
+    hipEvent_t a, b;
+    timing_pair(ctx, FDFS_KERNEL_CRC_SEG, a, b);
+    e = fdfs::launch_crc_seg(ctx->sar, static_cast<const uint8_t *>(pieces->base), pieces->offset, pieces->size, np,
+                             nseg, first, bsum, ctx->d_tabs, crc, ctx->seg_grid, st, a, b);
+    if (e == hipSuccess)
+        e = fdfs::launch_crc_pieces(crc, pfile, pstart, pieces->size, np, fsize, nfiles, mine, ctx->d_tabs, st);
+    return e;
+}
+
+// The fold of every rank's block into crc_out, then the error words to the
+// host (the call's last synchronisation): 0, or EINVAL with the reason.
+static int cg_fold(fdfs_gpu_ctx *ctx, const fdfs::CrcParts &blk, int nranks, const uint64_t *fsize, uint64_t nfiles,
+                   uint32_t *crc_out, hipStream_t st, const char *who)
+{
+    uint64_t *derr = ctx->dann + kAnnMax + 64 * kAnnMax + 4;
+    uint64_t *herr = ctx->hann + 64 * kAnnTail + 64 * kAnnMax + 4;
+    hipError_t e = fdfs::launch_zero_u32(derr, 4, st);
+    if (e == hipSuccess)
+        e = fdfs::launch_crc_fold(blk, (uint32_t)nranks, fsize, nfiles, crc_out, derr, ctx->d_tabs, st);
+    if (e == hipSuccess)
+        e = hipMemcpyAsync(herr, derr, 16, hipMemcpyDeviceToHost, st);
+    if (e == hipSuccess)
+        e = hipStreamSynchronize(st);
+    if (e != hipSuccess)
+        return fail(ctx, e, who);
+    if (herr[0] || herr[1]) {
+        std::snprintf(ctx->err, sizeof(ctx->err),
+                      "%s: pieces outside their files on rank mask 0x%llx; %llu files not covered exactly by "
+                      "their pieces (crc_out invalid)",
+                      who, (unsigned long long)herr[0], (unsigned long long)herr[1]);
+        return EINVAL;
+    }
+    return 0;
+}
+
+}  // extern "C++"
+
+int fdfs_gpu_crc_batch_global(fdfs_gpu_ctx *ctx, void *comm, const fdfs_gpu_batch *pieces, const uint64_t *piece_file,
+                              const uint64_t *piece_start, const uint64_t *file_size, uint64_t nfiles,
+                              uint32_t *crc_out, void *stream)
+{
+    if (!ctx || !comm)
+        return EINVAL;
+    ncclComm_t c = static_cast<ncclComm_t>(comm);
+    int nranks = 0, me = 0;
+    if (ncclCommCount(c, &nranks) != ncclSuccess || ncclCommUserRank(c, &me) != ncclSuccess ||
+        nranks < 1 || nranks > 64)
+        return EINVAL;
+    std::lock_guard<std::recursive_mutex> lk(ctx->mu);
+    DeviceGuard g(ctx->device);
+    if (!g.ok)
+        return ENODEV;
+    hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+    // as in dedup_global, a local error is announced, not returned, so that
+    // no rank waits alone in a collective
+    int err = capturing(st) ? EINVAL : cg_check(pieces, piece_file, piece_start, file_size, nfiles, crc_out);
+    const uint64_t bb = fdfs::CrcParts::block_bytes(nfiles);
+    if (!err)
+        err = ensure_buf(ctx, &ctx->xa, &ctx->xa_bytes, bb * nranks, st);
+    if (!err)
+        err = ensure_ws(ctx, cg_ws_bytes(pieces->n), st);
+    WsScope wsc(ctx, st);
+    uint64_t *ann = ctx->dann, *all = ctx->dann + kAnnMax;
+    uint64_t *htail = ctx->hann, *hall = ctx->hann + 64 * kAnnTail;
+    htail[0] = nfiles;
+    htail[1] = (uint64_t)err;
+    // 1. announcement {nfiles, errno} of every rank: the sizes of the
+    //    exchange agree, or every rank returns the first rank's error
+    hipError_t e = hipMemcpyAsync(ann, htail, 16, hipMemcpyHostToDevice, st);
+    if (e != hipSuccess)
+        return fail(ctx, e, "crc_batch_global announce");
+    ncclResult_t r = ncclAllGather(ann, all, 2, ncclUint64, c, st);
+    if (r != ncclSuccess)
+        return nccl_fail(ctx, r, "ncclAllGather announcements");
+    if ((e = hipMemcpyAsync(hall, all, 16ull * nranks, hipMemcpyDeviceToHost, st)) != hipSuccess ||
+        (e = hipStreamSynchronize(st)) != hipSuccess)
+        return fail(ctx, e, "crc_batch_global announcements");
+    for (int p = 0; p < nranks; p++) {
+        if (hall[2 * p + 1] || hall[2 * p] != nfiles) {
+            const int perr = hall[2 * p + 1] ? (int)hall[2 * p + 1] : EINVAL;
+            std::snprintf(ctx->err, sizeof(ctx->err), "crc_batch_global: rank %d %s", p,
+                          hall[2 * p + 1] ? (perr == ENOMEM ? "is out of memory" : "has invalid arguments")
+                                          : "passed a different file count");
+            return perr;
+        }
+    }
+    // 2. this rank's pieces into its block of the all-gather buffer,
+    // 3. the blocks to every rank (in place), 4. the fold
+    const fdfs::CrcParts blk{static_cast<char *>(ctx->xa), nfiles, bb};
+    if ((e = cg_pieces(ctx, pieces, piece_file, piece_start, file_size, nfiles, blk, (uint32_t)me, st)) != hipSuccess)
+        return fail(ctx, e, "crc_batch_global pieces");
+    if ((r = ncclAllGather(blk.base + me * bb, blk.base, bb, ncclUint8, c, st)) != ncclSuccess)
+        return nccl_fail(ctx, r, "ncclAllGather crc blocks");
+    return cg_fold(ctx, blk, nranks, file_size, nfiles, crc_out, st, "crc_batch_global");
+}
+
+int fdfs_gpu_crc_batch_global_local(fdfs_gpu_ctx *ctx, int nranks, const fdfs_gpu_batch *pieces,
+                                    const uint64_t *const *piece_file, const uint64_t *const *piece_start,
+                                    const uint64_t *file_size, uint64_t nfiles, uint32_t *crc_out, void *stream)
+{
+    if (!ctx || nranks < 1 || nranks > 64 || !pieces || !piece_file || !piece_start)
+        return EINVAL;
+    uint32_t maxp = 0;
+    for (int p = 0; p < nranks; p++) {
+        if (cg_check(&pieces[p], piece_file[p], piece_start[p], file_size, nfiles, crc_out))
+            return EINVAL;
+        maxp = std::max(maxp, pieces[p].n);
+    }
+    std::lock_guard<std::recursive_mutex> lk(ctx->mu);
+    DeviceGuard g(ctx->device);
+    if (!g.ok)
+        return ENODEV;
+    hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+    if (capturing(st)) {
+        std::snprintf(ctx->err, sizeof(ctx->err), "crc_batch_global_local synchronises; not capturable");
+        return EINVAL;
+    }
+    const uint64_t bb = fdfs::CrcParts::block_bytes(nfiles);
+    int rc = ensure_buf(ctx, &ctx->xa, &ctx->xa_bytes, bb * nranks, st);
+    if (!rc)
+        rc = ensure_ws(ctx, cg_ws_bytes(maxp), st);
+    if (rc)
+        return rc;
+    WsScope wsc(ctx, st);
+    // every virtual rank's block where the all-gather would put it (the
+    // ranks' segmented passes share the workspace, stream-ordered)
+    const fdfs::CrcParts blk{static_cast<char *>(ctx->xa), nfiles, bb};
+    for (int p = 0; p < nranks; p++) {
+        const hipError_t e =
+            cg_pieces(ctx, &pieces[p], piece_file[p], piece_start[p], file_size, nfiles, blk, (uint32_t)p, st);
+        if (e != hipSuccess)
+            return fail(ctx, e, "crc_batch_global_local pieces");
+    }
+    return cg_fold(ctx, blk, nranks, file_size, nfiles, crc_out, st, "crc_batch_global_local");
+}
+
 // ---- formats that consume the CRC, FastDHT routing, scrub ----
 
 int fdfs_gpu_file_ids(fdfs_gpu_ctx *ctx, uint32_t server_id, const uint32_t *crc32,

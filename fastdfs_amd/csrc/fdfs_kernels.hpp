@@ -88,6 +88,36 @@ hipError_t launch_final(int method, const fdfs_gpu_file_state *states, const uin
                         hipStream_t st);
 hipError_t launch_crc_combine(const uint32_t *a, const uint32_t *b, const uint64_t *len_b, uint32_t n,
                               uint32_t *out, const DevTables *tabs, hipStream_t st);
+// Split-file CRC: one rank's block of per-file words is {CRC term u32 x
+// nfiles, error word, length sum u64 x nfiles}; `base` is rank 0's block and
+// rank r's starts `stride` bytes further per rank (the all-gather's layout).
+struct CrcParts {
+    char *base;
+    uint64_t nfiles, stride;
+    static uint64_t err_off(uint64_t nfiles) { return (4 * nfiles + 7) & ~7ull; }
+    static uint64_t block_bytes(uint64_t nfiles) { return err_off(nfiles) + 8 + 8 * nfiles; }
+    __host__ __device__ uint32_t *word(uint32_t r, uint64_t f) const
+    {
+        return reinterpret_cast<uint32_t *>(base + r * stride) + f;
+    }
+    __host__ __device__ uint32_t *err(uint32_t r) const
+    {
+        return reinterpret_cast<uint32_t *>(base + r * stride + ((4 * nfiles + 7) & ~7ull));
+    }
+    __host__ __device__ uint64_t *len(uint32_t r, uint64_t f) const
+    {
+        return reinterpret_cast<uint64_t *>(base + r * stride + ((4 * nfiles + 7) & ~7ull) + 8) + f;
+    }
+};
+// Each piece's term XORed into its rank's block (launch_crc_pieces), then
+// the fold of nranks blocks into the files' CRCs, the mask of ranks that
+// reported an error (err_out[0]) and the count of files whose pieces do not
+// add up to their size (err_out[1], zeroed by the caller).
+hipError_t launch_crc_pieces(const uint32_t *crc, const uint64_t *pfile, const uint64_t *pstart, const uint64_t *plen,
+                             uint32_t np, const uint64_t *fsize, uint64_t nfiles, const CrcParts &blk,
+                             const DevTables *tabs, hipStream_t st);
+hipError_t launch_crc_fold(const CrcParts &blk, uint32_t nranks, const uint64_t *fsize, uint64_t nfiles,
+                           uint32_t *crc_out, uint64_t *err_out, const DevTables *tabs, hipStream_t st);
 // Duplicate state indices of an update batch: *flag = 1 duplicate, 2 the
 // reserved value ~0 (table: sidx_table_size(n) u32 of scratch).
 uint32_t sidx_table_size(uint32_t n);

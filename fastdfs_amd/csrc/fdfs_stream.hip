@@ -179,6 +179,88 @@ hipError_t launch_crc_carry(const uint32_t *crc, const uint64_t *sizes, uint32_t
     return hipGetLastError();
 }
 
+// Split-file CRC (fdfs_gpu_crc_batch_global).  Piece i holds bytes
+// [start, start + len) of file f, and crc[i] = CRC32_FINAL(CRC32_ex(piece,
+// XINIT)) from crc_seg_kernel.  Over GF(2) the file's register is
+//   CRC32_ex(file, XINIT) = M^size XINIT ^ XOR_i M^(size - start_i - len_i) CRC32_ex(piece_i, 0)
+// whenever the pieces tile the file, in any order and on any rank, and
+// CRC32_ex(piece, 0) = ~crc[i] ^ M^len XINIT.  A rank's block (CrcParts)
+// holds per file the XOR of its pieces' terms and the sum of their lengths,
+// and an error word (bit 0: a piece names a file >= nfiles or runs past its
+// file's end; such a piece is dropped).
+__global__ void crc_piece_kernel(const uint32_t *__restrict__ crc, const uint64_t *__restrict__ pfile,
+                                 const uint64_t *__restrict__ pstart, const uint64_t *__restrict__ plen,
+                                 uint32_t np, const uint64_t *__restrict__ fsize, uint64_t nfiles,
+                                 CrcParts blk, const DevTables *__restrict__ tabs)
+{
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= np)
+        return;
+    const uint64_t f = pfile[i], a = pstart[i], len = plen[i];
+    if (f >= nfiles) {
+        atomicOr(blk.err(0), 1u);
+        return;
+    }
+    const uint64_t size = fsize[f];
+    if (a > size || len > size - a) {
+        atomicOr(blk.err(0), 1u);
+        return;
+    }
+    const uint32_t c0 = ~crc[i] ^ advance_bytes(tabs->t, 0xFFFFFFFFu, len);
+    atomicXor(blk.word(0, f), advance_bytes(tabs->t, c0, size - a - len));
+    atomicAdd(reinterpret_cast<unsigned long long *>(blk.len(0, f)), (unsigned long long)len);
+}
+
+// The fold over the ranks' blocks: crc_out[f] = CRC32_FINAL(M^size XINIT ^
+// XOR_r term_r[f]); err_out[0] = the mask of ranks whose error word is set,
+// err_out[1] = the files whose pieces' lengths do not add up to their size
+// (zeroed by the caller).
+__global__ void crc_fold_kernel(CrcParts blk, uint32_t nranks, const uint64_t *__restrict__ fsize, uint64_t nfiles,
+                                uint32_t *__restrict__ crc_out, uint64_t *__restrict__ err_out,
+                                const DevTables *__restrict__ tabs)
+{
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+        uint64_t m = 0;
+        for (uint32_t r = 0; r < nranks; r++)
+            if (*blk.err(r))
+                m |= 1ull << r;
+        err_out[0] = m;
+    }
+    uint32_t bad = 0;
+    for (uint64_t f = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; f < nfiles;
+         f += (uint64_t)gridDim.x * blockDim.x) {
+        const uint64_t size = fsize[f];
+        uint32_t x = advance_bytes(tabs->t, 0xFFFFFFFFu, size);
+        uint64_t covered = 0;
+        for (uint32_t r = 0; r < nranks; r++) {
+            x ^= *blk.word(r, f);
+            covered += *blk.len(r, f);
+        }
+        crc_out[f] = ~x;
+        bad += covered != size;
+    }
+    if (bad)
+        atomicAdd(reinterpret_cast<unsigned long long *>(err_out + 1), (unsigned long long)bad);
+}
+
+hipError_t launch_crc_pieces(const uint32_t *crc, const uint64_t *pfile, const uint64_t *pstart, const uint64_t *plen,
+                             uint32_t np, const uint64_t *fsize, uint64_t nfiles, const CrcParts &blk,
+                             const DevTables *tabs, hipStream_t st)
+{
+    if (np)
+        crc_piece_kernel<<<blocks(np), 256, 0, st>>>(crc, pfile, pstart, plen, np, fsize, nfiles, blk, tabs);
+    return hipGetLastError();
+}
+
+hipError_t launch_crc_fold(const CrcParts &blk, uint32_t nranks, const uint64_t *fsize, uint64_t nfiles,
+                           uint32_t *crc_out, uint64_t *err_out, const DevTables *tabs, hipStream_t st)
+{
+    const uint64_t g = (nfiles + 255) / 256;
+    crc_fold_kernel<<<(unsigned)(g < 1 ? 1 : g > 16384 ? 16384 : g), 256, 0, st>>>(blk, nranks, fsize, nfiles, crc_out,
+                                                                                err_out, tabs);
+    return hipGetLastError();
+}
+
 hipError_t launch_final(int method, const fdfs_gpu_file_state *states, const uint32_t *sidx, uint32_t n,
                         uint32_t *crc_out, uint8_t *sig_out, int32_t *codes_out, hipStream_t st)
 {

@@ -58,7 +58,7 @@ def plan_crc_pieces(sizes, nranks: int) -> list[list[tuple[int, int, int]]]:
     return plan
 
 
-def crc_batch_global(kernels, sizes, plan, data: torch.Tensor, offsets: torch.Tensor, group=None):
+def crc_batch_global(kernels, sizes, plan, data: torch.Tensor, offsets: torch.Tensor, group=None, comm=None):
     """CRC32 of files whose bytes are spread over the ranks as `plan`
     (plan_crc_pieces) says: this rank holds its pieces in `data` at
     `offsets` (int64, one per piece of plan[rank], in plan order).
@@ -69,7 +69,21 @@ def crc_batch_global(kernels, sizes, plan, data: torch.Tensor, offsets: torch.Te
     acc = M^|piece| acc ^ part (fdfs_gpu_crc_combine), from CRC32_XINIT; the
     file CRC is CRC32_FINAL(acc).  Returns uint32 CRCs (int32 bit patterns)
     of all files on every rank.  kernels: a fastdfs_amd.Context (tests
-    substitute a CPU double)."""
+    substitute a CPU double).
+
+    comm: a fastdfs_amd.api.Comm -> the whole step runs inside libfdfs_gpu
+    (fdfs_gpu_crc_batch_global: each piece's term advanced to its file's
+    end, one ncclAllGather of 12 bytes per file, the fold on the device),
+    the C recovery caller's path; this function then only builds the piece
+    arrays from the plan."""
+    if comm is not None:
+        dev = data.device
+        mine = plan[comm.rank]
+        pf = torch.tensor([p[0] for p in mine], dtype=torch.int64, device=dev)
+        ps = torch.tensor([p[1] for p in mine], dtype=torch.int64, device=dev)
+        lens = torch.tensor([p[2] for p in mine], dtype=torch.int64, device=dev)
+        fs = torch.from_numpy(np.asarray(sizes, dtype=np.int64)).to(dev)
+        return kernels.crc_batch_global(comm, data, offsets, lens, pf, ps, fs)
     rank, world = dist.get_rank(group), dist.get_world_size(group)
     dev = data.device
     sizes = np.asarray(sizes, dtype=np.int64)

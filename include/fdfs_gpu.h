@@ -285,6 +285,44 @@ int fdfs_gpu_dedup_global_local(fdfs_gpu_ctx *ctx, int nranks, const uint8_t *co
                                 const uint64_t *const *gidx, const uint64_t *n, uint64_t *const *rep_out,
                                 uint32_t *const *ref_out, void *stream);
 
+/* Split-file CRC32 over N GPUs: the bytes of `nfiles` files
+ * are spread over the ranks in pieces, cut anywhere (e.g. the files'
+ * concatenated byte stream in equal shares, fastdfs_amd/dist.py
+ * plan_crc_pieces: a recovery or scrub pass over a few huge files keeps
+ * every GPU busy).  Each rank passes the pieces it holds as a batch (piece
+ * i = bytes [base + offset[i], + size[i]) on this rank's device) with
+ * piece_file[i] (the file it belongs to) and piece_start[i] (its first
+ * byte's position in that file), device uint64 arrays of pieces->n entries;
+ * file_size: device uint64[nfiles], the same on every rank.  Every rank gets
+ * crc_out (device uint32[nfiles]) = the CRC32 (%u value) of every file.
+ * Inside: CRC32_ex of every piece from CRC32_XINIT (the segmented kernel),
+ * each piece's CRC32_ex(piece, 0) advanced to the end of its file by a
+ * GF(2) power of the zero-byte step and XORed into a per-file word, one
+ * ncclAllGather of those words (12 bytes per file per rank), and the fold
+ * M^size CRC32_XINIT ^ (the ranks' words), then CRC32_FINAL -- CRC32_ex is
+ * linear over GF(2), so pieces may come in any order from any rank (the
+ * reference's CRC32_ex(.., init) chaining, storage/storage_dio.c:467,
+ * client/fdfs_crc32.c:67-99, computed for the pieces apart).  The pieces of
+ * all ranks must tile each file exactly: a piece outside its file, or a file
+ * whose pieces' lengths do not add up to its size, makes every rank return
+ * EINVAL (crc_out invalid).  An argument error or allocation failure on ANY
+ * rank is returned by every rank (first, an all-gather of {nfiles, errno},
+ * one host synchronisation).  Synchronous: returns after crc_out is written
+ * (a second synchronisation reads the ranks' error words); not capturable.
+ * EIO (a failed launch or RCCL call) leaves the communicator unusable. */
+int fdfs_gpu_crc_batch_global(fdfs_gpu_ctx *ctx, void *comm, const fdfs_gpu_batch *pieces,
+                              const uint64_t *piece_file, const uint64_t *piece_start,
+                              const uint64_t *file_size, uint64_t nfiles, uint32_t *crc_out, void *stream);
+
+/* fdfs_gpu_crc_batch_global for `nranks` VIRTUAL ranks in this process, all
+ * on this context's device: pieces[p], piece_file[p], piece_start[p] are
+ * virtual rank p's (host arrays of nranks entries, device data), crc_out the
+ * one result.  The same per-rank blocks and fold as the RCCL form, each
+ * block written where the all-gather would put it. */
+int fdfs_gpu_crc_batch_global_local(fdfs_gpu_ctx *ctx, int nranks, const fdfs_gpu_batch *pieces,
+                                    const uint64_t *const *piece_file, const uint64_t *const *piece_start,
+                                    const uint64_t *file_size, uint64_t nfiles, uint32_t *crc_out, void *stream);
+
 /* Convenience RCCL communicator setup for callers without one: rank 0 gets
  * a 128-byte id (ncclGetUniqueId) and sends it to the others by any means;
  * every rank then calls fdfs_gpu_comm_init (ncclCommInitRank on ctx's

@@ -274,14 +274,101 @@ def test_crc_batch_global_one_rank(oracle, ctxs):
     s.close()
     dist.init_process_group("nccl", init_method=f"tcp://127.0.0.1:{port}", rank=0, world_size=1,
                             device_id=torch.device("cuda", 0))
+    from fastdfs_amd.api import Comm
     try:
         for v in (0, 1):
-            crc = crc_batch_global(ctxs[v], sizes, plan, torch.from_numpy(buf).cuda(),
-                                   torch.tensor(offs, dtype=torch.int64, device="cuda"))
-            got = crc.cpu().numpy().view(np.uint32)
-            assert [int(x) for x in got] == [oracle.crc32(f, v) for f in files], v
+            want = [oracle.crc32(f, v) for f in files]
+            comm = Comm(ctxs[v])
+            try:
+                # torch.distributed steps, then the same plan through
+                # fdfs_gpu_crc_batch_global on libfdfs_gpu's communicator
+                for c in (None, comm):
+                    crc = crc_batch_global(ctxs[v], sizes, plan, torch.from_numpy(buf).cuda(),
+                                           torch.tensor(offs, dtype=torch.int64, device="cuda"), comm=c)
+                    got = crc.cpu().numpy().view(np.uint32)
+                    assert [int(x) for x in got] == want, (v, c is None)
+            finally:
+                comm.close()
     finally:
         dist.destroy_process_group()
+
+
+def _rank_pieces(files, pieces, rng, dev="cuda"):
+    """One rank's share as crc_batch_global takes it: its pieces' bytes
+    packed at random gaps (any alignment) in one device buffer."""
+    offs, pos, chunks = [], 0, []
+    for f, a, ln in pieces:
+        pos += int(rng.integers(0, 9))
+        offs.append(pos)
+        chunks.append((pos, files[f][a:a + ln]))
+        pos += ln
+    buf = np.zeros(pos + 1, np.uint8)
+    for p0, b in chunks:
+        buf[p0:p0 + len(b)] = b
+    t = lambda x: torch.tensor(x, dtype=torch.int64, device=dev)  # noqa: E731
+    return (torch.from_numpy(buf).to(dev), t(offs), t([p[2] for p in pieces]), t([p[0] for p in pieces]),
+            t([p[1] for p in pieces]))
+
+
+@pytest.mark.parametrize("world", [2, 3, 8])
+def test_crc_batch_global_ranks(oracle, ctxs, world):
+    """fdfs_gpu_crc_batch_global's blocks and fold at world 2, 3 and 8
+    (virtual ranks on this GPU, each block where the all-gather puts it):
+    (a) plan_crc_pieces' equal byte shares of 300 files incl. two of 48 MiB
+    that span several ranks, (b) every file cut at random points into pieces
+    dealt to random ranks in random order.  Both variants equal the oracle's
+    CRC32 of every file."""
+    from fastdfs_amd.dist import plan_crc_pieces
+
+    rng = np.random.default_rng(700 + world)
+    sizes = np.concatenate([[0, 1, 48 << 20], rng.integers(0, 400_000, 296), [(48 << 20) + 5]]).astype(np.int64)
+    files = _files(rng, sizes)
+    offs = np.zeros(sizes.size, np.uint64)
+    offs[1:] = np.cumsum(sizes)[:-1]
+    allb = np.concatenate(files)
+    fs = torch.from_numpy(sizes).cuda()
+    rnd: list[list[tuple[int, int, int]]] = [[] for _ in range(world)]
+    for f, n in enumerate(sizes.tolist()):
+        k = int(rng.integers(1, 6))
+        edges = np.unique(np.concatenate([[0, n], rng.integers(0, n + 1, k)])) if n else np.array([0, 0])
+        for a, b in zip(edges[:-1], edges[1:]):
+            rnd[int(rng.integers(0, world))].append((f, int(a), int(b - a)))
+    for pcs in rnd:
+        rng.shuffle(pcs)
+    for v in (0, 1):
+        want, _ = oracle.dio_batch(allb, offs, sizes.astype(np.uint64), 0, v, nthreads=8)
+        for plan in (plan_crc_pieces(sizes, world), rnd):
+            ranks = [_rank_pieces(files, plan[r], rng) for r in range(world)]
+            crc = ctxs[v].crc_batch_global_local(ranks, fs)
+            assert np.array_equal(crc.cpu().numpy().view(np.uint32), want), (world, v, plan is rnd)
+
+
+def test_crc_batch_global_rejects_bad_tilings(ctxs):
+    """Pieces that do not tile their files make the call fail (EINVAL), not
+    return a wrong CRC: a piece past its file's end, a file index past
+    nfiles, a gap, an overlap."""
+    import fastdfs_amd as F
+    rng = np.random.default_rng(77)
+    sizes = np.array([1000, 5000, 0], np.int64)
+    files = _files(rng, sizes)
+    fs = torch.from_numpy(sizes).cuda()
+    good = [[(0, 0, 600), (1, 0, 5000)], [(0, 600, 400)]]
+    crc = ctxs[0].crc_batch_global_local([_rank_pieces(files, p, rng) for p in good], fs)
+    assert crc.numel() == 3
+    bad = {"past end": [[(0, 0, 600), (1, 0, 5000)], [(0, 600, 401)]],
+           "file index": [[(0, 0, 600), (1, 0, 5000)], [(0, 600, 400), (3, 0, 0)]],
+           "gap": [[(0, 0, 600), (1, 0, 5000)], [(0, 601, 399)]],
+           "overlap": [[(0, 0, 600), (1, 0, 5000)], [(0, 500, 500)]]}
+    for name, plan in bad.items():
+        pieces = [[(f, a, n) for f, a, n in p if f < 3] for p in plan]
+        ranks = [_rank_pieces(files, pieces[r], rng) for r in range(2)]
+        if name == "file index":  # a piece naming file 3 of 3
+            d, o, s, pf, ps = ranks[1]
+            ranks[1] = (d, torch.cat([o, o[:1]]), torch.cat([s, torch.zeros_like(s[:1])]),
+                        torch.cat([pf, torch.full_like(pf[:1], 3)]), torch.cat([ps, torch.zeros_like(ps[:1])]))
+        with pytest.raises(F.FdfsGpuError) as ei:
+            ctxs[0].crc_batch_global_local(ranks, fs)
+        assert ei.value.errno == 22, name
 
 
 def test_two_streams_one_context(oracle):
