@@ -23,11 +23,12 @@ step bench_c4 600 python3 bench.py --config c4 || exit $?
 step bench_c5 600 python3 bench.py --config c5 --steps 5 --warmup 1 || exit $?
 step bench_c1 900 python3 bench.py --config c1 --steps 3 --warmup 1 || exit $?
 for c in c1 c2 c3 c4 c5; do tail -1 $O/bench_$c.log | cut -c1-300; done
-step stats_c2 600 rocprofv3 --kernel-trace --stats -d $O/stats_c2 -o run --output-format csv -- $B $S || exit $?
+step stats_c2 600 rocprofv3 --kernel-trace --stats -d $O/stats_c2 -o run --output-format csv -- $B --steps 10 --warmup 3 || exit $?
 step stats_c3 600 rocprofv3 --kernel-trace --stats -d $O/stats_c3 -o run --output-format csv -- $B --config c3 --steps 2 --warmup 1 || exit $?
 step stats_c4 600 rocprofv3 --kernel-trace --stats -d $O/stats_c4 -o run --output-format csv -- $B --config c4 $S || exit $?
 step stats_c5 600 rocprofv3 --kernel-trace --stats -d $O/stats_c5 -o run --output-format csv -- $B --config c5 $S || exit $?
 step stats_c1 900 rocprofv3 --kernel-trace --stats -d $O/stats_c1 -o run --output-format csv -- $B --config c1 --steps 2 --warmup 1 || exit $?
+find $O -name "*kernel_trace.csv" -size +8M -delete  # keep the small traces (steady-state means)
 fi
 if [ "${PART:-all}" != 1 ]; then  # PART=2: PMC passes and probes
 for c in c2 c3 c4 c5; do

@@ -25,6 +25,24 @@ def short(name):
     return name.split("(")[0].replace("void ", "").replace("fdfs::", "")
 
 
+def steady(trace, out_path):
+    """Per fdfs kernel from a kernel trace: dispatches, mean over all, mean
+    without the first dispatch (cold: first touch of the batch's pages, the
+    tables' upload), min and max, in ms."""
+    per = {}
+    for r in csv.DictReader(open(trace)):
+        name = r.get("Kernel_Name") or r.get("Name") or ""
+        if "fdfs::" not in name:
+            continue
+        t = (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e6
+        per.setdefault(short(name), []).append(t)
+    with open(out_path, "w") as out:
+        out.write("# kernel dispatches mean_ms mean_without_first_ms min_ms max_ms (rocprofv3 --kernel-trace)\n")
+        for k, v in sorted(per.items(), key=lambda kv: -sum(kv[1])):
+            rest = v[1:] if len(v) > 1 else v
+            out.write(f"{k} {len(v)} {sum(v) / len(v):.4f} {sum(rest) / len(rest):.4f} {min(v):.4f} {max(v):.4f}\n")
+
+
 def main(src, dst):
     os.makedirs(dst, exist_ok=True)
     for c in ("c1", "c2", "c3", "c4", "c5"):
@@ -43,6 +61,8 @@ def main(src, dst):
                     if "fdfs::" in r["Name"] or "rocclr" in r["Name"]:
                         r["Name"] = short(r["Name"])
                         w.writerow(r)
+        for f in glob.glob(os.path.join(src, f"stats_{c}", "**", "*kernel_trace.csv"), recursive=True):
+            steady(f, os.path.join(dst, f"kernel_steady_{c}.txt"))
         if c == "c5":  # the dedup group is five kernels: traffic summed over them
             tot = {}
             for kind in ("fetch", "write"):
