@@ -60,6 +60,9 @@ def parse():
                    help="CPU baseline threads (0 = every core this process may run on)")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--unsigned-hash", action="store_true")
+    p.add_argument("--answers", default="arrays", choices=["arrays", "packed"],
+                   help="one-GPU dedup output: rep/ref arrays (fdfs_gpu_dedup) or packed 16-byte "
+                        "records (fdfs_gpu_dedup_packed)")
     p.add_argument("--exchange", default="rccl", choices=["rccl", "torch"],
                    help="N>1 dedup exchange: libfdfs_gpu's fdfs_gpu_dedup_global over its own RCCL "
                         "communicator, or the same steps over torch.distributed")
@@ -115,6 +118,7 @@ def timed(fn, steps, warmup, world):
 
 
 COMM = None  # fastdfs_amd.api.Comm of the run (N > 1, --exchange rccl)
+PACKED = False  # --answers packed
 
 
 def dedup_step(ctx, sig, gidx, world, stats=None):
@@ -122,7 +126,7 @@ def dedup_step(ctx, sig, gidx, world, stats=None):
         return dedup_global(ctx, sig, gidx, stats=stats, comm=COMM)
     # one GPU holds the whole ingest in order: the ingest index is the
     # position (gidx NULL in fdfs_gpu_dedup, the same answers as arange)
-    return ctx.dedup(sig)
+    return ctx.dedup_packed(sig) if PACKED else ctx.dedup(sig)
 
 
 def cgroup_cpus() -> float | None:
@@ -381,7 +385,8 @@ def main():
     world, rank, local = setup_dist(args)
     dev = torch.device("cuda", local)
     ctx = F.Context(local, unsigned_hash=args.unsigned_hash)
-    global COMM
+    global COMM, PACKED
+    PACKED = args.answers == "packed"
     rccl_check = None
     if world > 1 and args.exchange == "rccl":
         COMM, rccl_check = rccl_exchange_check(ctx, world, rank, dev)
@@ -516,7 +521,10 @@ def main():
                     "scaling": "strong",
                     "config": {"workload": "config 5: 100M-file dedup, 10% duplicates, "
                                            "bucket + RCCL all-to-all + hash grouping",
-                               "records_total": total, "parallelism": f"dp{world}"}})
+                               "records_total": total, "parallelism": f"dp{world}",
+                               "answers": ("fdfs_gpu_dedup_packed (16-byte {rep, ref} records)" if PACKED
+                                           else "fdfs_gpu_dedup (rep u64[n] + ref u32[n])") if world == 1
+                               else "fdfs_gpu_dedup_global (rep u64[n] + ref u32[n])"}})
         if world > 1:  # all ranks' bytes to peers per step, over the step time
             res["xgmi"] = {"bytes_per_step": round(peer), "gbs": round(peer / (dt / args.steps) / 1e9, 1),
                            "links_peak_gbs": 7 * 153.0 * world}

@@ -52,6 +52,7 @@ EXPORTS = (
     "fdfs_gpu_update_batch",
     "fdfs_gpu_final_batch",
     "fdfs_gpu_crc_combine",
+    "fdfs_gpu_dedup_packed",
     "fdfs_gpu_dedup_global",
     "fdfs_gpu_dedup_global_local",
     "fdfs_gpu_crc_batch_global",
@@ -160,6 +161,8 @@ def load() -> ctypes.CDLL:
     L.fdfs_gpu_final_batch.argtypes = [vp, vp, vp, u32, i32, vp, vp, vp, vp]
     L.fdfs_gpu_crc_combine.restype = i32
     L.fdfs_gpu_crc_combine.argtypes = [vp, vp, vp, vp, u32, vp, vp]
+    L.fdfs_gpu_dedup_packed.restype = i32
+    L.fdfs_gpu_dedup_packed.argtypes = [vp, vp, vp, u64, vp, vp]
     L.fdfs_gpu_dedup_global.restype = i32
     L.fdfs_gpu_dedup_global.argtypes = [vp, vp, vp, vp, u64, vp, vp, vp]
     L.fdfs_gpu_dedup_global_local.restype = i32

@@ -281,6 +281,16 @@ class Context:
                                         ref.data_ptr(), _stream_handle(stream)), "fdfs_gpu_dedup")
         return rep, ref
 
+    def dedup_packed(self, sig: torch.Tensor, gidx: torch.Tensor | None = None, stream=None):
+        """fdfs_gpu_dedup_packed: int64[n, 2] with [:, 0] = rep and [:, 1] =
+        ref (the 16-byte fdfs_gpu_dedup_answer records; ref's reserved high
+        word is 0)."""
+        n = _check_sig(sig, gidx)
+        out = torch.empty((n, 2), dtype=torch.int64, device=sig.device)
+        self._rc(self._L.fdfs_gpu_dedup_packed(self._h, sig.data_ptr(), _ptr(gidx), n, out.data_ptr(),
+                                               _stream_handle(stream)), "fdfs_gpu_dedup_packed")
+        return out
+
     def dedup_global(self, comm: "Comm", sig: torch.Tensor, gidx: torch.Tensor | None, stream=None):
         """fdfs_gpu_dedup_global: this rank's share of a multi-GPU ingest
         grouped across every rank of `comm` over RCCL; (rep int64[n], ref

@@ -857,7 +857,7 @@ static int dedup_common(fdfs_gpu_ctx *ctx, const uint8_t *sig, uint32_t stride,
         return EINVAL;
     if (n == 0)
         return 0;
-    if (!sig || !rep_out || !ref_out || n >= 0xFFFFFFFFull)
+    if (!sig || !rep_out || n >= 0xFFFFFFFFull)  // ref_out == nullptr: packed answers at rep_out
         return EINVAL;
     // records are read as u64 words, rep written as u64
     if ((reinterpret_cast<uintptr_t>(sig) | reinterpret_cast<uintptr_t>(gidx) |
@@ -877,19 +877,29 @@ static int dedup_common(fdfs_gpu_ctx *ctx, const uint8_t *sig, uint32_t stride,
     hipEvent_t a, b;
     timing_pair(ctx, FDFS_KERNEL_DEDUP, a, b);
     hipError_t e = fdfs::launch_dedup_group(sig, stride, gidx, gstride, n, ctx->ws, rep_out, ref_out,
-                                            st, a, b);
+                                            ref_out == nullptr, st, a, b);
     return e == hipSuccess ? 0 : fail(ctx, e, "dedup launch");
 }
 
 int fdfs_gpu_dedup(fdfs_gpu_ctx *ctx, const uint8_t *sig, const uint64_t *gidx, uint64_t n,
                    uint64_t *rep_out, uint32_t *ref_out, void *stream)
 {
+    if (n && !ref_out)
+        return EINVAL;
     return dedup_common(ctx, sig, 24, gidx, gidx ? 1 : 0, n, rep_out, ref_out, stream);
+}
+
+int fdfs_gpu_dedup_packed(fdfs_gpu_ctx *ctx, const uint8_t *sig, const uint64_t *gidx, uint64_t n,
+                          fdfs_gpu_dedup_answer *out, void *stream)
+{
+    return dedup_common(ctx, sig, 24, gidx, gidx ? 1 : 0, n, reinterpret_cast<uint64_t *>(out), nullptr, stream);
 }
 
 int fdfs_gpu_dedup_group(fdfs_gpu_ctx *ctx, const uint8_t *records, uint64_t n, uint64_t *rep_out,
                          uint32_t *ref_out, void *stream)
 {
+    if (n && !ref_out)
+        return EINVAL;
     // rows {sig[24], gidx}: gidx is the 4th uint64 of each 32-byte row
     return dedup_common(ctx, records, 32, records ? reinterpret_cast<const uint64_t *>(records + 24) : nullptr,
                         4, n, rep_out, ref_out, stream);
@@ -1100,7 +1110,7 @@ int fdfs_gpu_index_ingest(fdfs_gpu_ctx *ctx, fdfs_gpu_index *ix, const uint8_t *
     hipEvent_t a, b;
     timing_pair(ctx, FDFS_KERNEL_DEDUP, a, b);
     // 1. the batch on its own (record positions as the ingest order)
-    hipError_t e = fdfs::launch_dedup_group(sig, 24, nullptr, 0, n, ctx->ws, rep_pos, ref_b, st, a, b);
+    hipError_t e = fdfs::launch_dedup_group(sig, 24, nullptr, 0, n, ctx->ws, rep_pos, ref_b, false, st, a, b);
     // 2. its classes against the index, 3. every record's answer
     if (e == hipSuccess)
         e = fdfs::launch_index_ingest(sig, gidx, ix->records, n, rep_pos, ref_b, ix->t, res_rep, res_ref,
@@ -1239,7 +1249,7 @@ static size_t dg_a_bytes(uint64_t n)
 
 static size_t dg_b_bytes(uint64_t m)
 {
-    return align_up(32 * m) + align_up(8 * m) + align_up(4 * m) + align_up(16 * m);
+    return align_up(32 * m) + align_up(16 * m);
 }
 
 // ann: nranks announcements of nranks + kAnnTail words, rank p's at p.
@@ -1309,9 +1319,7 @@ struct DgSide {
     uint64_t *cursor = nullptr;  // [64] bucket cursors
     uint64_t m = 0;              // rows this rank groups as owner
     uint8_t *rows_in = nullptr;  // [m]
-    uint64_t *rep_in = nullptr;  // [m]
-    uint32_t *ref_in = nullptr;  // [m]
-    uint64_t *ans = nullptr;     // [m] {rep, ref} for the way back
+    uint64_t *ans = nullptr;     // [m] {rep, ref} for the way back (the group's packed answers)
 };
 
 static void dg_carve_a(DgSide &s, void *mem)
@@ -1328,8 +1336,6 @@ static void dg_carve_b(DgSide &s, void *mem, uint64_t m)
     Carve c{static_cast<char *>(mem)};
     s.m = m;
     s.rows_in = c.take<uint8_t>(32 * m);
-    s.rep_in = c.take<uint64_t>(m);
-    s.ref_in = c.take<uint32_t>(m);
     s.ans = c.take<uint64_t>(2 * m);
 }
 
@@ -1372,16 +1378,13 @@ static hipError_t dg_announce(uint64_t *ann_tail, uint64_t *h, uint64_t b_room, 
 }
 
 // Phase 3: the owner groups its rows (min gidx from the rows' own word 3),
-// answers packed for the way back.
+// its answers written packed, {rep, ref} per row, as the way back sends them.
 static hipError_t dg_group(fdfs_gpu_ctx *ctx, DgSide &s, hipStream_t st)
 {
     hipEvent_t a, b;
     timing_pair(ctx, FDFS_KERNEL_DEDUP, a, b);
-    hipError_t e = fdfs::launch_dedup_group(s.rows_in, 32, reinterpret_cast<const uint64_t *>(s.rows_in + 24), 4, s.m,
-                                            ctx->ws, s.rep_in, s.ref_in, st, a, b);
-    if (e == hipSuccess)
-        e = fdfs::launch_answer_pack(s.rep_in, s.ref_in, s.m, s.ans, st);
-    return e;
+    return fdfs::launch_dedup_group(s.rows_in, 32, reinterpret_cast<const uint64_t *>(s.rows_in + 24), 4, s.m,
+                                    ctx->ws, s.ans, nullptr, true, st, a, b);
 }
 
 // Phase 5: the answers into record order.

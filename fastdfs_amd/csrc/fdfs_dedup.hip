@@ -257,13 +257,35 @@ __device__ __forceinline__ int32_t block_max_excl(int32_t v, int32_t *wmax)
     return run;
 }
 
+// Per-record answers: two arrays (rep u64[n], ref u32[n]), or packed (the
+// fdfs_gpu_dedup_answer array of fdfs_gpu_dedup_packed, and the exchange
+// rows of fdfs_gpu_dedup_global): 16 bytes {rep, ref, 0} per record at
+// `rep`.  Packed, a record's two answers share a line: one random store in
+// dp_group instead of two.
+struct DpOut {
+    uint64_t *rep;
+    uint32_t *ref;
+    bool packed;
+    __device__ __forceinline__ uint64_t rep_at(uint64_t r) const { return packed ? rep[2 * r] : rep[r]; }
+    __device__ __forceinline__ void store(uint64_t r, uint64_t rp, uint32_t rf, bool with_rep) const
+    {
+        if (packed) {
+            *reinterpret_cast<uint4 *>(rep + 2 * r) = make_uint4((uint32_t)rp, (uint32_t)(rp >> 32), rf, 0u);
+        } else {
+            if (with_rep)
+                rep[r] = rp;
+            ref[r] = rf;
+        }
+    }
+};
+
 // K1: keys, the singleton answer (rep = own gidx, ref = 1) of every record,
 // and the tile's entries sorted by digit (top d1 bits; unstable: order inside
 // a partition does not matter) written back as one contiguous run.
 __global__ __launch_bounds__(kDpTileThreads) void dp_tile_kernel(
     const uint8_t *__restrict__ sig, uint32_t stride, const uint64_t *__restrict__ gidx,
     uint32_t gstride, uint64_t n, int d1, uint64_t tiles, uint64_t *__restrict__ ent1,
-    uint64_t *__restrict__ rep_out, uint32_t *__restrict__ ref_out, uint64_t *__restrict__ cnt1,
+    DpOut out, uint64_t *__restrict__ cnt1,
     uint32_t *__restrict__ loc1)
 {
     __shared__ uint32_t h[1 << kDpMaxD1];
@@ -287,8 +309,7 @@ __global__ __launch_bounds__(kDpTileThreads) void dp_tile_kernel(
             key[it] = (uint32_t)sig_hash(a, b, c);
             // every record starts as its own class; dp_group overwrites the
             // records of classes with more than one member
-            rep_out[r] = gstride ? gidx[r * gstride] : r;
-            ref_out[r] = 1;
+            out.store(r, gstride ? gidx[r * gstride] : r, 1u, true);
         }
     }
 #pragma unroll
@@ -553,12 +574,12 @@ __device__ __forceinline__ uint32_t dp_insert(uint64_t *word, uint32_t size, uin
 // instead of a third array.  GM_INDEX: no gidx, the record index itself.
 enum { GM_INDEX = 0, GM_REP = 1, GM_ROW = 2 };
 
-__device__ __forceinline__ uint64_t gidx_of(const uint64_t *rep, const uint8_t *sig, uint32_t stride,
+__device__ __forceinline__ uint64_t gidx_of(const DpOut &out, const uint8_t *sig, uint32_t stride,
                                             int gmode, uint32_t r)
 {
     if (gmode == GM_ROW)
         return *reinterpret_cast<const uint64_t *>(sig + (uint64_t)r * stride + 24);
-    return gmode == GM_REP ? rep[r] : (uint64_t)r;
+    return gmode == GM_REP ? out.rep_at(r) : (uint64_t)r;
 }
 
 // The partition's entries, gathered from its run in each chunk of its
@@ -632,8 +653,7 @@ struct DpArgs {
     int gmode;
     uint64_t *gword, *gmin;
     uint32_t *gcnt, *gslot;
-    uint64_t *rep_out;
-    uint32_t *ref_out;
+    DpOut out;
 };
 
 // The LDS grouping of one partition whose entries are in registers (the
@@ -682,8 +702,8 @@ __device__ __forceinline__ void dp_group_lds(DpLds &L, const DpArgs &A, const ui
         } else {
             load_sig(A.sig + (uint64_t)x * A.stride, ra[k], rb[k], rc[k]);
             load_sig(A.sig + (uint64_t)y * A.stride, oa[k], ob[k], oc[k]);
-            gr[k] = gidx_of(A.rep_out, A.sig, A.stride, GM, x);
-            go[k] = gidx_of(A.rep_out, A.sig, A.stride, GM, y);
+            gr[k] = gidx_of(A.out, A.sig, A.stride, GM, x);
+            go[k] = gidx_of(A.out, A.sig, A.stride, GM, y);
         }
     }
 #pragma unroll
@@ -696,7 +716,7 @@ __device__ __forceinline__ void dp_group_lds(DpLds &L, const DpArgs &A, const ui
                 slot[k] = dp_insert<true>(L.word, kDpSlots, (uint32_t)(en[k] >> 32), r, dp_next(slot[k], kDpSlots, true),
                                           A.sig, A.stride, own[k]);
                 if (own[k] != r)
-                    go[k] = gidx_of(A.rep_out, A.sig, A.stride, GM, own[k]);
+                    go[k] = gidx_of(A.out, A.sig, A.stride, GM, own[k]);
             }
             atomicAdd(&L.cn[slot[k]], 1u);
             if (own[k] != r)
@@ -713,9 +733,8 @@ __device__ __forceinline__ void dp_group_lds(DpLds &L, const DpArgs &A, const ui
             if (c > 1 && !(PROBE & 2)) {
                 const uint32_t r = (uint32_t)en[k];
                 const uint64_t m = L.mn[slot[k]];
-                if (GM != GM_INDEX || m != r)  // the class's first record keeps dp_tile's rep = r
-                    A.rep_out[r] = m;
-                A.ref_out[r] = c;
+                // the class's first record keeps dp_tile's rep = r
+                A.out.store(r, m, c, GM != GM_INDEX || m != r);
             }
         }
     }
@@ -787,8 +806,8 @@ __device__ __forceinline__ void dp_group_slow(DpLds &L, uint32_t *rpos, uint64_t
             const uint32_t slot = dp_insert<false>(w, size, key, r, dp_home(key, size, false), A.sig, A.stride, o);
             atomicAdd(&c[slot], 1u);
             if (o != r) {
-                const uint64_t a = gidx_of(A.rep_out, A.sig, A.stride, A.gmode, r);
-                const uint64_t b2 = gidx_of(A.rep_out, A.sig, A.stride, A.gmode, o);
+                const uint64_t a = gidx_of(A.out, A.sig, A.stride, A.gmode, r);
+                const uint64_t b2 = gidx_of(A.out, A.sig, A.stride, A.gmode, o);
                 atomicMin(reinterpret_cast<unsigned long long *>(&m[slot]), (unsigned long long)(a < b2 ? a : b2));
             }
             A.gslot[vs + l] = slot;
@@ -805,8 +824,7 @@ __device__ __forceinline__ void dp_group_slow(DpLds &L, uint32_t *rpos, uint64_t
             const uint32_t slot = A.gslot[vs + l];
             if (c[slot] > 1) {
                 const uint32_t r = (uint32_t)A.ent2[dp_src(l, nk, rpos, rsrc)];
-                A.rep_out[r] = m[slot];
-                A.ref_out[r] = c[slot];
+                A.out.store(r, m[slot], c[slot], true);
             }
         }
         __syncthreads();
@@ -838,7 +856,7 @@ template <int PROBE, int GM>
 __global__ __launch_bounds__(kDpGroupThreads) __attribute__((amdgpu_waves_per_eu(8))) void dp_group_kernel(
     const uint64_t *__restrict__ ent2, int d2, uint64_t tiles, const uint64_t *__restrict__ off1,
     const uint32_t *__restrict__ cb, const uint16_t *__restrict__ cdo, const uint8_t *__restrict__ sig,
-    uint32_t stride, uint64_t *__restrict__ rep_out, uint32_t *__restrict__ ref_out, uint32_t *__restrict__ slow)
+    uint32_t stride, DpOut out, uint32_t *__restrict__ slow)
 {
     __shared__ DpLds L;
     uint32_t *rpos = reinterpret_cast<uint32_t *>(L.mn);
@@ -869,7 +887,7 @@ __global__ __launch_bounds__(kDpGroupThreads) __attribute__((amdgpu_waves_per_eu
         en[k] = l < cnt ? ent2[dp_src(l, R.nch, rpos, rsrc)] : 0ull;
     }
     __syncthreads();  // run table reads done before the table init
-    const DpArgs A{ent2, sig, stride, GM, nullptr, nullptr, nullptr, nullptr, rep_out, ref_out};
+    const DpArgs A{ent2, sig, stride, GM, nullptr, nullptr, nullptr, nullptr, out};
     dp_group_lds<PROBE, GM>(L, A, en, cnt);
 }
 
@@ -878,14 +896,13 @@ __global__ __launch_bounds__(kDpGroupThreads) void dp_group_slow_kernel(
     const uint64_t *__restrict__ ent2, int d2, uint64_t tiles, const uint64_t *__restrict__ off1,
     const uint32_t *__restrict__ cb, const uint16_t *__restrict__ cdo, const uint8_t *__restrict__ sig,
     uint32_t stride, int gmode, uint64_t *__restrict__ gword, uint64_t *__restrict__ gmin,
-    uint32_t *__restrict__ gcnt, uint32_t *__restrict__ gslot, uint64_t *__restrict__ rep_out,
-    uint32_t *__restrict__ ref_out, const uint32_t *__restrict__ slow)
+    uint32_t *__restrict__ gcnt, uint32_t *__restrict__ gslot, DpOut out, const uint32_t *__restrict__ slow)
 {
     __shared__ DpLds L;
     uint32_t *rpos = reinterpret_cast<uint32_t *>(L.mn);
     uint64_t *rsrc = L.mn + kDpRuns / 2;
     uint64_t *wsum = L.mn + kDpRuns / 2 + kDpRuns;
-    const DpArgs A{ent2, sig, stride, gmode, gword, gmin, gcnt, gslot, rep_out, ref_out};
+    const DpArgs A{ent2, sig, stride, gmode, gword, gmin, gcnt, gslot, out};
     const uint32_t ns = slow[0];
     for (uint32_t i = blockIdx.x; i < ns; i += gridDim.x) {
         DpRuns R;
@@ -918,7 +935,7 @@ static unsigned grid_for(uint64_t n, unsigned block)
 
 hipError_t launch_dedup_group(const uint8_t *sig, uint32_t sig_stride, const uint64_t *gidx,
                               uint32_t gidx_stride, uint64_t n, void *ws, uint64_t *rep_out,
-                              uint32_t *ref_out, hipStream_t st, hipEvent_t ev0, hipEvent_t ev1)
+                              uint32_t *ref_out, bool packed, hipStream_t st, hipEvent_t ev0, hipEvent_t ev1)
 {
     if (n == 0)
         return hipSuccess;
@@ -945,11 +962,12 @@ hipError_t launch_dedup_group(const uint8_t *sig, uint32_t sig_stride, const uin
     uint32_t *gcnt = reinterpret_cast<uint32_t *>(take(8 * n));
     uint32_t *slow = reinterpret_cast<uint32_t *>(take(4 * (pl.nparts() + 1)));  // count, partitions
     uint32_t *gslot = reinterpret_cast<uint32_t *>(ent1);  // ent1 is dead after dp_split
+    const DpOut out{rep_out, ref_out, packed};
     hipError_t e;
     if (ev0)
         (void)hipEventRecord(ev0, st);
     dp_tile_kernel<<<(unsigned)pl.tiles, kDpTileThreads, 0, st>>>(sig, sig_stride, gidx, gidx_stride, n, pl.d1,
-                                                                  pl.tiles, ent1, rep_out, ref_out, cnt1, loc1);
+                                                                  pl.tiles, ent1, out, cnt1, loc1);
     if ((e = launch_exclusive_scan(cnt1, ncnt, off1, bsum, st)) != hipSuccess)
         return e;
     dp_chunks_kernel<<<1, 256, 0, st>>>(off1, pl.d1, pl.tiles, cb, slow);
@@ -966,7 +984,7 @@ hipError_t launch_dedup_group(const uint8_t *sig, uint32_t sig_stride, const uin
                           : GM_REP;
 #define DP_GROUP(P, G)                                                                                       \
     dp_group_kernel<P, G><<<(unsigned)pl.nparts(), kDpGroupThreads, 0, st>>>(ent2, pl.d2, pl.tiles, off1, cb, cdo, \
-                                                                           sig, sig_stride, rep_out, ref_out, slow)
+                                                                           sig, sig_stride, out, slow)
 #ifdef FDFS_PROBES
     // measurement build only (make probes): FDFS_GPU_DEDUP_PROBE bit 0 = no
     // confirmation reads, bit 1 = no final stores (wrong results)
@@ -991,7 +1009,7 @@ hipError_t launch_dedup_group(const uint8_t *sig, uint32_t sig_stride, const uin
         DP_GROUP(0, GM_INDEX);
 #undef DP_GROUP
     dp_group_slow_kernel<<<256, kDpGroupThreads, 0, st>>>(ent2, pl.d2, pl.tiles, off1, cb, cdo, sig, sig_stride, gmode,
-                                                          gword, gmin, gcnt, gslot, rep_out, ref_out, slow);
+                                                          gword, gmin, gcnt, gslot, out, slow);
     if (ev1)
         (void)hipEventRecord(ev1, st);
     return hipGetLastError();
@@ -1068,17 +1086,9 @@ __global__ void bucket_scatter_kernel(const uint8_t *__restrict__ sig, const uin
     }
 }
 
-// Multi-GPU dedup (fdfs_gpu_dedup_global): the owner's per-row answers
-// packed as {rep, ref} pairs for the return exchange, and the exchanged
-// answers mapped back to the rank's records through row_of.
-__global__ void answer_pack_kernel(const uint64_t *__restrict__ rep, const uint32_t *__restrict__ ref,
-                                   uint64_t m, uint64_t *__restrict__ ans)
-{
-    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < m;
-         i += (uint64_t)gridDim.x * blockDim.x)
-        reinterpret_cast<ulonglong2 *>(ans)[i] = make_ulonglong2(rep[i], ref[i]);
-}
-
+// Multi-GPU dedup (fdfs_gpu_dedup_global): the exchanged {rep, ref} answers
+// (the owners' packed group output) mapped back to the rank's records
+// through row_of.
 __global__ void answer_gather_kernel(const uint64_t *__restrict__ back, const uint64_t *__restrict__ row_of,
                                      uint64_t n, uint64_t *__restrict__ rep_out, uint32_t *__restrict__ ref_out)
 {
@@ -1088,14 +1098,6 @@ __global__ void answer_gather_kernel(const uint64_t *__restrict__ back, const ui
         rep_out[i] = a.x;
         ref_out[i] = (uint32_t)a.y;
     }
-}
-
-hipError_t launch_answer_pack(const uint64_t *rep, const uint32_t *ref, uint64_t m, uint64_t *ans,
-                              hipStream_t st)
-{
-    if (m)
-        answer_pack_kernel<<<grid_for(m, 256), 256, 0, st>>>(rep, ref, m, ans);
-    return hipGetLastError();
 }
 
 hipError_t launch_answer_gather(const uint64_t *back, const uint64_t *row_of, uint64_t n, uint64_t *rep_out,

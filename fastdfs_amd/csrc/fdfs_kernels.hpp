@@ -152,9 +152,10 @@ hipError_t launch_scrub(const uint32_t *crc, const uint32_t *expect, uint32_t n,
 
 // dedup path (fdfs_dedup.hip)
 uint64_t dedup_ws_bytes(uint64_t n);
+// packed: rep_out is an array of 16-byte {rep, ref, 0} records (ref_out unused)
 hipError_t launch_dedup_group(const uint8_t *sig, uint32_t sig_stride, const uint64_t *gidx,
                               uint32_t gidx_stride, uint64_t n, void *ws, uint64_t *rep_out,
-                              uint32_t *ref_out, hipStream_t st, hipEvent_t ev0, hipEvent_t ev1);
+                              uint32_t *ref_out, bool packed, hipStream_t st, hipEvent_t ev0, hipEvent_t ev1);
 hipError_t launch_dedup_bucket(const uint8_t *sig, const uint64_t *gidx, uint64_t n,
                                uint32_t nranks, uint8_t *records_out, uint64_t *counts_out,
                                uint64_t *cursor, uint64_t *row_of_out, hipStream_t st,
@@ -176,8 +177,6 @@ hipError_t launch_index_ingest(const uint8_t *sig, const uint64_t *gidx, uint64_
                                uint64_t *res_rep, uint32_t *res_ref, uint64_t *rep_out, uint32_t *ref_out,
                                hipStream_t st);
 
-hipError_t launch_answer_pack(const uint64_t *rep, const uint32_t *ref, uint64_t m, uint64_t *ans,
-                              hipStream_t st);
 hipError_t launch_answer_gather(const uint64_t *back, const uint64_t *row_of, uint64_t n, uint64_t *rep_out,
                                 uint32_t *ref_out, hipStream_t st);
 

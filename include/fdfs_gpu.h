@@ -199,6 +199,18 @@ int fdfs_gpu_crc_combine(fdfs_gpu_ctx *ctx, const uint32_t *crc_a, const uint32_
 int fdfs_gpu_dedup(fdfs_gpu_ctx *ctx, const uint8_t *sig, const uint64_t *gidx,
                    uint64_t n, uint64_t *rep_out, uint32_t *ref_out, void *stream);
 
+/* The same answers packed, one 16-byte record per input record: rep and ref
+ * of a record share a cache line, so the group's random answer stores
+ * dirty one line per record instead of two (and the singleton answers are
+ * one 16-byte store).  out: device fdfs_gpu_dedup_answer[n], 8-aligned. */
+typedef struct {
+    uint64_t rep;       /* as rep_out of fdfs_gpu_dedup */
+    uint32_t ref;       /* as ref_out */
+    uint32_t reserved;  /* written 0 */
+} fdfs_gpu_dedup_answer;
+int fdfs_gpu_dedup_packed(fdfs_gpu_ctx *ctx, const uint8_t *sig, const uint64_t *gidx, uint64_t n,
+                          fdfs_gpu_dedup_answer *out, void *stream);
+
 /* Multi-GPU dedup building blocks (one process per GPU; the exchange between
  * the two calls is the caller's all-to-all over RCCL/xGMI).
  * Bucket: packs records {sig[24], gidx (uint64 LE)} into 32-byte rows grouped

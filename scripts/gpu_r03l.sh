@@ -1,0 +1,12 @@
+# Round 3: packed dedup answers -- parity (dedup tests, the config-5 set and
+# the multi-rank code, whose owner group now writes the packed rows), then
+# config 5 with rep/ref arrays vs packed records, alternating.
+export TMPDIR=/tmp
+O=gpurun_out/r03l; mkdir -p $O
+timeout -k 10 900 python3 -u -m pytest tests/test_gpu_dedup.py tests/test_gpu_configs.py -k "dedup or config5" -v --timeout 300 --timeout-method thread > $O/pytest.log 2>&1; rc=$?
+tail -3 $O/pytest.log; grep -E "FAILED|ERROR" $O/pytest.log | head
+[ $rc -ne 0 ] && exit $rc
+for r in 1 2; do for a in arrays packed; do
+  timeout -k 10 300 python3 bench.py --config c5 --steps 10 --warmup 3 --no-cpu-baseline --answers $a > $O/c5_${a}_$r.log 2>&1 || exit $?
+  python3 -c "import json;d=json.loads(open('$O/c5_${a}_$r.log').read().strip().split('\n')[-1]);print('$a r=$r', d['value'], d['ms_per_step'], d['roofline']['kernel_ms_avg'])"
+done; done

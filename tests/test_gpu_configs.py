@@ -96,15 +96,21 @@ def c5_oracle(oracle):
 
 def test_config5_bench_set(c5_oracle, ctxs):
     """The bench's config-5 set (100M signatures, 10 % duplicates) on one
-    GPU: every record's class source and class size equal the oracle's."""
+    GPU: every record's class source and class size equal the oracle's, as
+    rep/ref arrays and as packed records."""
     torch.cuda.empty_cache()
     orep, oref = c5_oracle
     sig, gidx = C.c5_signatures(C5_TOTAL, 1, 0, "cuda")
     rep, ref = ctxs[0].dedup(sig)
     torch.cuda.synchronize()
-    del sig, gidx
     assert np.array_equal(rep.cpu().numpy(), orep)
     assert np.array_equal(ref.cpu().numpy(), oref)
+    del rep, ref
+    out = ctxs[0].dedup_packed(sig).cpu().numpy()  # bench.py --answers packed
+    del sig, gidx
+    assert np.array_equal(out[:, 0], orep)
+    assert np.array_equal(out[:, 1], oref.astype(np.int64))
+    del out
     assert int(oref.max()) > 1 and (oref > 1).sum() > C5_TOTAL // 20
     torch.cuda.empty_cache()
 

@@ -159,6 +159,40 @@ def test_dedup_partition_plans(oracle, ctx, n):
     assert np.array_equal(ref.cpu().numpy(), oref.astype(np.int32))
 
 
+def _packed_case(name):
+    if name == "uniform":
+        return _sigs(300_000, 250_000, 5), None
+    if name == "gidx":
+        sig = _sigs(20_000, 5000, 9)
+        return sig, np.random.default_rng(9).permutation(10**9)[:20_000].astype(np.int64)
+    if name == "heavy":  # one class over the LDS table: the HBM-table path
+        sig = _sigs(200_000, 50_000, 11)
+        sig[::3] = sig[0]
+        return sig, None
+    coll = _colliding(3500, 3500)  # "collisions": one probe chain past the LDS table
+    sig = np.concatenate([np.tile(coll, (2, 1)), _sigs(30_000, 20_000, 78)])
+    return np.ascontiguousarray(sig[np.random.default_rng(5).permutation(len(sig))]), None
+
+
+@pytest.mark.parametrize("case", ["uniform", "gidx", "heavy", "collisions"])
+def test_dedup_packed_equals_arrays(oracle, ctx, case):
+    """fdfs_gpu_dedup_packed: the same rep / ref as fdfs_gpu_dedup in 16-byte
+    records (reserved word 0), through the LDS and the HBM-table groups and
+    with ingest indices (the class minimum read back from the packed
+    records); the arrays form against the oracle as well."""
+    sig, gidx = _packed_case(case)
+    st = torch.from_numpy(sig).cuda()
+    gt = None if gidx is None else torch.from_numpy(gidx).cuda()
+    rep, ref = ctx.dedup(st, gt)
+    out = ctx.dedup_packed(st, gt).cpu().numpy()
+    assert np.array_equal(out[:, 0], rep.cpu().numpy())
+    assert np.array_equal(out[:, 1], ref.cpu().numpy().astype(np.int64))
+    if gidx is None:
+        orep, oref = oracle.dedup(sig)
+        assert np.array_equal(out[:, 0], orep.astype(np.int64))
+        assert np.array_equal(out[:, 1], oref.astype(np.int64))
+
+
 def test_misaligned_records_rejected(ctx):
     """Records are read as u64 words: a signature buffer off an 8-byte
     boundary is EINVAL (0-or-errno convention), never a misaligned read."""
