@@ -314,13 +314,22 @@ KERNEL_OF = {F.SIG_CRC_ONLY: (_lib.KERNEL_CRC_SEG, "crc_seg_kernel<SAR,2>"),
              F.SIG_MD5: (_lib.KERNEL_SIG_LANE, "md5_stage_kernel<SAR>")}
 
 
-def chain_floor_ms(ctx, data, offs_t, sizes_t, sizes, method, kernel):
+def chain_floor_ms(ctx, data, offs_t, sizes_t, sizes, method, kernel, alone=False):
     """The lane-serial floor of a lane-per-file batch: the same kernel over
-    a batch of the batch's largest file alone (one lane, one dependent
-    chain: MD5 / ELFHash have no intra-file parallel form), timed by the
-    library's HIP events on the launch stream."""
+    a batch holding the batch's largest file (one lane, one dependent chain:
+    MD5 / ELFHash have no intra-file parallel form), timed by the library's
+    HIP events on the launch stream.  The largest file goes in with as many
+    empty files as keep the batch above the library's small-batch threshold
+    (one wave per SIMD, CUs x 256 files) when the real batch is above it, so
+    the file takes the path it takes in the batch (config 3: CRC fused into
+    its MD5 lane); alone=True times it as a one-file batch (config 3: the
+    small-batch path moves its CRC to the segmented kernel, the MD5 chain
+    alone)."""
     k = int(np.argmax(sizes))
-    o1, s1 = offs_t[k:k + 1].contiguous(), sizes_t[k:k + 1].contiguous()
+    lat = torch.cuda.get_device_properties(data.device).multi_processor_count * 256
+    pad = lat if (len(sizes) > lat and not alone) else 0
+    o1 = torch.cat([offs_t[k:k + 1], offs_t[k:k + 1].expand(pad)]).contiguous()
+    s1 = torch.cat([sizes_t[k:k + 1], torch.zeros(pad, dtype=sizes_t.dtype, device=sizes_t.device)]).contiguous()
     ctx.sig_batch(data, o1, s1, method=method, check_bounds=False)
     torch.cuda.synchronize()
     ctx.set_timing(True)
@@ -473,7 +482,13 @@ def main():
                          "frac": round(fms / avg_ms, 4), "hbm_frac": round(achieved / HBM_PEAK_GBS, 4),
                          "chain_floor_ms": round(fms, 3), "chain_floor_file_bytes": fbytes,
                          "note": "peak = batch bytes over the time the same kernel takes for the "
-                                 "largest file alone (one lane's serial chain)"})
+                                 "largest file on the path it takes in the batch (one lane's serial "
+                                 "chain; the other files of that timing batch are empty)"})
+            if method == F.SIG_MD5:
+                ams, _ = chain_floor_ms(ctx, data, offs_t, sizes_t, sizes, method, kernel, alone=True)
+                roof["md5_alone_floor_ms"] = round(ams, 3)
+                roof["md5_alone_note"] = ("the largest file as a one-file batch: its CRC moves to the "
+                                          "segmented kernel and the lane runs MD5 alone")
         res["roofline"] = roof
         valu = load_valu(args.config, avg_ms) if not args.method else None
         if valu:

@@ -10,3 +10,5 @@ for r in 1 2; do for a in arrays packed; do
   timeout -k 10 300 python3 bench.py --config c5 --steps 10 --warmup 3 --no-cpu-baseline --answers $a > $O/c5_${a}_$r.log 2>&1 || exit $?
   python3 -c "import json;d=json.loads(open('$O/c5_${a}_$r.log').read().strip().split('\n')[-1]);print('$a r=$r', d['value'], d['ms_per_step'], d['roofline']['kernel_ms_avg'])"
 done; done
+timeout -k 10 600 python3 bench.py --config c3 --steps 3 --warmup 1 --no-cpu-baseline > $O/c3.log 2>&1 || exit $?
+python3 -c "import json;d=json.loads(open('$O/c3.log').read().strip().split('\n')[-1]);print(d['value'], d['ms_per_step'], d['roofline'])"
