@@ -311,7 +311,7 @@ def dedup_strong(ctx, sig, gidx, world, steps, warmup):
 METHODS = {"crc": F.SIG_CRC_ONLY, "hash": F.SIG_HASH, "md5": F.SIG_MD5}
 KERNEL_OF = {F.SIG_CRC_ONLY: (_lib.KERNEL_CRC_SEG, "crc_seg_kernel<SAR,2>"),
              F.SIG_HASH: (_lib.KERNEL_SIG_LANE, "sig_hash_kernel<SAR>"),
-             F.SIG_MD5: (_lib.KERNEL_SIG_LANE, "md5_stage_kernel<SAR>")}
+             F.SIG_MD5: (_lib.KERNEL_SIG_LANE, "md5_pair_kernel<SAR>")}
 
 
 def chain_floor_ms(ctx, data, offs_t, sizes_t, sizes, method, kernel, alone=False):

@@ -306,6 +306,181 @@ __global__ __launch_bounds__(64 * kMd5Waves) void md5_stage_kernel(
     }
 }
 
+// ------------------------------------------------ MD5 path, paired waves
+//
+// The one-shot batch form (no state) of the kernel above with the CRC taken
+// off the MD5 lane.  A workgroup is two waves on one 64-file chunk at a time:
+// wave 0 runs the 64 MD5 chains only; wave 1 issues the cooperative loads,
+// stages each round's 128 bytes of every file in LDS and computes the CRCs
+// from the same rows.  In the fused form the CRC's ~35 instructions per 16
+// bytes sit on the MD5 lane, whose wave issues one instruction every several
+// cycles (a dependent chain at one wave per SIMD): the largest file's chain
+// was 80 ms fused against 53-58 ms for MD5 alone (profiles/r02).  Here the
+// CRC runs on a second wave that fills the issue slots the MD5 chain leaves
+// empty, and the MD5 wave has neither loads nor LDS stores to issue.
+//
+// Rows are double-buffered: the loader writes round r into buffer r & 1,
+// both waves meet at one barrier per round, then hash that buffer.  The
+// loader writes buffer (r + 1) & 1 only after the barrier of round r, which
+// the MD5 wave reaches only once it has finished round r - 1 on that buffer.
+// The barrier is s_barrier after lgkmcnt(0) alone: the loader's next round of
+// loads stays in flight across it (__syncthreads would wait for them).
+// Four workgroups per CU (35.8 KB of LDS each), the same 64 MD5 lanes per
+// SIMD as the fused form's one wave per SIMD.
+__device__ __forceinline__ void pair_barrier()
+{
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+}
+
+template <bool SAR>
+__global__ __launch_bounds__(128) void md5_pair_kernel(
+    const uint8_t *__restrict__ base, const uint64_t *__restrict__ offs,
+    const uint64_t *__restrict__ sizes, const uint32_t *__restrict__ order, uint32_t n,
+    const DevTables *__restrict__ tabs, const uint64_t *__restrict__ big_min_p, uint32_t *__restrict__ queue,
+    int pmode, uint32_t *__restrict__ crc_out, uint8_t *__restrict__ sig_out, int32_t *__restrict__ codes_out)
+{
+    // pmode (probe build only; 0 in production): 1 = MD5 wave at s_setprio
+    // 2, 2 = no CRC arithmetic, 3 = no MD5 arithmetic (wrong results)
+    constexpr int CH = kMd5Chunk;
+    constexpr int PIECES = CH / 16;
+    constexpr int FPI = 64 / PIECES;
+    constexpr int NLD = 64 / FPI;
+    constexpr int STRIDE = CH + 16;
+    constexpr int BPR = CH / 64;
+    static_assert(NLD == 8, "the asm waits below name 8 registers");
+    __shared__ uint32_t sD[16 * 256];
+    __shared__ uint32_t sT[256];
+    __shared__ __attribute__((aligned(16))) uint8_t sbuf[2][64 * STRIDE];
+    __shared__ uint32_t s_chunk;
+    lds_fill(sD, &tabs->t.D[0][0], 16 * 256);
+    lds_fill(sT, tabs->t.T, 256);
+    __syncthreads();
+    typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+    // wave-uniform role (an SGPR, so both roles' barriers are scalar branches)
+    const bool loader = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6) != 0;
+    if (!loader && pmode == 1)
+        __builtin_amdgcn_s_setprio(2);
+    const int lane = threadIdx.x & 63;
+    const uint32_t nw = (n + 63) / 64;
+    const uint8_t *safe = reinterpret_cast<const uint8_t *>(tabs);
+    const uint32_t K16 = tabs->t.K16;
+    const uint64_t big_min = big_min_p ? *big_min_p : ~0ull;
+    for (;;) {
+        if (threadIdx.x == 64)
+            s_chunk = atomicAdd(queue, 1u);
+        __syncthreads();
+        const uint32_t chunk = __builtin_amdgcn_readfirstlane(s_chunk);
+        __syncthreads();  // s_chunk read by both waves before the next chunk's write
+        if (chunk >= nw)
+            break;
+        const uint32_t i = chunk * 64 + lane;
+        bool valid = i < n;
+        uint32_t f = valid ? order[i] : 0;
+        if (f >= n) {  // a stale order entry (the binning flagged it): no file
+            valid = false;
+            f = 0;
+        }
+        const uint64_t L = valid ? sizes[f] : 0;
+        const uint8_t *p = valid ? base + offs[f] : safe;
+        const uint64_t nblk = L >> 6;
+        uint64_t mx = nblk;
+#pragma unroll
+        for (int o = 32; o; o >>= 1) {
+            const uint64_t y = __shfl_xor(mx, o);
+            mx = y > mx ? y : mx;
+        }
+        const uint64_t rounds = (mx + BPR - 1) / BPR;
+        const uint8_t *tp = p + (nblk << 6);
+        if (loader) {
+            const bool small = L < big_min && pmode != 2;  // else the CRC comes from crc_seg_kernel
+            const int piece = lane % PIECES, fsub = lane / PIECES;
+            const uint8_t *lp[NLD];
+            uint64_t lim[NLD];
+#pragma unroll
+            for (int k = 0; k < NLD; k++) {
+                const int src = k * FPI + fsub;
+                lp[k] = reinterpret_cast<const uint8_t *>(__shfl((uintptr_t)p, src)) + piece * 16;
+                lim[k] = __shfl(nblk, src) * 4;
+            }
+            u32x4 RA[NLD], RB[NLD];
+            auto issue = [&](u32x4 (&R)[NLD], uint64_t r) {
+                const uint64_t rp = r * PIECES + piece;
+#pragma unroll
+                for (int k = 0; k < NLD; k++) {
+                    const uint8_t *a = (rp < lim[k]) ? lp[k] + r * CH : safe;
+                    asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(R[k]) : "v"(a) : "memory");
+                }
+            };
+            auto stage = [&](u32x4 (&R)[NLD], uint8_t *tile) {
+                asm volatile("s_waitcnt vmcnt(8)" : "+v"(R[0]), "+v"(R[1]), "+v"(R[2]), "+v"(R[3]) :: "memory");
+                asm volatile("" : "+v"(R[4]), "+v"(R[5]), "+v"(R[6]), "+v"(R[7]));
+#pragma unroll
+                for (int k = 0; k < NLD; k++)
+                    *reinterpret_cast<u32x4 *>(tile + (k * FPI + fsub) * STRIDE + piece * 16) = R[k];
+            };
+            uint32_t c = 0xFFFFFFFFu;  // CRC32_XINIT (storage/storage_service.c:7149)
+            auto crc_round = [&](uint64_t r, const uint8_t *tile) {
+                const uint4 *q = reinterpret_cast<const uint4 *>(tile + lane * STRIDE);
+#pragma unroll
+                for (int b = 0; b < BPR; b++)
+                    if (small && r * BPR + b < nblk) {
+                        c = chain16<SAR>(sD, c, q[4 * b + 0], K16);
+                        c = chain16<SAR>(sD, c, q[4 * b + 1], K16);
+                        c = chain16<SAR>(sD, c, q[4 * b + 2], K16);
+                        c = chain16<SAR>(sD, c, q[4 * b + 3], K16);
+                    }
+            };
+            issue(RA, 0);
+            for (uint64_t r = 0; r < rounds; r += 2) {
+                issue(RB, r + 1);
+                stage(RA, sbuf[0]);
+                pair_barrier();
+                crc_round(r, sbuf[0]);
+                issue(RA, r + 2);
+                if (r + 1 < rounds) {
+                    stage(RB, sbuf[1]);
+                    pair_barrier();
+                    crc_round(r + 1, sbuf[1]);
+                }
+            }
+            asm volatile("s_waitcnt vmcnt(0)"
+                         : "+v"(RA[0]), "+v"(RA[1]), "+v"(RA[2]), "+v"(RA[3]), "+v"(RA[4]), "+v"(RA[5]),
+                           "+v"(RA[6]), "+v"(RA[7]), "+v"(RB[0]), "+v"(RB[1]), "+v"(RB[2]), "+v"(RB[3]),
+                           "+v"(RB[4]), "+v"(RB[5]), "+v"(RB[6]), "+v"(RB[7]) :: "memory");
+            if (valid && small) {
+                const uint32_t rt = (uint32_t)(L & 63u);
+                for (uint32_t k = 0; k < rt; k++)  // CRC of the tail bytes
+                    c = crc_byte<SAR>(sT, c, tp[k]);
+                crc_out[f] = c ^ 0xFFFFFFFFu;  // CRC32_FINAL (storage/storage_dio.c:500)
+            }
+        } else {
+            uint32_t st[4] = {0x67452301u, 0xefcdab89u, 0x98badcfeu, 0x10325476u};  // my_md5_init
+            const uint8_t *mine = &sbuf[0][0] + lane * STRIDE;
+            for (uint64_t r = 0; r < rounds; r++) {
+                pair_barrier();
+                const uint4 *q = reinterpret_cast<const uint4 *>(mine + (r & 1) * (64 * STRIDE));
+#pragma unroll
+                for (int b = 0; b < BPR; b++) {
+                    if (r * BPR + b < nblk && pmode != 3) {
+                        const uint4 a0 = q[4 * b], a1 = q[4 * b + 1], a2 = q[4 * b + 2], a3 = q[4 * b + 3];
+                        const uint32_t m[16] = {a0.x, a0.y, a0.z, a0.w, a1.x, a1.y, a1.z, a1.w,
+                                                a2.x, a2.y, a2.z, a2.w, a3.x, a3.y, a3.z, a3.w};
+                        md5_compress(st, m);
+                    }
+                }
+            }
+            if (valid) {
+                md5_finish(st, tp, L);
+                if (sig_out)  // memcpy(sig + 8, md5 digest, 16) (storage/storage_service.c:119)
+                    store_sig(sig_out + 24ull * f, L, st[0], st[1], st[2], st[3]);
+                if (codes_out)
+                    reinterpret_cast<int4 *>(codes_out)[f] =
+                        make_int4((int)st[0], (int)st[1], (int)st[2], (int)st[3]);
+            }
+        }
+    }
+}
+
 hipError_t launch_md5_stage(bool sar, const uint8_t *base, const uint64_t *offs,
                             const uint64_t *sizes, uint32_t n, const uint32_t *order,
                             const DevTables *tabs, const uint64_t *big_min, uint32_t *queue, uint32_t *crc_out,
@@ -333,6 +508,26 @@ hipError_t launch_md5_stage(bool sar, const uint8_t *base, const uint64_t *offs,
 #endif
     constexpr unsigned kBlk = 64 * kMd5Waves;
     const uint32_t nw = (n + 63) / 64;
+#ifdef FDFS_PROBES
+    static int pair = -1;
+    if (pair < 0) {  // A/B (make probes): FDFS_GPU_MD5_PAIR=0 -> the fused kernel, 2.. -> md5_pair_kernel pmode 1..
+        const char *ev = getenv("FDFS_GPU_MD5_PAIR");
+        pair = ev ? atoi(ev) : 1;
+    }
+#else
+    constexpr int pair = 1;
+#endif
+    if (pair != 0 && mode != 0 && queue && !states) {  // queue zeroed by the caller
+        const unsigned g = 4u * (unsigned)ncu[dev];
+        const unsigned grid2 = g < nw ? g : nw;
+        if (sar)
+            md5_pair_kernel<true><<<grid2, 128, 0, st>>>(base, offs, sizes, order, n, tabs, big_min, queue, pair - 1,
+                                                        crc_out, sig_out, codes_out);
+        else
+            md5_pair_kernel<false><<<grid2, 128, 0, st>>>(base, offs, sizes, order, n, tabs, big_min, queue, pair - 1,
+                                                         crc_out, sig_out, codes_out);
+        return hipGetLastError();
+    }
     unsigned grid = (n + kBlk - 1) / kBlk;
     uint32_t *q = nullptr;
     if (mode && queue) {  // queue zeroed by the caller (launch_sig_lane's workspace memset)
