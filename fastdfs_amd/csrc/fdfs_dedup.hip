@@ -20,13 +20,15 @@
 //      K4 dp_split     one workgroup per chunk: gathers its entries along the
 //                      tile runs, sorts them by the next D2 bits in LDS and
 //                      writes the chunk back contiguously
-//      K5 dp_group     one workgroup per partition (~1K records): gathers its
-//                      run from each chunk of its bucket; an open-addressing
-//                      table in LDS keyed by key32, a slot is claimed by
-//                      64-bit CAS of {key32, claimer} and never changes,
-//                      equal keys are confirmed on the full 24 bytes against
-//                      the claimer's row, class min(gidx) and size by LDS
-//                      atomics, then rep/ref written per record.
+//      K5 dp_group     one workgroup per partition (~1.5K records): gathers
+//                      its run from each chunk of its bucket; an
+//                      open-addressing table in LDS keyed by key bits, a
+//                      slot is claimed by 32-bit CAS of {key bits, claimer's
+//                      local index} and never changes, the entries that met
+//                      an equal key are listed and confirmed on the full 24
+//                      bytes against the claimer's row, class min(gidx) and
+//                      size by LDS atomics, then rep/ref written per record
+//                      of a multi-member class.
 //    Every random-access atomic stays in LDS: device-scope atomics to
 //    random addresses run at a few percent of the HBM rate on MI355X
 //    (MI355X_MICROARCH.md, global atomics), which is what bounded the
@@ -40,6 +42,7 @@
 
 #include <climits>
 #include <cstdlib>
+#include <type_traits>
 
 namespace fdfs {
 
@@ -103,28 +106,28 @@ constexpr int kDpSplitThreads = 1024;
 constexpr int kDpSplitPer = 8;
 constexpr int kDpChunk = kDpSplitThreads * kDpSplitPer;  // entries per K4 chunk
 static_assert(kDpChunk < 65536, "chunk digit starts are u16");
-// LDS table of the group kernel: 2048 slots (40 KB) for partitions of up to
-// 1024 records (mean <= 768), four 512-thread workgroups per CU.  The group
-// is latency-bound (a chain of dependent global round trips per partition),
-// so what sets its rate is the number of partitions in flight per CU: four
-// half-size ones instead of round 2's two 4096-slot / 1024-thread ones, the
-// same 32 waves per CU.  FDFS_DP_TABLE_LOG=12 builds the round-2 form
-// (`make ab`, the A/B library).
-#ifndef FDFS_DP_TABLE_LOG
-#define FDFS_DP_TABLE_LOG 11
-#endif
-constexpr int kDpSlotsLog = FDFS_DP_TABLE_LOG;
-constexpr int kDpSlots = 1 << kDpSlotsLog;
-// Records per partition grouped in LDS: two entries per thread of the
-// group.  At three the per-thread arrays of the confirmation phase went past
-// the 64 VGPRs of 32 waves per CU and hipcc spilled them to scratch,
-// serialising the three entries' row loads into three round trips.
-// dp_plan keeps the mean partition at <= 3/4 of the cap, ~9 sigma below it
-// for uniform keys; larger partitions (heavy duplication, adversarial keys)
-// take dp_group_slow.
-constexpr uint32_t kDpCap = kDpSlots / 2;
+// The group kernel is latency-bound: a partition is a chain of dependent
+// round trips (run table, entries, confirmation rows, answers), so its rate
+// is the number of records in flight per CU, which LDS and registers cap.
+// Round 3: 512-thread workgroups of up to 2048 records (four entries per
+// thread, mean <= 1536), an LDS table of 32-bit words {key bits, local
+// index} (the partition's records by local index beside it), and only the
+// entries that met an equal key -- compacted into a list -- load rows, so
+// no thread holds rows for entries that joined nothing.  40 KB per
+// workgroup (GM_INDEX; 48 KB with 64-bit class minima): four workgroups =
+// 8192 records in flight per CU, twice round 2's two-entry form (64-bit
+// words {key32, record}, 20 B per slot at two slots per record).
+constexpr int kDpGroupThreads = 512;
+constexpr int kDpEpt = 4;  // entries per thread
+constexpr uint32_t kDpCap = kDpGroupThreads * kDpEpt;  // records per partition grouped in LDS
+// 3070 slots: load <= 2/3 at the cap (<= 1/2 at dp_plan's mean); the two
+// spare words of a 3072-word region keep the arrays after it 8-byte aligned.
+constexpr uint32_t kDpSlots = kDpCap * 3 / 2 - 2;
+constexpr int kDpLocBits = 12;  // local index field of an LDS table word
+static_assert(kDpCap < (1u << kDpLocBits), "local index field");
+constexpr uint32_t kDpKeyMask = (1u << (32 - kDpLocBits)) - 1;  // key bits kept in a word
+constexpr uint32_t kDpWEmpty = ~0u;
 constexpr uint64_t kDpEmpty = ~0ull;
-constexpr int kDpGroupThreads = kDpSlots / 4;
 constexpr int kDpRuns = kDpGroupThreads;  // chunk runs per K5 gather batch (one per thread)
 
 struct DpPlan {
@@ -513,24 +516,24 @@ __global__ __launch_bounds__(kDpSplitThreads) void dp_split_kernel(
         cdo[(uint64_t)g * nd2 + k] = (uint16_t)cl[k];
 }
 
-// Open-addressing tables (LDS or a partition's HBM region) hold one 64-bit
-// word per slot: {key32, claimer record}, set once by CAS and never changed.
-__device__ __forceinline__ uint32_t dp_home(uint32_t key, uint32_t size, bool masked)
+// Open-addressing tables, linear probing from a multiplicative home slot.
+// Every slot is set once by CAS and never changed, so the first slot with a
+// given key along a probe sequence is the same for every later probe.
+__device__ __forceinline__ uint32_t dp_home(uint32_t key, uint32_t size)
 {
-    return masked ? ((key * 0x9E3779B1u) >> (32 - kDpSlotsLog))
-                  : (uint32_t)(((uint64_t)(key * 0x9E3779B1u) * size) >> 32);
+    return (uint32_t)(((uint64_t)(key * 0x9E3779B1u) * size) >> 32);
 }
 
-__device__ __forceinline__ uint32_t dp_next(uint32_t slot, uint32_t size, bool masked)
+__device__ __forceinline__ uint32_t dp_next(uint32_t slot, uint32_t size)
 {
-    return masked ? ((slot + 1) & (kDpSlots - 1)) : (slot + 1 == size ? 0 : slot + 1);
+    return slot + 1 == size ? 0 : slot + 1;
 }
 
+// HBM table of an oversized partition: 64-bit words {key32, claimer record}.
 // Key-only probe from `slot`: claim the first empty slot, or stop at the
 // first slot whose key equals ours.  Returns the slot; `owner` = its claimer
 // (r itself when this record claimed it).  Equal keys still need the
 // full-signature check (dp_insert continues past a mismatch).
-template <bool MASKED>
 __device__ __forceinline__ uint32_t dp_probe(uint64_t *word, uint32_t size, uint32_t key, uint32_t r,
                                              uint32_t slot, uint32_t &owner)
 {
@@ -548,22 +551,46 @@ __device__ __forceinline__ uint32_t dp_probe(uint64_t *word, uint32_t size, uint
             owner = (uint32_t)cur;
             return slot;
         }
-        slot = dp_next(slot, size, MASKED);
+        slot = dp_next(slot, size);
     }
 }
 
 // Full insert from `slot`: probe, confirm an equal key on the 24 bytes, walk
 // on past a key collision with a different signature.
-template <bool MASKED>
 __device__ __forceinline__ uint32_t dp_insert(uint64_t *word, uint32_t size, uint32_t key, uint32_t r,
                                               uint32_t slot, const uint8_t *sig, uint32_t stride,
                                               uint32_t &owner)
 {
     for (;;) {
-        slot = dp_probe<MASKED>(word, size, key, r, slot, owner);
+        slot = dp_probe(word, size, key, r, slot, owner);
         if (owner == r || sig_equal(sig, stride, r, owner))
             return slot;
-        slot = dp_next(slot, size, MASKED);
+        slot = dp_next(slot, size);
+    }
+}
+
+// LDS table of a partition: 32-bit words {low key bits << kDpLocBits | local
+// index of the claimer}.  Within a partition the top d1 + d2 key bits are
+// all equal, so the kept 20 bits hold every bit that tells its records apart
+// (16 of them at dp_plan's 2^16 partitions for 100M records).
+__device__ __forceinline__ uint32_t dp_lprobe(uint32_t *word, uint32_t kb, uint32_t l, uint32_t slot,
+                                              uint32_t &owner)
+{
+    const uint32_t mine = kb << kDpLocBits | l;
+    for (;;) {
+        uint32_t cur = word[slot];
+        if (cur == kDpWEmpty) {
+            cur = atomicCAS(&word[slot], kDpWEmpty, mine);
+            if (cur == kDpWEmpty) {
+                owner = l;
+                return slot;  // claimed
+            }
+        }
+        if ((cur >> kDpLocBits) == kb) {
+            owner = cur & ((1u << kDpLocBits) - 1);
+            return slot;
+        }
+        slot = dp_next(slot, kDpSlots);
     }
 }
 
@@ -636,15 +663,20 @@ __device__ __forceinline__ uint64_t dp_src(uint32_t l, uint32_t nk, const uint32
 // Only records of classes with more than one member are written (random
 // stores); K1 already wrote every record's singleton answer.  The class
 // minimum needs ingest indices only there: every member that joined a
-// claimed slot folds min(own, claimer's) into the slot, so a class of k > 1
-// members gets all k indices and a singleton reads none.
-constexpr int kDpEpt = (kDpCap + kDpGroupThreads - 1) / kDpGroupThreads;  // entries per thread
+// claimed slot folds min(own, claimer's) into the claimer's minimum, so a
+// class of k > 1 members gets all k indices and a singleton reads none.
+template <int GM>
+using DpMin = typename std::conditional<GM == GM_INDEX, uint32_t, uint64_t>::type;
 
-struct DpLds {  // dp_group_kernel's LDS table (20 B per slot: 40 KB, four workgroups per CU)
-    uint64_t word[kDpSlots];
-    uint64_t mn[kDpSlots];
-    uint32_t cn[kDpSlots];
+template <int GM>
+struct alignas(16) DpLds {  // 40 KB for GM_INDEX (four workgroups per CU), 48 KB with 64-bit minima
+    uint32_t word[kDpSlots + 2];  // the table; before it, the gather's run table (dp_run_tables)
+    uint32_t rec[kDpCap];         // local index -> record
+    uint32_t cn[kDpCap / 2];      // class sizes (u16 pairs) at the claimer's local index
+    uint32_t jl[kDpCap];          // entries that met an equal key: local | claimer << 16; jl[kDpCap - 1] = count
+    DpMin<GM> mn[kDpCap];         // class minimum ingest index at the claimer's local index
 };
+static_assert(sizeof(DpLds<GM_INDEX>) == 40960, "four workgroups per CU");
 
 struct DpArgs {
     const uint64_t *ent2;
@@ -656,133 +688,188 @@ struct DpArgs {
     DpOut out;
 };
 
-// The LDS grouping of one partition whose entries are in registers (the
-// round-1 code path).  Ends with a barrier.
+// The gather's run table lives in the LDS table region (dead before the
+// table is initialised).
+struct DpRunTab {
+    uint32_t *rpos;
+    uint64_t *rsrc, *wsum;
+    template <int GM>
+    __device__ explicit DpRunTab(DpLds<GM> &L)
+        : rpos(L.word), rsrc(reinterpret_cast<uint64_t *>(L.word + kDpRuns)), wsum(rsrc + kDpRuns)
+    {
+    }
+};
+static_assert(kDpRuns + 2 * kDpRuns + 2 * (kDpGroupThreads / 64) <= kDpSlots, "gather tables fit in the table region");
+
+__device__ __forceinline__ void dp_lds_min(uint32_t *p, uint64_t v) { atomicMin(p, (uint32_t)v); }
+__device__ __forceinline__ void dp_lds_min(uint64_t *p, uint64_t v)
+{
+    atomicMin(reinterpret_cast<unsigned long long *>(p), (unsigned long long)v);
+}
+
+__device__ __forceinline__ uint32_t dp_cn(const uint32_t *cn, uint32_t l)
+{
+    return (cn[l >> 1] >> (16 * (l & 1))) & 0xFFFFu;
+}
+
+// The LDS grouping of one partition whose key halves and records (kh, rc)
+// are in registers, entry k of this thread at local index threadIdx.x + k *
+// 512.  Ends with a barrier.
 // probe: measurement build only (make probes), FDFS_GPU_DEDUP_PROBE bit 0 =
 // no confirmation reads (every equal key taken as equal), bit 1 = no final
 // stores; results are wrong under either
 template <int PROBE, int GM>
-__device__ __forceinline__ void dp_group_lds(DpLds &L, const DpArgs &A, const uint64_t (&en)[kDpEpt], uint32_t cnt)
+__device__ __forceinline__ void dp_group_lds(DpLds<GM> &L, const DpArgs &A, const uint32_t (&kh)[kDpEpt],
+                                             const uint32_t (&rc)[kDpEpt], uint32_t cnt)
 {
-    for (int k = threadIdx.x; k < kDpSlots; k += blockDim.x) {
-        L.word[k] = kDpEmpty;
-        L.mn[k] = kDpEmpty;
-        L.cn[k] = 0;
+    constexpr int NT = kDpGroupThreads;
+    for (int k = threadIdx.x; k < (int)kDpSlots; k += NT)
+        L.word[k] = kDpWEmpty;
+    for (int k = threadIdx.x; k < (int)kDpCap / 2; k += NT)
+        L.cn[k] = 0x00010001u;  // every entry counts itself (read at claimers only)
+    for (int k = threadIdx.x; k < (int)kDpCap; k += NT)
+        L.mn[k] = (DpMin<GM>)~0ull;
+#pragma unroll
+    for (int k = 0; k < kDpEpt; k++) {
+        const uint32_t l = threadIdx.x + k * NT;
+        if (l < cnt)
+            L.rec[l] = rc[k];
+    }
+    if (threadIdx.x == 0)
+        L.jl[kDpCap - 1] = 0;
+    __syncthreads();
+    // (1) key-only probes, LDS only; an entry that met an equal key goes to
+    // the list (at most cnt - 1 of them: every class has a claimer)
+    uint32_t claim = 0;  // bit k: entry k claimed its slot
+#pragma unroll
+    for (int k = 0; k < kDpEpt; k++) {
+        const uint32_t l = threadIdx.x + k * NT;
+        if (l < cnt) {
+            uint32_t own;
+            dp_lprobe(L.word, kh[k] & kDpKeyMask, l, dp_home(kh[k], kDpSlots), own);
+            if (own == l)
+                claim |= 1u << k;
+            else
+                L.jl[atomicAdd(&L.jl[kDpCap - 1], 1u)] = l | own << 16;
+        }
     }
     __syncthreads();
-    // (1) key-only probes: LDS only
-    uint32_t slot[kDpEpt], own[kDpEpt];
-#pragma unroll
-    for (int k = 0; k < kDpEpt; k++) {
-        const uint32_t l = threadIdx.x + k * kDpGroupThreads;
-        own[k] = (uint32_t)en[k];
-        if (l < cnt) {
-            const uint32_t key = (uint32_t)(en[k] >> 32);
-            slot[k] = dp_probe<true>(L.word, kDpSlots, key, (uint32_t)en[k], dp_home(key, kDpSlots, true), own[k]);
-        }
-    }
-    // (2) confirmations of every joined entry issued together: both
-    // signature rows and both ingest indices per entry.  Branch-free: an
-    // entry that joined nothing reads record 0's row (one cached line per
-    // wave) and ignores it, so every entry's loads leave back to back and
-    // the wave waits once (in if-blocks hipcc waited for each entry's rows
-    // before issuing the next entry's).
-    uint64_t ra[kDpEpt], rb[kDpEpt], rc[kDpEpt], oa[kDpEpt], ob[kDpEpt], oc[kDpEpt];
-    uint64_t gr[kDpEpt], go[kDpEpt];
-#pragma unroll
-    for (int k = 0; k < kDpEpt; k++) {
-        const uint32_t r = (uint32_t)en[k];
-        const uint32_t l = threadIdx.x + k * kDpGroupThreads;
-        const bool jn = l < cnt && own[k] != r;
-        const uint32_t x = jn ? r : 0u, y = jn ? own[k] : 0u;
-        if constexpr (PROBE & 1) {
-            ra[k] = rb[k] = rc[k] = oa[k] = ob[k] = oc[k] = 0;
-            gr[k] = r;
-            go[k] = own[k];
-        } else {
-            load_sig(A.sig + (uint64_t)x * A.stride, ra[k], rb[k], rc[k]);
-            load_sig(A.sig + (uint64_t)y * A.stride, oa[k], ob[k], oc[k]);
-            gr[k] = gidx_of(A.out, A.sig, A.stride, GM, x);
-            go[k] = gidx_of(A.out, A.sig, A.stride, GM, y);
-        }
-    }
-#pragma unroll
-    for (int k = 0; k < kDpEpt; k++) {
-        const uint32_t l = threadIdx.x + k * kDpGroupThreads;
-        if (l < cnt) {
-            const uint32_t r = (uint32_t)en[k];
-            if (own[k] != r && !(ra[k] == oa[k] && rb[k] == ob[k] && rc[k] == oc[k])) {
-                // 32-bit key collision with a different signature: walk on
-                slot[k] = dp_insert<true>(L.word, kDpSlots, (uint32_t)(en[k] >> 32), r, dp_next(slot[k], kDpSlots, true),
-                                          A.sig, A.stride, own[k]);
-                if (own[k] != r)
-                    go[k] = gidx_of(A.out, A.sig, A.stride, GM, own[k]);
+    // (2) the listed entries confirm on the full 24 bytes -- one per thread
+    // for up to 512 of them, both rows' loads in flight together -- and fold
+    // into their class
+    const uint32_t nj = L.jl[kDpCap - 1];
+    for (uint32_t j = threadIdx.x; j < nj; j += NT) {
+        const uint32_t e = L.jl[j];
+        const uint32_t l = e & 0xFFFFu;
+        uint32_t own = e >> 16;
+        const uint32_t r = L.rec[l];
+        uint32_t o = L.rec[own];
+        uint64_t gl = r, go = o;
+        if constexpr (!(PROBE & 1)) {
+            uint64_t ra, rb, rcc, oa, ob, oc;
+            load_sig(A.sig + (uint64_t)r * A.stride, ra, rb, rcc);
+            load_sig(A.sig + (uint64_t)o * A.stride, oa, ob, oc);
+            if constexpr (GM != GM_INDEX) {
+                gl = gidx_of(A.out, A.sig, A.stride, GM, r);
+                go = gidx_of(A.out, A.sig, A.stride, GM, o);
             }
-            atomicAdd(&L.cn[slot[k]], 1u);
-            if (own[k] != r)
-                atomicMin(reinterpret_cast<unsigned long long *>(&L.mn[slot[k]]),
-                          (unsigned long long)(gr[k] < go[k] ? gr[k] : go[k]));
-        }
-    }
-    __syncthreads();
-#pragma unroll
-    for (int k = 0; k < kDpEpt; k++) {
-        const uint32_t l = threadIdx.x + k * kDpGroupThreads;
-        if (l < cnt) {
-            const uint32_t c = L.cn[slot[k]];
-            if (c > 1 && !(PROBE & 2)) {
-                const uint32_t r = (uint32_t)en[k];
-                const uint64_t m = L.mn[slot[k]];
-                // the class's first record keeps dp_tile's rep = r
-                A.out.store(r, m, c, GM != GM_INDEX || m != r);
+            if (!(ra == oa && rb == ob && rcc == oc)) {
+                // a key-bit collision with a different signature (rare):
+                // walk on from the slot it met -- the first slot with its
+                // key bits along its probe sequence, found again because
+                // every slot is set once -- confirming each equal key
+                const uint32_t key = (uint32_t)sig_hash(ra, rb, rcc), kb = key & kDpKeyMask;
+                uint32_t slot = dp_lprobe(L.word, kb, l, dp_home(key, kDpSlots), own);
+                for (;;) {
+                    slot = dp_lprobe(L.word, kb, l, dp_next(slot, kDpSlots), own);
+                    if (own == l)
+                        break;  // claimed a slot of its own
+                    o = L.rec[own];
+                    if (sig_equal(A.sig, A.stride, r, o))
+                        break;
+                }
+                go = GM == GM_INDEX ? (uint64_t)o : gidx_of(A.out, A.sig, A.stride, GM, o);
             }
         }
+        if (own != l) {
+            atomicAdd(&L.cn[own >> 1], 1u << (16 * (own & 1)));
+            dp_lds_min(&L.mn[own], gl < go ? gl : go);
+        }
+        L.jl[j] = l | own << 16;  // its class (itself if it claimed a slot)
     }
     __syncthreads();
+    // (3) answers of the records of multi-member classes
+    if constexpr (!(PROBE & 2)) {
+#pragma unroll
+        for (int k = 0; k < kDpEpt; k++) {
+            const uint32_t l = threadIdx.x + k * NT;
+            if ((claim >> k) & 1u) {
+                const uint32_t c = dp_cn(L.cn, l);
+                if (c > 1) {
+                    const uint64_t m = L.mn[l];
+                    // the class's first record keeps dp_tile's rep = r
+                    A.out.store(rc[k], m, c, GM != GM_INDEX || m != rc[k]);
+                }
+            }
+        }
+        for (uint32_t j = threadIdx.x; j < nj; j += NT) {
+            const uint32_t e = L.jl[j];
+            const uint32_t l = e & 0xFFFFu, own = e >> 16;
+            const uint32_t c = dp_cn(L.cn, own);
+            if (c > 1)
+                A.out.store(L.rec[l], L.mn[own], c, true);
+        }
+    }
+    __syncthreads();
+}
+
+// A partition's entries as key halves and records (kh, rc), entry k of this
+// thread at local index threadIdx.x + k * 512; loads clamped to the last
+// entry so that all of a thread's loads leave together.
+__device__ __forceinline__ void dp_split_entry(uint64_t en, uint32_t &kh, uint32_t &rc)
+{
+    kh = (uint32_t)(en >> 32);
+    rc = (uint32_t)en;
 }
 
 // A partition the pipeline did not gather: a bucket of more than kDpRuns
 // chunks (its runs come in batches), or more records than the LDS table
 // holds (grouped on a table in its own HBM region, 2 * cnt slots at
 // 2 * its virtual start).  Ends with a barrier.
-__device__ __forceinline__ void dp_group_slow(DpLds &L, uint32_t *rpos, uint64_t *rsrc, uint64_t *wsum,
-                                              const DpArgs &A, const DpRuns &R)
+template <int GM>
+__device__ __forceinline__ void dp_group_slow(DpLds<GM> &L, const DpArgs &A, const DpRuns &R)
 {
+    const DpRunTab T(L);
     uint32_t cnt = 0, below = 0;
     for (uint32_t kb = 0; kb < R.nch; kb += kDpRuns) {
         uint32_t s = 0, len = 0;
         if (kb + threadIdx.x < R.nch)
             R.run(kb + threadIdx.x, s, len);
         uint64_t t2;
-        block_exclusive_scan64((uint64_t)s << 32 | len, wsum, t2);
+        block_exclusive_scan64((uint64_t)s << 32 | len, T.wsum, t2);
         cnt += (uint32_t)t2;
         below += (uint32_t)(t2 >> 32);
     }
     if (cnt == 0)
         return;
     if (cnt <= kDpCap) {
-        uint64_t en[kDpEpt];
+        uint32_t kh[kDpEpt], rc[kDpEpt];
 #pragma unroll
         for (int k = 0; k < kDpEpt; k++)
-            en[k] = 0;
+            kh[k] = rc[k] = 0;
         for (uint32_t kb = 0, l0 = 0; kb < R.nch; kb += kDpRuns) {
             const uint32_t nk = (R.nch - kb) < (uint32_t)kDpRuns ? (R.nch - kb) : (uint32_t)kDpRuns;
-            const uint32_t l1 = l0 + (uint32_t)dp_batch(R, kb, l0, rpos, rsrc, wsum);
+            const uint32_t l1 = l0 + (uint32_t)dp_batch(R, kb, l0, T.rpos, T.rsrc, T.wsum);
 #pragma unroll
             for (int k = 0; k < kDpEpt; k++) {
                 const uint32_t l = threadIdx.x + k * kDpGroupThreads;
                 if (l >= l0 && l < l1)
-                    en[k] = A.ent2[dp_src(l, nk, rpos, rsrc)];
+                    dp_split_entry(A.ent2[dp_src(l, nk, T.rpos, T.rsrc)], kh[k], rc[k]);
             }
             __syncthreads();
             l0 = l1;
         }
-        if (A.gmode == GM_ROW)
-            dp_group_lds<0, GM_ROW>(L, A, en, cnt);
-        else if (A.gmode == GM_REP)
-            dp_group_lds<0, GM_REP>(L, A, en, cnt);
-        else
-            dp_group_lds<0, GM_INDEX>(L, A, en, cnt);
+        dp_group_lds<0, GM>(L, A, kh, rc, cnt);
         return;
     }
     const uint64_t vs = R.bs + below;
@@ -798,16 +885,16 @@ __device__ __forceinline__ void dp_group_slow(DpLds &L, uint32_t *rpos, uint64_t
     __syncthreads();
     for (uint32_t kb = 0, l0 = 0; kb < R.nch; kb += kDpRuns) {
         const uint32_t nk = (R.nch - kb) < (uint32_t)kDpRuns ? (R.nch - kb) : (uint32_t)kDpRuns;
-        const uint32_t l1 = l0 + (uint32_t)dp_batch(R, kb, l0, rpos, rsrc, wsum);
+        const uint32_t l1 = l0 + (uint32_t)dp_batch(R, kb, l0, T.rpos, T.rsrc, T.wsum);
         for (uint32_t l = l0 + threadIdx.x; l < l1; l += blockDim.x) {
-            const uint64_t en = A.ent2[dp_src(l, nk, rpos, rsrc)];
+            const uint64_t en = A.ent2[dp_src(l, nk, T.rpos, T.rsrc)];
             const uint32_t r = (uint32_t)en, key = (uint32_t)(en >> 32);
             uint32_t o;
-            const uint32_t slot = dp_insert<false>(w, size, key, r, dp_home(key, size, false), A.sig, A.stride, o);
+            const uint32_t slot = dp_insert(w, size, key, r, dp_home(key, size), A.sig, A.stride, o);
             atomicAdd(&c[slot], 1u);
             if (o != r) {
-                const uint64_t a = gidx_of(A.out, A.sig, A.stride, A.gmode, r);
-                const uint64_t b2 = gidx_of(A.out, A.sig, A.stride, A.gmode, o);
+                const uint64_t a = gidx_of(A.out, A.sig, A.stride, GM, r);
+                const uint64_t b2 = gidx_of(A.out, A.sig, A.stride, GM, o);
                 atomicMin(reinterpret_cast<unsigned long long *>(&m[slot]), (unsigned long long)(a < b2 ? a : b2));
             }
             A.gslot[vs + l] = slot;
@@ -819,11 +906,11 @@ __device__ __forceinline__ void dp_group_slow(DpLds &L, uint32_t *rpos, uint64_t
     __syncthreads();
     for (uint32_t kb = 0, l0 = 0; kb < R.nch; kb += kDpRuns) {
         const uint32_t nk = (R.nch - kb) < (uint32_t)kDpRuns ? (R.nch - kb) : (uint32_t)kDpRuns;
-        const uint32_t l1 = l0 + (uint32_t)dp_batch(R, kb, l0, rpos, rsrc, wsum);
+        const uint32_t l1 = l0 + (uint32_t)dp_batch(R, kb, l0, T.rpos, T.rsrc, T.wsum);
         for (uint32_t l = l0 + threadIdx.x; l < l1; l += blockDim.x) {
             const uint32_t slot = A.gslot[vs + l];
             if (c[slot] > 1) {
-                const uint32_t r = (uint32_t)A.ent2[dp_src(l, nk, rpos, rsrc)];
+                const uint32_t r = (uint32_t)A.ent2[dp_src(l, nk, T.rpos, T.rsrc)];
                 A.out.store(r, m[slot], c[slot], true);
             }
         }
@@ -832,11 +919,9 @@ __device__ __forceinline__ void dp_group_slow(DpLds &L, uint32_t *rpos, uint64_t
     }
 }
 
-// K5: one workgroup per partition.  The run table (rpos, rsrc) and the scan
-// partials live in the table's mn array until the table is initialised.  A
-// partition of a bucket with more than kDpRuns chunks (its runs come in
-// batches) or of more than kDpCap records (the HBM table) is listed for
-// dp_group_slow_kernel instead.
+// K5: one workgroup per partition.  A partition of a bucket with more than
+// kDpRuns chunks (its runs come in batches) or of more than kDpCap records
+// (the HBM table) is listed for dp_group_slow_kernel instead.
 static_assert(kDpRuns == kDpGroupThreads, "one run per thread in a batch");
 
 __device__ __forceinline__ void dp_runs_of(uint32_t q, int d2, uint64_t tiles, const uint64_t *off1,
@@ -853,16 +938,13 @@ __device__ __forceinline__ void dp_runs_of(uint32_t q, int d2, uint64_t tiles, c
 }
 
 template <int PROBE, int GM>
-__global__ __launch_bounds__(kDpGroupThreads) __attribute__((amdgpu_waves_per_eu(8))) void dp_group_kernel(
+__global__ __launch_bounds__(kDpGroupThreads) __attribute__((amdgpu_waves_per_eu(GM == GM_INDEX ? 8 : 6))) void dp_group_kernel(
     const uint64_t *__restrict__ ent2, int d2, uint64_t tiles, const uint64_t *__restrict__ off1,
     const uint32_t *__restrict__ cb, const uint16_t *__restrict__ cdo, const uint8_t *__restrict__ sig,
     uint32_t stride, DpOut out, uint32_t *__restrict__ slow)
 {
-    __shared__ DpLds L;
-    uint32_t *rpos = reinterpret_cast<uint32_t *>(L.mn);
-    uint64_t *rsrc = L.mn + kDpRuns / 2;
-    uint64_t *wsum = L.mn + kDpRuns / 2 + kDpRuns;
-    static_assert(kDpRuns / 2 + kDpRuns + kDpGroupThreads / 64 <= kDpSlots, "gather tables fit in mn");
+    __shared__ DpLds<GM> L;
+    const DpRunTab T(L);
     // XCD-aware order: workgroups are dealt to the 8 XCDs round-robin, so
     // XCD x takes a contiguous range of partitions; neighbouring digits of
     // one bucket share the lines of their runs (ent2) and of the chunks'
@@ -872,7 +954,7 @@ __global__ __launch_bounds__(kDpGroupThreads) __attribute__((amdgpu_waves_per_eu
     const uint32_t q = x < rem ? x * (per + 1) + i : rem * (per + 1) + (x - rem) * per + i;
     DpRuns R;
     dp_runs_of(q, d2, tiles, off1, cb, cdo, R);
-    const uint32_t cnt = R.nch > (uint32_t)kDpRuns ? ~0u : (uint32_t)dp_batch(R, 0, 0, rpos, rsrc, wsum);
+    const uint32_t cnt = R.nch > (uint32_t)kDpRuns ? ~0u : (uint32_t)dp_batch(R, 0, 0, T.rpos, T.rsrc, T.wsum);
     if (cnt == 0)
         return;
     if (cnt > kDpCap) {
@@ -880,34 +962,32 @@ __global__ __launch_bounds__(kDpGroupThreads) __attribute__((amdgpu_waves_per_eu
             slow[1 + atomicAdd(slow, 1u)] = q;
         return;
     }
-    uint64_t en[kDpEpt];
+    uint32_t kh[kDpEpt], rc[kDpEpt];
 #pragma unroll
     for (int k = 0; k < kDpEpt; k++) {
         const uint32_t l = threadIdx.x + k * kDpGroupThreads;
-        en[k] = l < cnt ? ent2[dp_src(l, R.nch, rpos, rsrc)] : 0ull;
+        dp_split_entry(ent2[dp_src(l < cnt ? l : cnt - 1, R.nch, T.rpos, T.rsrc)], kh[k], rc[k]);
     }
     __syncthreads();  // run table reads done before the table init
     const DpArgs A{ent2, sig, stride, GM, nullptr, nullptr, nullptr, nullptr, out};
-    dp_group_lds<PROBE, GM>(L, A, en, cnt);
+    dp_group_lds<PROBE, GM>(L, A, kh, rc, cnt);
 }
 
 // The listed partitions (slow[0] of them), a few persistent workgroups.
+template <int GM>
 __global__ __launch_bounds__(kDpGroupThreads) void dp_group_slow_kernel(
     const uint64_t *__restrict__ ent2, int d2, uint64_t tiles, const uint64_t *__restrict__ off1,
     const uint32_t *__restrict__ cb, const uint16_t *__restrict__ cdo, const uint8_t *__restrict__ sig,
-    uint32_t stride, int gmode, uint64_t *__restrict__ gword, uint64_t *__restrict__ gmin,
+    uint32_t stride, uint64_t *__restrict__ gword, uint64_t *__restrict__ gmin,
     uint32_t *__restrict__ gcnt, uint32_t *__restrict__ gslot, DpOut out, const uint32_t *__restrict__ slow)
 {
-    __shared__ DpLds L;
-    uint32_t *rpos = reinterpret_cast<uint32_t *>(L.mn);
-    uint64_t *rsrc = L.mn + kDpRuns / 2;
-    uint64_t *wsum = L.mn + kDpRuns / 2 + kDpRuns;
-    const DpArgs A{ent2, sig, stride, gmode, gword, gmin, gcnt, gslot, out};
+    __shared__ DpLds<GM> L;
+    const DpArgs A{ent2, sig, stride, GM, gword, gmin, gcnt, gslot, out};
     const uint32_t ns = slow[0];
     for (uint32_t i = blockIdx.x; i < ns; i += gridDim.x) {
         DpRuns R;
         dp_runs_of(slow[1 + i], d2, tiles, off1, cb, cdo, R);
-        dp_group_slow(L, rpos, rsrc, wsum, A, R);
+        dp_group_slow<GM>(L, A, R);
         __syncthreads();
     }
 }
@@ -1008,8 +1088,15 @@ hipError_t launch_dedup_group(const uint8_t *sig, uint32_t sig_stride, const uin
     else
         DP_GROUP(0, GM_INDEX);
 #undef DP_GROUP
-    dp_group_slow_kernel<<<256, kDpGroupThreads, 0, st>>>(ent2, pl.d2, pl.tiles, off1, cb, cdo, sig, sig_stride, gmode,
-                                                          gword, gmin, gcnt, gslot, out, slow);
+    if (gmode == GM_ROW)
+        dp_group_slow_kernel<GM_ROW><<<256, kDpGroupThreads, 0, st>>>(ent2, pl.d2, pl.tiles, off1, cb, cdo, sig,
+                                                                    sig_stride, gword, gmin, gcnt, gslot, out, slow);
+    else if (gmode == GM_REP)
+        dp_group_slow_kernel<GM_REP><<<256, kDpGroupThreads, 0, st>>>(ent2, pl.d2, pl.tiles, off1, cb, cdo, sig,
+                                                                    sig_stride, gword, gmin, gcnt, gslot, out, slow);
+    else
+        dp_group_slow_kernel<GM_INDEX><<<256, kDpGroupThreads, 0, st>>>(ent2, pl.d2, pl.tiles, off1, cb, cdo, sig,
+                                                                      sig_stride, gword, gmin, gcnt, gslot, out, slow);
     if (ev1)
         (void)hipEventRecord(ev1, st);
     return hipGetLastError();
