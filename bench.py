@@ -256,7 +256,7 @@ def load_traffic(config: str, kernel: str):
     return None, None
 
 
-SQ_KERNEL = {"c2": "sig_hash_kernel<true, 0, 0", "c3": "md5_stage_kernel<true"}  # name prefixes
+SQ_KERNEL = {"c2": "sig_hash_kernel<true, 0, 0", "c3": "md5_pair_kernel<true"}  # name prefixes
 
 
 def load_valu(config: str, avg_ms: float):

@@ -14,7 +14,7 @@ sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
 from pmc_summary import load  # noqa: E402
 
 BENCH_KERNEL = {"c2": ("sig_hash_kernel<true, 0, 0, false", "sig_hash_kernel<SAR>"),
-                "c3": ("md5_stage_kernel<true", "md5_stage_kernel<SAR>"),
+                "c3": ("md5_pair_kernel<true", "md5_pair_kernel<SAR>"),
                 "c4": ("crc_seg_kernel<true, 2>", "crc_seg_kernel<SAR,2>")}
 
 
