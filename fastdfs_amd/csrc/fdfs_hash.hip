@@ -144,7 +144,10 @@ __global__ __launch_bounds__(TM == 2 || MODE == 5 ? 1024 : kHashBlock) __attribu
     // SV vectors per step: 8 (one 128-byte line) or, probe MODE 6, 4 (half
     // a line: two 16-VGPR load sets instead of two of 32, and only B's last
     // four vectors in LDS)
-    constexpr int SV = MODE == 6 ? 4 : 8;
+    constexpr int SV = (MODE == 6 || MODE == 7) ? 4 : 8;
+    // register sets of loads in flight: MODE 7 (probe) = four 64-byte sets,
+    // the same 64 VGPRs as two 128-byte sets but 192 bytes of lookahead
+    constexpr int NSETS = MODE == 7 ? 4 : 2;
     constexpr uint32_t SB = 16 * SV;  // bytes per step
     __shared__ uint4 sB[2 * SV * 64];
     if constexpr (TM == 2)
@@ -334,7 +337,7 @@ __global__ __launch_bounds__(TM == 2 || MODE == 5 ? 1024 : kHashBlock) __attribu
         // register sets, asm loads (hipcc would sink plain loads to their
         // use), issued unconditionally (past-the-end steps read `safe`) so no
         // register an asm load is still writing is ever copied.
-        u32x4 RA[SV], RB[SV];
+        u32x4 RS[NSETS][SV];
         auto issue = [&](u32x4 (&R)[SV], uint32_t stp) {
             const uint8_t *ln = (MODE != 2 && stp < nsteps) ? reinterpret_cast<const uint8_t *>(w + SV * (uint64_t)stp) : safe;
 #pragma unroll
@@ -365,25 +368,46 @@ __global__ __launch_bounds__(TM == 2 || MODE == 5 ? 1024 : kHashBlock) __attribu
             ld(3, QBC(3));
 #undef QBC
         };
-        auto wait_older = [&](u32x4 (&R)[SV]) {  // R is the older of the two sets in flight
+        // R is the oldest of the NSETS sets in flight
+        auto wait_older = [&](u32x4 (&R)[SV]) {
             if constexpr (SV == 8) {
+                static_assert(NSETS == 2, "128-byte steps: two sets");
                 asm volatile("s_waitcnt vmcnt(8)" : "+v"(R[0]), "+v"(R[1]), "+v"(R[2]), "+v"(R[3]) :: "memory");
                 asm volatile("" : "+v"(R[4]), "+v"(R[5]), "+v"(R[6]), "+v"(R[7]));
+            } else if constexpr (NSETS == 4) {
+                asm volatile("s_waitcnt vmcnt(12)" : "+v"(R[0]), "+v"(R[1]), "+v"(R[2]), "+v"(R[3]) :: "memory");
             } else {
                 asm volatile("s_waitcnt vmcnt(4)" : "+v"(R[0]), "+v"(R[1]), "+v"(R[2]), "+v"(R[3]) :: "memory");
             }
         };
         auto drain = [&]() {
-            if constexpr (SV == 8) {
-                asm volatile("s_waitcnt vmcnt(0)"
-                             : "+v"(RA[0]), "+v"(RA[1]), "+v"(RA[2]), "+v"(RA[3]), "+v"(RA[4]), "+v"(RA[5]),
-                               "+v"(RA[6]), "+v"(RA[7]) :: "memory");
-                asm volatile("" : "+v"(RB[0]), "+v"(RB[1]), "+v"(RB[2]), "+v"(RB[3]), "+v"(RB[4]), "+v"(RB[5]),
-                                  "+v"(RB[6]), "+v"(RB[7]));
-            } else {
-                asm volatile("s_waitcnt vmcnt(0)" : "+v"(RA[0]), "+v"(RA[1]), "+v"(RA[2]), "+v"(RA[3]) :: "memory");
-                asm volatile("" : "+v"(RB[0]), "+v"(RB[1]), "+v"(RB[2]), "+v"(RB[3]));
+#pragma unroll
+            for (int k = 0; k < NSETS; k++) {
+                if constexpr (SV == 8) {
+                    asm volatile("s_waitcnt vmcnt(0)"
+                                 : "+v"(RS[k][0]), "+v"(RS[k][1]), "+v"(RS[k][2]), "+v"(RS[k][3]), "+v"(RS[k][4]),
+                                   "+v"(RS[k][5]), "+v"(RS[k][6]), "+v"(RS[k][7]) :: "memory");
+                } else {
+                    asm volatile("s_waitcnt vmcnt(0)" : "+v"(RS[k][0]), "+v"(RS[k][1]), "+v"(RS[k][2]), "+v"(RS[k][3]) :: "memory");
+                }
             }
+        };
+        // Steps [first, end) with NSETS - 1 steps' loads ahead of the one
+        // hashed (past-the-end steps load `safe`).
+        auto pipeline = [&](auto &&iss_fn, auto &&step_fn, uint32_t first, uint32_t end) {
+#pragma unroll
+            for (int k = 0; k < NSETS - 1; k++)
+                iss_fn(RS[k], first + k);
+            for (uint32_t st = first; st < end; st += NSETS) {
+#pragma unroll
+                for (int k = 0; k < NSETS; k++) {
+                    iss_fn(RS[(k + NSETS - 1) % NSETS], st + k + NSETS - 1);
+                    wait_older(RS[k]);
+                    if (k == 0 || st + k < end)
+                        step_fn(RS[k], st + k < nsteps);
+                }
+            }
+            drain();
         };
         // Small lanes only ever end, so the steps where a lane below big_min
         // is still hashing are a prefix [0, nfull) of the wave's steps.  The
@@ -402,18 +426,13 @@ __global__ __launch_bounds__(TM == 2 || MODE == 5 ? 1024 : kHashBlock) __attribu
                 else
                     issue(R, stp);
             };
-            iss(RA, 0);
-            for (uint32_t st = 0; st < nfull; st += 2) {
-                iss(RB, st + 1);
-                wait_older(RA);
-                step(RA, st < nsteps);
-                iss(RA, st + 2);
-                wait_older(RB);
-                if (st + 1 < nfull)
-                    step(RB, st + 1 < nsteps);
-            }
-            drain();
+            pipeline(iss, step, 0u, nfull);
         }
+        // The rest of the steps (waves of big files: ELF alone, its
+        // dependent chain the bound).  Four 64-byte load sets here (192 B of
+        // lookahead in the same registers) measured 906-962 against 826-940
+        // ms on config 1, within that config's run-to-run spread
+        // (profiles/r03/hash_pipeline_ab.txt): not kept.
         auto step_chain = [&](u32x4 (&a)[SV], bool ok) {
             if (MODE == 1 || !ok)
                 return;
@@ -425,19 +444,8 @@ __global__ __launch_bounds__(TM == 2 || MODE == 5 ? 1024 : kHashBlock) __attribu
                 elf_word4_chain<SAR, true>(a[q][3], e);
             }
         };
-        if (nfull < nmax) {
-            issue(RA, nfull);
-            for (uint32_t st = nfull; st < nmax; st += 2) {
-                issue(RB, st + 1);
-                wait_older(RA);
-                step_chain(RA, st < nsteps);
-                issue(RA, st + 2);
-                wait_older(RB);
-                if (st + 1 < nmax)
-                    step_chain(RB, st + 1 < nsteps);
-            }
-            drain();
-        }
+        if (nfull < nmax)
+            pipeline(issue, step_chain, nfull, nmax);
         // planes -> value: sum_j P_j << 8j over the lane quad (j = lane & 3),
         // then back to the file's lane; undo the padded steps (M^-SB each)
         uint32_t s31 = 0, s33 = 0;
@@ -590,7 +598,8 @@ hipError_t launch_sig_hash(bool sar, const uint8_t *base, const uint64_t *offs,
     // measurement build only (make probes): FDFS_GPU_HASH_MODE 1 = loads
     // only, 2 = compute only (wrong results), 3 = CRC lookups / ELF / CRC
     // XOR tree in that order, 4 = ELF in the 3-op chain form, 5 = production
-    // code in 1024-thread workgroups; FDFS_GPU_HASH_TM CRC table form
+    // code in 1024-thread workgroups, 6 = 64-byte steps, 7 = 64-byte steps
+    // with four load sets in flight; FDFS_GPU_HASH_TM CRC table form
     // 0 = slice-by-16 bytes, 2 = rotated rep8
     static int mode = -1;
     if (mode < 0) {
@@ -660,6 +669,8 @@ hipError_t launch_sig_hash(bool sar, const uint8_t *base, const uint64_t *offs,
         HASH_LAUNCH(true, 5);
     else if (mode == 6)  // 64-byte steps: two 16-VGPR load sets
         HASH_LAUNCH(true, 6);
+    else if (mode == 7)  // 64-byte steps: four 16-VGPR load sets (192 bytes ahead)
+        HASH_LAUNCH(true, 7);
     else
 #endif
     if (sar)
