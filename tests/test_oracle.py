@@ -83,6 +83,25 @@ def test_chunking_invariance(oracle, variant):
         assert oracle.dio_file(d, oracle.METHOD_MD5, variant, chunk=chunk) == m
 
 
+@pytest.mark.parametrize("variant", [0, 1])
+def test_crc_split_identity(oracle, variant):
+    """What the segmented kernels and md5_pair_kernel's two-chain CRC rely
+    on: CRC32_ex (storage/storage_dio.c:467) is linear in (state, data) for
+    both shift variants, so crc(c, A || B) = M^|B| crc(c, A) ^ crc(0, B), with
+    M^n x = crc(x, n zero bytes) (the zero-data CRC from state 0 is 0)."""
+    rng = np.random.default_rng(11 + variant)
+    zeros = np.zeros(4096, np.uint8)
+    for _ in range(200):
+        la, lb = (int(x) for x in rng.integers(0, 300, 2))
+        a = rng.integers(0, 256, la, dtype=np.uint8)
+        b = rng.integers(0, 256, lb, dtype=np.uint8)
+        c = int(rng.integers(-2**31, 2**31))
+        whole = oracle.crc32_ex(np.concatenate([a, b]), c, variant)
+        adv = oracle.crc32_ex(zeros[:lb], oracle.crc32_ex(a, c, variant), variant)
+        assert whole == adv ^ oracle.crc32_ex(b, 0, variant)
+    assert oracle.crc32_ex(zeros, 0, variant) == 0
+
+
 def test_sig_pack_layout(oracle):
     """STORAGE_GEN_FILE_SIGNATURE: be64 size, then be32 x4 (hash) / raw md5."""
     d = np.frombuffer(b"hello fastdfs", dtype=np.uint8)
