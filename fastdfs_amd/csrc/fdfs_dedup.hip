@@ -816,8 +816,13 @@ __device__ __forceinline__ void dp_group_lds(DpLds<GM> &L, const DpArgs &A, cons
             const uint32_t e = L.jl[j];
             const uint32_t l = e & 0xFFFFu, own = e >> 16;
             const uint32_t c = dp_cn(L.cn, own);
-            if (c > 1)
-                A.out.store(L.rec[l], L.mn[own], c, true);
+            if (c > 1) {
+                const uint32_t r = L.rec[l];
+                const uint64_t m = L.mn[own];
+                // with no gidx a listed entry may be its class's first record
+                // too (the claimer is whichever entry probed first)
+                A.out.store(r, m, c, GM != GM_INDEX || m != r);
+            }
         }
     }
     __syncthreads();
