@@ -26,4 +26,6 @@ for label, (data, o, s) in (("aliased", (buf, offs_t, sizes_t)),):
         ctx.sig_batch(data, o, s, method=F.SIG_MD5)
     torch.cuda.synchronize()
     ms, k = ctx.read_timing(_lib.KERNEL_SIG_LANE)
-    print(f"{label}: md5_stage_kernel {ms / k:.2f} ms over {int(sizes.sum()) / 1e9:.1f} GB", flush=True)
+    print(f"{label}: MD5 lane kernel {ms / k:.2f} ms over {int(sizes.sum()) / 1e9:.1f} GB "
+          f"(FDFS_GPU_PROBE_LIB={os.environ.get('FDFS_GPU_PROBE_LIB', '')} "
+          f"FDFS_GPU_MD5_PAIR={os.environ.get('FDFS_GPU_MD5_PAIR', '')})", flush=True)
