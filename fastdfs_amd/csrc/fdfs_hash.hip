@@ -421,10 +421,16 @@ __global__ __launch_bounds__(TM == 2 || MODE == 5 ? 1024 : kHashBlock) __attribu
         }
         if (nfull) {
             auto iss = [&](u32x4 (&R)[SV], uint32_t stp) {
+                // probe MODE 8: the step's loads issued at raised wave
+                // priority, so they leave ahead of the other waves' VALU
+                if constexpr (MODE == 8)
+                    __builtin_amdgcn_s_setprio(2);
                 if constexpr (QL)
                     issue_q(R, stp);
                 else
                     issue(R, stp);
+                if constexpr (MODE == 8)
+                    __builtin_amdgcn_s_setprio(0);
             };
             pipeline(iss, step, 0u, nfull);
         }
@@ -599,7 +605,8 @@ hipError_t launch_sig_hash(bool sar, const uint8_t *base, const uint64_t *offs,
     // only, 2 = compute only (wrong results), 3 = CRC lookups / ELF / CRC
     // XOR tree in that order, 4 = ELF in the 3-op chain form, 5 = production
     // code in 1024-thread workgroups, 6 = 64-byte steps, 7 = 64-byte steps
-    // with four load sets in flight; FDFS_GPU_HASH_TM CRC table form
+    // with four load sets in flight, 8 = loads issued at raised priority;
+    // FDFS_GPU_HASH_TM CRC table form
     // 0 = slice-by-16 bytes, 2 = rotated rep8
     static int mode = -1;
     if (mode < 0) {
@@ -671,6 +678,8 @@ hipError_t launch_sig_hash(bool sar, const uint8_t *base, const uint64_t *offs,
         HASH_LAUNCH(true, 6);
     else if (mode == 7)  // 64-byte steps: four 16-VGPR load sets (192 bytes ahead)
         HASH_LAUNCH(true, 7);
+    else if (mode == 8)  // the step's loads issued at s_setprio 2
+        HASH_LAUNCH(true, 8);
     else
 #endif
     if (sar)
