@@ -459,13 +459,27 @@ __global__ __launch_bounds__(128) void md5_pair_kernel(
             for (uint64_t r = 0; r < rounds; r++) {
                 pair_barrier();
                 const uint4 *q = reinterpret_cast<const uint4 *>(mine + (r & 1) * (64 * STRIDE));
+                // block b + 1's words are read from LDS (for every lane,
+                // outside the per-lane branch) while block b is compressed
+                uint4 cur[4] = {q[0], q[1], q[2], q[3]};
 #pragma unroll
                 for (int b = 0; b < BPR; b++) {
+                    uint4 nxt[4];
+                    if (b + 1 < BPR) {
+#pragma unroll
+                        for (int k = 0; k < 4; k++)
+                            nxt[k] = q[4 * (b + 1) + k];
+                    }
                     if (r * BPR + b < nblk && pmode != 3) {
-                        const uint4 a0 = q[4 * b], a1 = q[4 * b + 1], a2 = q[4 * b + 2], a3 = q[4 * b + 3];
-                        const uint32_t m[16] = {a0.x, a0.y, a0.z, a0.w, a1.x, a1.y, a1.z, a1.w,
-                                                a2.x, a2.y, a2.z, a2.w, a3.x, a3.y, a3.z, a3.w};
+                        const uint32_t m[16] = {cur[0].x, cur[0].y, cur[0].z, cur[0].w, cur[1].x, cur[1].y,
+                                                cur[1].z, cur[1].w, cur[2].x, cur[2].y, cur[2].z, cur[2].w,
+                                                cur[3].x, cur[3].y, cur[3].z, cur[3].w};
                         md5_compress(st, m);
+                    }
+                    if (b + 1 < BPR) {
+#pragma unroll
+                        for (int k = 0; k < 4; k++)
+                            cur[k] = nxt[k];
                     }
                 }
             }

@@ -20,7 +20,7 @@ __device__ __forceinline__ uint32_t rotl(uint32_t x, int s)
 
 #define MD5_F(b, c, d) ((d) ^ ((b) & ((c) ^ (d))))
 #define MD5_G(b, c, d) ((c) ^ ((d) & ((b) ^ (c))))
-#define MD5_H(b, c, d) ((b) ^ (c) ^ (d))
+#define MD5_H(b, c, d) __builtin_amdgcn_bitop3_b32((b), (c), (d), 0x96)  // one op, not two v_xor
 #define MD5_I(b, c, d) ((c) ^ ((b) | ~(d)))
 // The step's critical path is F -> add -> rotate -> add.  a, m and k are
 // known steps ahead, so (a + m + k) is summed off the path and the on-path
