@@ -340,7 +340,9 @@ __global__ __launch_bounds__(128) void md5_pair_kernel(
     int pmode, uint32_t *__restrict__ crc_out, uint8_t *__restrict__ sig_out, int32_t *__restrict__ codes_out)
 {
     // pmode (probe build only; 0 in production): 1 = MD5 wave at s_setprio
-    // 2, 2 = no CRC arithmetic, 3 = no MD5 arithmetic (wrong results)
+    // 2, 2 = no CRC arithmetic, 3 = no MD5 arithmetic (wrong results), 4 =
+    // both waves at s_setprio 2 while their chunk is among the largest
+    // quarter (the chunks that end the batch), 0 after
     constexpr int CH = kMd5Chunk;
     constexpr int PIECES = CH / 16;
     constexpr int FPI = 64 / PIECES;
@@ -373,6 +375,12 @@ __global__ __launch_bounds__(128) void md5_pair_kernel(
         __syncthreads();  // s_chunk read by both waves before the next chunk's write
         if (chunk >= nw)
             break;
+        if (pmode == 4) {
+            if (chunk < nw / 4)
+                __builtin_amdgcn_s_setprio(2);
+            else
+                __builtin_amdgcn_s_setprio(0);
+        }
         const uint32_t i = chunk * 64 + lane;
         bool valid = i < n;
         uint32_t f = valid ? order[i] : 0;
