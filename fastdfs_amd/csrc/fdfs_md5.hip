@@ -375,12 +375,14 @@ __global__ __launch_bounds__(128) void md5_pair_kernel(
         __syncthreads();  // s_chunk read by both waves before the next chunk's write
         if (chunk >= nw)
             break;
+#ifdef FDFS_PROBES
         if (pmode == 4) {
             if (chunk < nw / 4)
                 __builtin_amdgcn_s_setprio(2);
             else
                 __builtin_amdgcn_s_setprio(0);
         }
+#endif
         const uint32_t i = chunk * 64 + lane;
         bool valid = i < n;
         uint32_t f = valid ? order[i] : 0;
