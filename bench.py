@@ -346,10 +346,11 @@ def rccl_exchange_check(ctx, world, rank, dev):
     fdfs_gpu_dedup_global gives every rank the same answers as the
     torch.distributed form of the exchange on a seeded 200K-record set with
     duplicates across ranks.  All ranks share their outcome (mismatching
-    records per rank, all-gathered) before the timed run; a failure or a
-    mismatch anywhere is printed on stderr by rank 0 with the rank and record
-    counts, recorded in the line, and the run then uses the torch.distributed
-    exchange.  Returns (Comm or None, the check's record for the JSON line)."""
+    records per rank, all-gathered) before the timed run.  A failure or a
+    mismatch anywhere is printed on stderr by rank 0 with the ranks and
+    record counts, and every rank then exits non-zero: a multi-GPU line is
+    fdfs_gpu_dedup_global's or none (no silent fallback to another
+    transport).  Returns (Comm, the check's record for the JSON line)."""
     from fastdfs_amd.api import Comm
     comm, why, bad, mine = None, "ok", 0, 0
     try:
@@ -383,10 +384,11 @@ def rccl_exchange_check(ctx, world, rank, dev):
     failed = {r: ("error" if b < 0 else f"{b} of {m} records differ") for r, (b, m) in enumerate(per_rank) if b}
     if rank == 0:
         print("=" * 72 + "\nERROR: fdfs_gpu_dedup_global (RCCL) disagrees with the torch.distributed "
-              f"exchange: {failed} (this rank: {why}).\nThe timed run below uses the torch.distributed "
-              "exchange; its line records this check.\n" + "=" * 72, file=sys.stderr, flush=True)
-    return None, {"records": 200_000, "vs_torch_exchange": "FAILED", "failed_ranks": failed,
-                  "rank0": why}
+              f"exchange: {failed} (rank 0: {why}).\nNo line is printed: the multi-GPU dedup must be "
+              "libfdfs_gpu's.\n" + "=" * 72, file=sys.stderr, flush=True)
+    ctx.close()
+    dist.destroy_process_group()
+    sys.exit(3)
 
 
 def main():
@@ -473,9 +475,10 @@ def main():
                 "algorithmic_bytes_per_launch": nbytes}
         if tsrc:
             roof["traffic_source"] = tsrc
-        if args.config in ("c1", "c3") and method != F.SIG_CRC_ONLY:
+        if args.config in ("c1", "c3", "c4") and method != F.SIG_CRC_ONLY:
             # lane-per-file batches whose largest file's dependent chain (MD5
-            # / ELFHash) outlasts the HBM stream: the roof is that chain
+            # / ELFHash) outlasts the HBM stream: the roof is that chain (c4
+            # with --method hash / md5: 1 GiB files, one lane each)
             fms, fbytes = chain_floor_ms(ctx, data, offs_t, sizes_t, sizes, method, kernel)
             roof.update({"bound": "md5_chain" if method == F.SIG_MD5 else "elf_chain",
                          "peak": round(per_launch / (fms * 1e-3) / 1e9, 1),
@@ -484,7 +487,7 @@ def main():
                          "note": "peak = batch bytes over the time the same kernel takes for the "
                                  "largest file on the path it takes in the batch (one lane's serial "
                                  "chain; the other files of that timing batch are empty)"})
-            if method == F.SIG_MD5:
+            if method == F.SIG_MD5 and args.config != "c4":
                 ams, _ = chain_floor_ms(ctx, data, offs_t, sizes_t, sizes, method, kernel, alone=True)
                 roof["md5_alone_floor_ms"] = round(ams, 3)
                 roof["md5_alone_note"] = ("the largest file as a one-file batch: its CRC moves to the "

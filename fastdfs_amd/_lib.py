@@ -48,6 +48,7 @@ EXPORTS = (
     "fdfs_gpu_sig_batch_host",
     "fdfs_gpu_scrub",
     "fdfs_gpu_last_error",
+    "fdfs_gpu_inject_error",
     "fdfs_gpu_state_init",
     "fdfs_gpu_update_batch",
     "fdfs_gpu_final_batch",
@@ -153,6 +154,8 @@ def load() -> ctypes.CDLL:
     L.fdfs_gpu_scrub.argtypes = [vp, ctypes.POINTER(FdfsGpuBatch), vp, vp, vp, vp, vp]
     L.fdfs_gpu_last_error.restype = ctypes.c_char_p
     L.fdfs_gpu_last_error.argtypes = [vp]
+    L.fdfs_gpu_inject_error.restype = i32
+    L.fdfs_gpu_inject_error.argtypes = [vp, vp]
     L.fdfs_gpu_state_init.restype = i32
     L.fdfs_gpu_state_init.argtypes = [vp, vp, u32, vp]
     L.fdfs_gpu_update_batch.restype = i32

@@ -126,6 +126,11 @@ class Context:
                  "fdfs_gpu_read_timing")
         return ms.value, cnt.value
 
+    def inject_error(self, stream=None):
+        """Test hook (fdfs_gpu_inject_error): queue a lane-path error on
+        `stream`; a later call of this context fails with EIO once."""
+        self._rc(self._L.fdfs_gpu_inject_error(self._h, _stream_handle(stream)), "fdfs_gpu_inject_error")
+
     def reserve(self, max_files: int, max_records: int = 0):
         self._rc(self._L.fdfs_gpu_reserve(self._h, max_files, max_records), "fdfs_gpu_reserve")
 

@@ -23,6 +23,8 @@ struct fdfs_gpu_ctx {
     fdfs::DevTables *d_tabs = nullptr;
     unsigned seg_grid = 0;
     uint32_t lat_files = 0;  // lane batches up to one wave per SIMD (BigCrcWs::lat_files)
+    uint32_t ncu = 0;        // the device's CU count, read once at open (BigCrcWs::ncu)
+    uint64_t lane_err_seen = 0;  // lane-path error count already reported (lane_err_check)
     // the segmented passes' stream when they run beside the lane kernel
     // (BigCrcWs::side) and its fork / join events
     hipStream_t side = nullptr;
@@ -123,6 +125,7 @@ fdfs::BigCrcWs carve_big(const fdfs_gpu_ctx *ctx, Carve &cv, uint32_t n)
     big.poly = cv.take<uint32_t>(2 * (size_t)n);
     big.big_min = cv.take<uint64_t>(1);
     big.lat_files = ctx->lat_files;
+    big.ncu = ctx->ncu;
 #ifdef FDFS_PROBES
     // measurement build only: FDFS_GPU_LAT_FILES overrides (0 = always kBigCrcMin)
     static long lf = -2;
@@ -190,29 +193,35 @@ struct WsScope {
     ~WsScope() { ws_leave(ctx, st); }
 };
 
-// The lane path's device error word (fdfs::kLaneErrWord) reaches the host
-// through a pinned word: copied after every lane launch, checked at the
-// start of the context's next call, which then fails with EIO.
-uint32_t *lane_err_host(fdfs_gpu_ctx *ctx)
-{
-    return reinterpret_cast<uint32_t *>(ctx->hann + 64 * kAnnTail + 64 * kAnnMax + 2);
-}
+// The lane path's device error word (fdfs::kLaneErrWord, zeroed with the
+// histogram at every launch) feeds a per-context error COUNT: after each lane
+// launch a one-thread kernel adds 1 to a device counter when the launch's
+// word is set, and the counter is copied to a pinned host word.  The count
+// only grows, so a later launch's copy can never erase an earlier launch's
+// error (a copy of the per-launch word itself could: two calls queued back
+// to back, the second's 0 landing after the first's 1).  The context's next
+// call whose check sees a count above the last one it reported fails with
+// EIO.  Device word: dann[kAnnErrCount]; host copy: hann[kHannErrCount].
+constexpr size_t kAnnErrCount = kAnnMax + 64 * kAnnMax + 6;
+constexpr size_t kHannErrCount = 64 * kAnnTail + 64 * kAnnMax + 2;
 
 hipError_t lane_err_note(fdfs_gpu_ctx *ctx, const uint32_t *hist, hipStream_t st)
 {
-    return hipMemcpyAsync(lane_err_host(ctx), hist + fdfs::kLaneErrWord, 4, hipMemcpyDeviceToHost, st);
+    hipError_t e = fdfs::launch_lane_err_count(hist ? hist + fdfs::kLaneErrWord : nullptr, ctx->dann + kAnnErrCount, st);
+    if (e == hipSuccess)
+        e = hipMemcpyAsync(ctx->hann + kHannErrCount, ctx->dann + kAnnErrCount, 8, hipMemcpyDeviceToHost, st);
+    return e;
 }
 
 int lane_err_check(fdfs_gpu_ctx *ctx)
 {
-    volatile uint32_t *h = lane_err_host(ctx);
-    const uint32_t v = *h;
-    if (!v)
+    const uint64_t v = __atomic_load_n(ctx->hann + kHannErrCount, __ATOMIC_ACQUIRE);
+    if (v <= ctx->lane_err_seen)
         return 0;
-    *h = 0;
+    ctx->lane_err_seen = v;
     std::snprintf(ctx->err, sizeof(ctx->err),
                   "an earlier signature call on this context found its size binning inconsistent "
-                  "(device error word 0x%x): its outputs are invalid", v);
+                  "(%llu launch(es) so far): its outputs are invalid", (unsigned long long)v);
     return EIO;
 }
 
@@ -358,6 +367,10 @@ int fdfs_gpu_open(int device, unsigned flags, fdfs_gpu_ctx **out)
         e = hipMalloc(reinterpret_cast<void **>(&ctx->dann), 8 * kAnnDevWords);
     if (e == hipSuccess)
         e = hipHostMalloc(reinterpret_cast<void **>(&ctx->hann), 8 * kAnnHostWords, 0);
+    if (e == hipSuccess)
+        e = hipMemset(ctx->dann, 0, 8 * kAnnDevWords);
+    if (e == hipSuccess)
+        std::memset(ctx->hann, 0, 8 * kAnnHostWords);
     delete h;
     if (e != hipSuccess) {
         if (ctx->d_tabs)
@@ -383,6 +396,11 @@ int fdfs_gpu_open(int device, unsigned flags, fdfs_gpu_ctx **out)
         ncu = prop.multiProcessorCount;
     ctx->seg_grid = (unsigned)(ncu * fdfs::crc_seg_blocks_per_cu());
     ctx->lat_files = (uint32_t)ncu * 4 * 64;
+    ctx->ncu = (uint32_t)ncu;
+    if ((e = hipDeviceSynchronize()) != hipSuccess) {  // the zeroed words above
+        fdfs_gpu_close(ctx);
+        return EIO;
+    }
     *out = ctx;
     return 0;
 }
@@ -434,6 +452,18 @@ int fdfs_gpu_reserve(fdfs_gpu_ctx *ctx, uint64_t max_files, uint64_t max_records
 }
 
 const char *fdfs_gpu_last_error(fdfs_gpu_ctx *ctx) { return ctx ? ctx->err : "null context"; }
+
+int fdfs_gpu_inject_error(fdfs_gpu_ctx *ctx, void *stream)
+{
+    if (!ctx)
+        return EINVAL;
+    std::lock_guard<std::recursive_mutex> lk(ctx->mu);
+    DeviceGuard g(ctx->device);
+    if (!g.ok)
+        return ENODEV;
+    const hipError_t e = lane_err_note(ctx, nullptr, reinterpret_cast<hipStream_t>(stream));
+    return e == hipSuccess ? 0 : fail(ctx, e, "inject_error");
+}
 
 int fdfs_gpu_set_timing(fdfs_gpu_ctx *ctx, int enable)
 {
@@ -554,6 +584,9 @@ static int update_batch(fdfs_gpu_ctx *ctx, const fdfs_gpu_batch *chunks, const u
     if (!chunks->base || !chunks->offset || !chunks->size || !states)
         return EINVAL;
     if (reinterpret_cast<uintptr_t>(states) & 15)
+        return EINVAL;
+    // the duplicate check's open-addressing table holds 2n slots, at most 2^31
+    if (check && state_idx && n > (1u << 30))
         return EINVAL;
     std::lock_guard<std::recursive_mutex> lk(ctx->mu);
     if (int rc0 = lane_err_check(ctx))
@@ -859,9 +892,12 @@ static int dedup_common(fdfs_gpu_ctx *ctx, const uint8_t *sig, uint32_t stride,
         return 0;
     if (!sig || !rep_out || n >= 0xFFFFFFFFull)  // ref_out == nullptr: packed answers at rep_out
         return EINVAL;
-    // records are read as u64 words, rep written as u64
+    // records are read as u64 words, rep written as u64; packed answers are
+    // written as one 16-byte store each
     if ((reinterpret_cast<uintptr_t>(sig) | reinterpret_cast<uintptr_t>(gidx) |
          reinterpret_cast<uintptr_t>(rep_out)) & 7)
+        return EINVAL;
+    if (!ref_out && (reinterpret_cast<uintptr_t>(rep_out) & 15))
         return EINVAL;
     std::lock_guard<std::recursive_mutex> lk(ctx->mu);
     if (int rc0 = lane_err_check(ctx))
@@ -1468,6 +1504,15 @@ int fdfs_gpu_dedup_global(fdfs_gpu_ctx *ctx, void *comm, const uint8_t *sig, con
     hipStream_t st = reinterpret_cast<hipStream_t>(stream);
     // A local error is announced, not returned: every rank takes part in the
     // all-gather and all of them return it together.
+    // It synchronises on the announcements, so it cannot be captured.  Inside
+    // a capture no collective would execute (not even one announcing the
+    // error: it would only be recorded), so a capturing rank returns EINVAL
+    // at once, before any collective is enqueued; that every rank calls
+    // outside a capture is the caller's contract (include/fdfs_gpu.h).
+    if (capturing(st)) {
+        std::snprintf(ctx->err, sizeof(ctx->err), "dedup_global synchronises; not capturable");
+        return EINVAL;
+    }
     int err = dg_check(sig, gidx, n, rep_out, ref_out, nranks);
     if (!err)
         err = ensure_buf(ctx, &ctx->xa, &ctx->xa_bytes, dg_a_bytes(n), st);
@@ -1725,9 +1770,14 @@ int fdfs_gpu_crc_batch_global(fdfs_gpu_ctx *ctx, void *comm, const fdfs_gpu_batc
     if (!g.ok)
         return ENODEV;
     hipStream_t st = reinterpret_cast<hipStream_t>(stream);
-    // as in dedup_global, a local error is announced, not returned, so that
-    // no rank waits alone in a collective
-    int err = capturing(st) ? EINVAL : cg_check(pieces, piece_file, piece_start, file_size, nfiles, crc_out);
+    // as in dedup_global: not capturable (EINVAL before any collective), and
+    // a local error is announced, not returned, so that no rank waits alone
+    // in a collective
+    if (capturing(st)) {
+        std::snprintf(ctx->err, sizeof(ctx->err), "crc_batch_global synchronises; not capturable");
+        return EINVAL;
+    }
+    int err = cg_check(pieces, piece_file, piece_start, file_size, nfiles, crc_out);
     const uint64_t bb = fdfs::CrcParts::block_bytes(nfiles);
     if (!err)
         err = ensure_buf(ctx, &ctx->xa, &ctx->xa_bytes, bb * nranks, st);

@@ -17,7 +17,8 @@ constexpr int kLaneWsDwords = 2 * kSizeBins + 64;  // size-bin histogram + curso
 // the size binning placed a file outside [0, n) or read a file index >= n
 // (a histogram that was not zero before counting); such files are skipped,
 // never read or written out of bounds.  The API copies it to the host after
-// the launch and fails the context's next call with EIO.
+// the launch and fails the context's next call with EIO (through a
+// per-context error count that only grows, fdfs_api.cpp lane_err_note).
 constexpr int kLaneErrWord = 2 * kSizeBins + 32;
 
 // signature path (fdfs_sig.hip)
@@ -25,6 +26,8 @@ uint64_t scan_workspace_elems(uint64_t n);
 // Zero n dwords on st with a kernel (ordered like any kernel node when the
 // sequence is captured in a hipGraph; see zero_u32_kernel).
 hipError_t launch_zero_u32(void *p, uint64_t ndwords, hipStream_t st);
+// count += 1 if *word != 0 (word == nullptr: unconditionally), one thread.
+hipError_t launch_lane_err_count(const uint32_t *word, uint64_t *count, hipStream_t st);
 hipError_t launch_exclusive_scan(const uint64_t *in, uint64_t n, uint64_t *out, uint64_t *bsum,
                                  hipStream_t st);
 // Lane paths: files of at least a threshold T get their CRC (and for HASH
@@ -42,6 +45,7 @@ struct BigCrcWs {  // device arrays of n entries (seg_first n + 1)
     uint32_t *poly;      // [2n]: simple_hash, Time33 per big file
     uint64_t *big_min;   // [1]: the T big_plan_kernel chose (read by the lane kernel)
     uint32_t lat_files;  // host: batches up to this many files choose T adaptively (0: never)
+    uint32_t ncu = 0;    // host: the context device's CU count (fdfs_gpu_open), sizes persistent grids
     uint32_t md5_bin = 0;  // MD5 batches above lat_files: T = the lower bound of this size bin (0: no offload)
     // side != nullptr: the segmented kernels run on `side`, concurrently with
     // the lane kernel (fork after big_plan_kernel, join before the patch)
@@ -69,7 +73,7 @@ hipError_t launch_md5_stage(bool sar, const uint8_t *base, const uint64_t *offs,
                             const uint64_t *sizes, uint32_t n, const uint32_t *order,
                             const DevTables *tabs, const uint64_t *big_min, uint32_t *queue, uint32_t *crc_out,
                             uint8_t *sig_out, int32_t *codes_out, fdfs_gpu_file_state *states,
-                            const uint32_t *sidx, hipStream_t st);
+                            const uint32_t *sidx, unsigned ncu, hipStream_t st);
 hipError_t launch_sig_hash(bool sar, const uint8_t *base, const uint64_t *offs,
                            const uint64_t *sizes, uint32_t n, const uint32_t *order,
                            const DevTables *tabs, const uint64_t *big_min, uint32_t *crc_out, uint8_t *sig_out,
@@ -89,13 +93,14 @@ hipError_t launch_final(int method, const fdfs_gpu_file_state *states, const uin
 hipError_t launch_crc_combine(const uint32_t *a, const uint32_t *b, const uint64_t *len_b, uint32_t n,
                               uint32_t *out, const DevTables *tabs, hipStream_t st);
 // Split-file CRC: one rank's block of per-file words is {CRC term u32 x
-// nfiles, error word, length sum u64 x nfiles}; `base` is rank 0's block and
-// rank r's starts `stride` bytes further per rank (the all-gather's layout).
+// nfiles, error word, length sum u64 x nfiles, boundary sum u64 x nfiles};
+// `base` is rank 0's block and rank r's starts `stride` bytes further per
+// rank (the all-gather's layout).
 struct CrcParts {
     char *base;
     uint64_t nfiles, stride;
     static uint64_t err_off(uint64_t nfiles) { return (4 * nfiles + 7) & ~7ull; }
-    static uint64_t block_bytes(uint64_t nfiles) { return err_off(nfiles) + 8 + 8 * nfiles; }
+    static uint64_t block_bytes(uint64_t nfiles) { return err_off(nfiles) + 8 + 16 * nfiles; }
     __host__ __device__ uint32_t *word(uint32_t r, uint64_t f) const
     {
         return reinterpret_cast<uint32_t *>(base + r * stride) + f;
@@ -108,11 +113,17 @@ struct CrcParts {
     {
         return reinterpret_cast<uint64_t *>(base + r * stride + ((4 * nfiles + 7) & ~7ull) + 8) + f;
     }
+    // sum over the file's pieces of H(end) - H(start) (mod 2^64): equals
+    // H(size) - H(0) exactly when the pieces tile the file (see crc_piece_kernel)
+    __host__ __device__ uint64_t *bnd(uint32_t r, uint64_t f) const
+    {
+        return reinterpret_cast<uint64_t *>(base + r * stride + ((4 * nfiles + 7) & ~7ull) + 8) + nfiles + f;
+    }
 };
 // Each piece's term XORed into its rank's block (launch_crc_pieces), then
 // the fold of nranks blocks into the files' CRCs, the mask of ranks that
 // reported an error (err_out[0]) and the count of files whose pieces do not
-// add up to their size (err_out[1], zeroed by the caller).
+// tile them exactly (err_out[1], zeroed by the caller).
 hipError_t launch_crc_pieces(const uint32_t *crc, const uint64_t *pfile, const uint64_t *pstart, const uint64_t *plen,
                              uint32_t np, const uint64_t *fsize, uint64_t nfiles, const CrcParts &blk,
                              const DevTables *tabs, hipStream_t st);

@@ -332,17 +332,19 @@ __device__ __forceinline__ void pair_barrier()
     asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
 }
 
-template <bool SAR>
+// PM: probe mode, a template parameter so that the production
+// instantiation (PM 0) carries no probe branch; PM != 0 is instantiated only
+// in the probe build (make probes): 1 = MD5 wave at s_setprio 2, 2 = no CRC
+// arithmetic, 3 = no MD5 arithmetic (wrong results), 4 = both waves at
+// s_setprio 2 while their chunk is among the largest quarter (the chunks
+// that end the batch), 0 after.
+template <bool SAR, int PM>
 __global__ __launch_bounds__(128) void md5_pair_kernel(
     const uint8_t *__restrict__ base, const uint64_t *__restrict__ offs,
     const uint64_t *__restrict__ sizes, const uint32_t *__restrict__ order, uint32_t n,
     const DevTables *__restrict__ tabs, const uint64_t *__restrict__ big_min_p, uint32_t *__restrict__ queue,
-    int pmode, uint32_t *__restrict__ crc_out, uint8_t *__restrict__ sig_out, int32_t *__restrict__ codes_out)
+    uint32_t *__restrict__ crc_out, uint8_t *__restrict__ sig_out, int32_t *__restrict__ codes_out)
 {
-    // pmode (probe build only; 0 in production): 1 = MD5 wave at s_setprio
-    // 2, 2 = no CRC arithmetic, 3 = no MD5 arithmetic (wrong results), 4 =
-    // both waves at s_setprio 2 while their chunk is among the largest
-    // quarter (the chunks that end the batch), 0 after
     constexpr int CH = kMd5Chunk;
     constexpr int PIECES = CH / 16;
     constexpr int FPI = 64 / PIECES;
@@ -360,8 +362,10 @@ __global__ __launch_bounds__(128) void md5_pair_kernel(
     typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
     // wave-uniform role (an SGPR, so both roles' barriers are scalar branches)
     const bool loader = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6) != 0;
-    if (!loader && pmode == 1)
-        __builtin_amdgcn_s_setprio(2);
+    if constexpr (PM == 1) {
+        if (!loader)
+            __builtin_amdgcn_s_setprio(2);
+    }
     const int lane = threadIdx.x & 63;
     const uint32_t nw = (n + 63) / 64;
     const uint8_t *safe = reinterpret_cast<const uint8_t *>(tabs);
@@ -375,14 +379,12 @@ __global__ __launch_bounds__(128) void md5_pair_kernel(
         __syncthreads();  // s_chunk read by both waves before the next chunk's write
         if (chunk >= nw)
             break;
-#ifdef FDFS_PROBES
-        if (pmode == 4) {
+        if constexpr (PM == 4) {
             if (chunk < nw / 4)
                 __builtin_amdgcn_s_setprio(2);
             else
                 __builtin_amdgcn_s_setprio(0);
         }
-#endif
         const uint32_t i = chunk * 64 + lane;
         bool valid = i < n;
         uint32_t f = valid ? order[i] : 0;
@@ -402,7 +404,7 @@ __global__ __launch_bounds__(128) void md5_pair_kernel(
         const uint64_t rounds = (mx + BPR - 1) / BPR;
         const uint8_t *tp = p + (nblk << 6);
         if (loader) {
-            const bool small = L < big_min && pmode != 2;  // else the CRC comes from crc_seg_kernel
+            const bool small = L < big_min && PM != 2;  // else the CRC comes from crc_seg_kernel
             const int piece = lane % PIECES, fsub = lane / PIECES;
             const uint8_t *lp[NLD];
             uint64_t lim[NLD];
@@ -480,7 +482,7 @@ __global__ __launch_bounds__(128) void md5_pair_kernel(
                         for (int k = 0; k < 4; k++)
                             nxt[k] = q[4 * (b + 1) + k];
                     }
-                    if (r * BPR + b < nblk && pmode != 3) {
+                    if (r * BPR + b < nblk && PM != 3) {
                         const uint32_t m[16] = {cur[0].x, cur[0].y, cur[0].z, cur[0].w, cur[1].x, cur[1].y,
                                                 cur[1].z, cur[1].w, cur[2].x, cur[2].y, cur[2].z, cur[2].w,
                                                 cur[3].x, cur[3].y, cur[3].z, cur[3].w};
@@ -509,18 +511,10 @@ hipError_t launch_md5_stage(bool sar, const uint8_t *base, const uint64_t *offs,
                             const uint64_t *sizes, uint32_t n, const uint32_t *order,
                             const DevTables *tabs, const uint64_t *big_min, uint32_t *queue, uint32_t *crc_out,
                             uint8_t *sig_out, int32_t *codes_out, fdfs_gpu_file_state *states,
-                            const uint32_t *sidx, hipStream_t st)
+                            const uint32_t *sidx, unsigned ncu, hipStream_t st)
 {
-    static int ncu[64];
-    int dev = 0;
-    hipError_t e = hipGetDevice(&dev);
-    if (e != hipSuccess)
-        return e;
-    if (dev < 0 || dev >= 64)
-        return hipErrorInvalidDevice;
-    if (ncu[dev] == 0 &&
-        (e = hipDeviceGetAttribute(&ncu[dev], hipDeviceAttributeMultiprocessorCount, dev)) != hipSuccess)
-        return e;
+    if (ncu == 0)
+        return hipErrorInvalidValue;
 #ifdef FDFS_PROBES
     static int mode = -1;
     if (mode < 0) {  // A/B (make probes): FDFS_GPU_MD5_QUEUE=0 -> one chunk per wave, all resident
@@ -534,7 +528,7 @@ hipError_t launch_md5_stage(bool sar, const uint8_t *base, const uint64_t *offs,
     const uint32_t nw = (n + 63) / 64;
 #ifdef FDFS_PROBES
     static int pair = -1;
-    if (pair < 0) {  // A/B (make probes): FDFS_GPU_MD5_PAIR=0 -> the fused kernel, 2.. -> md5_pair_kernel pmode 1..
+    if (pair < 0) {  // A/B (make probes): FDFS_GPU_MD5_PAIR=0 -> the fused kernel, 2.. -> md5_pair_kernel PM 1..
         const char *ev = getenv("FDFS_GPU_MD5_PAIR");
         pair = ev ? atoi(ev) : 1;
     }
@@ -542,24 +536,35 @@ hipError_t launch_md5_stage(bool sar, const uint8_t *base, const uint64_t *offs,
     constexpr int pair = 1;
 #endif
     if (pair != 0 && mode != 0 && queue && !states) {  // queue zeroed by the caller
-        const unsigned g = 4u * (unsigned)ncu[dev];
+        const unsigned g = 4u * ncu;
         const unsigned grid2 = g < nw ? g : nw;
-        if (sar)
-            md5_pair_kernel<true><<<grid2, 128, 0, st>>>(base, offs, sizes, order, n, tabs, big_min, queue, pair - 1,
-                                                        crc_out, sig_out, codes_out);
+#define PAIR_LAUNCH(PM)                                                                                       \
+    (sar ? md5_pair_kernel<true, PM><<<grid2, 128, 0, st>>>(base, offs, sizes, order, n, tabs, big_min, queue, \
+                                                           crc_out, sig_out, codes_out)                      \
+         : md5_pair_kernel<false, PM><<<grid2, 128, 0, st>>>(base, offs, sizes, order, n, tabs, big_min, queue, \
+                                                            crc_out, sig_out, codes_out))
+#ifdef FDFS_PROBES
+        if (pair == 2)
+            PAIR_LAUNCH(1);
+        else if (pair == 3)
+            PAIR_LAUNCH(2);
+        else if (pair == 4)
+            PAIR_LAUNCH(3);
+        else if (pair == 5)
+            PAIR_LAUNCH(4);
         else
-            md5_pair_kernel<false><<<grid2, 128, 0, st>>>(base, offs, sizes, order, n, tabs, big_min, queue, pair - 1,
-                                                         crc_out, sig_out, codes_out);
+#endif
+            PAIR_LAUNCH(0);
+#undef PAIR_LAUNCH
         return hipGetLastError();
     }
     unsigned grid = (n + kBlk - 1) / kBlk;
     uint32_t *q = nullptr;
     if (mode && queue) {  // queue zeroed by the caller (launch_sig_lane's workspace memset)
         q = queue;
-        const unsigned g = (unsigned)ncu[dev];
-        grid = g < (nw + kMd5Waves - 1) / kMd5Waves ? g : (nw + kMd5Waves - 1) / kMd5Waves;
+        grid = ncu < (nw + kMd5Waves - 1) / kMd5Waves ? ncu : (nw + kMd5Waves - 1) / kMd5Waves;
     }
-    const uint32_t w1 = (uint32_t)ncu[dev] * kMd5Waves;
+    const uint32_t w1 = ncu * kMd5Waves;
 #define MD5_LAUNCH(S, T)                                                                              \
     md5_stage_kernel<S, T><<<grid, kBlk, 0, st>>>(base, offs, sizes, order, n, tabs, big_min, w1, q, \
                                                   crc_out, sig_out, codes_out, states, sidx)

@@ -832,6 +832,22 @@ hipError_t launch_zero_u32(void *p, uint64_t ndwords, hipStream_t st)
     return hipGetLastError();
 }
 
+// The context's lane-path error count (fdfs_api.cpp lane_err_note): +1 when
+// this launch's error word is set (word == nullptr: a fault injected by
+// fdfs_gpu_inject_error).  One thread; stream-ordered like every call of a
+// context, so the plain add needs no atomic.
+__global__ void lane_err_count_kernel(const uint32_t *__restrict__ word, uint64_t *__restrict__ count)
+{
+    if (threadIdx.x == 0 && (!word || *word))
+        *count += 1;
+}
+
+hipError_t launch_lane_err_count(const uint32_t *word, uint64_t *count, hipStream_t st)
+{
+    lane_err_count_kernel<<<1, 64, 0, st>>>(word, count);
+    return hipGetLastError();
+}
+
 // Small scans (a batch's segment counts, a small dedup's [digit][tile]
 // counts) in one block: one launch instead of three.  Only up to one pass of
 // the block: a single CU moves the 63K counts of a 1M-record dedup in 38 us
@@ -935,7 +951,7 @@ hipError_t launch_sig_lane(bool sar, int method, const uint8_t *base, const uint
     if (ev0)
         (void)hipEventRecord(ev0, st);
     e = (method == 2) ? launch_md5_stage(sar, base, offs, sizes, n, order, tabs, bmin, hist + 2 * kSizeBins,
-                                         crc_out, sig_out, codes_out, states, sidx, st)
+                                         crc_out, sig_out, codes_out, states, sidx, big ? big->ncu : 0, st)
                       : launch_sig_hash(sar, base, offs, sizes, n, order, tabs, bmin, crc_out, sig_out,
                                         codes_out, states, sidx, st);
     if (e != hipSuccess)

@@ -185,9 +185,26 @@ hipError_t launch_crc_carry(const uint32_t *crc, const uint64_t *sizes, uint32_t
 //   CRC32_ex(file, XINIT) = M^size XINIT ^ XOR_i M^(size - start_i - len_i) CRC32_ex(piece_i, 0)
 // whenever the pieces tile the file, in any order and on any rank, and
 // CRC32_ex(piece, 0) = ~crc[i] ^ M^len XINIT.  A rank's block (CrcParts)
-// holds per file the XOR of its pieces' terms and the sum of their lengths,
-// and an error word (bit 0: a piece names a file >= nfiles or runs past its
-// file's end; such a piece is dropped).
+// holds per file the XOR of its pieces' terms, the sum of their lengths and
+// the sum of H(end) - H(start) over them (H a 64-bit mix of a position, sums
+// mod 2^64), and an error word (bit 0: a piece names a file >= nfiles or runs
+// past its file's end; such a piece is dropped).
+//
+// Why the boundary sum: the number of pieces covering byte x is (starts <=
+// x) - (ends <= x), so it is 1 on [0, size) and 0 elsewhere -- every byte
+// covered exactly once -- if and only if the multiset of ends minus the
+// multiset of starts is {size} - {0}.  Summing H over that difference checks
+// this with a 2^-64-class false-accept chance (overlapping pieces plus a
+// matching gap, e.g. [0, 10) twice for a 20-byte file, pass the length sum
+// alone; they fail here).
+__device__ __forceinline__ uint64_t piece_pos_hash(uint64_t x)
+{
+    x += 0x9E3779B97F4A7C15ull;
+    x = (x ^ (x >> 30)) * 0xBF58476D1CE4E5B9ull;
+    x = (x ^ (x >> 27)) * 0x94D049BB133111EBull;
+    return x ^ (x >> 31);
+}
+
 __global__ void crc_piece_kernel(const uint32_t *__restrict__ crc, const uint64_t *__restrict__ pfile,
                                  const uint64_t *__restrict__ pstart, const uint64_t *__restrict__ plen,
                                  uint32_t np, const uint64_t *__restrict__ fsize, uint64_t nfiles,
@@ -209,11 +226,14 @@ __global__ void crc_piece_kernel(const uint32_t *__restrict__ crc, const uint64_
     const uint32_t c0 = ~crc[i] ^ advance_bytes(tabs->t, 0xFFFFFFFFu, len);
     atomicXor(blk.word(0, f), advance_bytes(tabs->t, c0, size - a - len));
     atomicAdd(reinterpret_cast<unsigned long long *>(blk.len(0, f)), (unsigned long long)len);
+    atomicAdd(reinterpret_cast<unsigned long long *>(blk.bnd(0, f)),
+              (unsigned long long)(piece_pos_hash(a + len) - piece_pos_hash(a)));
 }
 
 // The fold over the ranks' blocks: crc_out[f] = CRC32_FINAL(M^size XINIT ^
 // XOR_r term_r[f]); err_out[0] = the mask of ranks whose error word is set,
-// err_out[1] = the files whose pieces' lengths do not add up to their size
+// err_out[1] = the files whose pieces do not tile them exactly: lengths that
+// do not add up to the size, or a boundary sum other than H(size) - H(0)
 // (zeroed by the caller).
 __global__ void crc_fold_kernel(CrcParts blk, uint32_t nranks, const uint64_t *__restrict__ fsize, uint64_t nfiles,
                                 uint32_t *__restrict__ crc_out, uint64_t *__restrict__ err_out,
@@ -231,13 +251,14 @@ __global__ void crc_fold_kernel(CrcParts blk, uint32_t nranks, const uint64_t *_
          f += (uint64_t)gridDim.x * blockDim.x) {
         const uint64_t size = fsize[f];
         uint32_t x = advance_bytes(tabs->t, 0xFFFFFFFFu, size);
-        uint64_t covered = 0;
+        uint64_t covered = 0, bsum = 0;
         for (uint32_t r = 0; r < nranks; r++) {
             x ^= *blk.word(r, f);
             covered += *blk.len(r, f);
+            bsum += *blk.bnd(r, f);
         }
         crc_out[f] = ~x;
-        bad += covered != size;
+        bad += covered != size || bsum != piece_pos_hash(size) - piece_pos_hash(0);
     }
     if (bad)
         atomicAdd(reinterpret_cast<unsigned long long *>(err_out + 1), (unsigned long long)bad);

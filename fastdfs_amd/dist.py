@@ -73,7 +73,7 @@ def crc_batch_global(kernels, sizes, plan, data: torch.Tensor, offsets: torch.Te
 
     comm: a fastdfs_amd.api.Comm -> the whole step runs inside libfdfs_gpu
     (fdfs_gpu_crc_batch_global: each piece's term advanced to its file's
-    end, one ncclAllGather of 12 bytes per file, the fold on the device),
+    end, one ncclAllGather of 20 bytes per file, the fold on the device),
     the C recovery caller's path; this function then only builds the piece
     arrays from the plan."""
     if comm is not None:

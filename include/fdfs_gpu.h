@@ -168,7 +168,8 @@ int fdfs_gpu_state_init(fdfs_gpu_ctx *ctx, fdfs_gpu_file_state *states, uint32_t
  * state_idx given, the call checks this first (one small kernel and a host
  * synchronisation) and returns EINVAL without touching any state on a
  * repeated index or the reserved index 0xFFFFFFFF (inside a stream capture
- * the check is skipped and the contract is the caller's).  Chunks may start
+ * the check is skipped and the contract is the caller's; with state_idx the
+ * checked call takes at most 2^30 chunks, EINVAL above).  Chunks may start
  * at any byte and have any length, including 0. */
 int fdfs_gpu_update_batch(fdfs_gpu_ctx *ctx, const fdfs_gpu_batch *chunks, const uint32_t *state_idx,
                           int method, fdfs_gpu_file_state *states, void *stream);
@@ -202,7 +203,8 @@ int fdfs_gpu_dedup(fdfs_gpu_ctx *ctx, const uint8_t *sig, const uint64_t *gidx,
 /* The same answers packed, one 16-byte record per input record: rep and ref
  * of a record share a cache line, so the group's random answer stores
  * dirty one line per record instead of two (and the singleton answers are
- * one 16-byte store).  out: device fdfs_gpu_dedup_answer[n], 8-aligned. */
+ * one 16-byte store).  out: device fdfs_gpu_dedup_answer[n], 16-byte aligned
+ * (EINVAL otherwise). */
 typedef struct {
     uint64_t rep;       /* as rep_out of fdfs_gpu_dedup */
     uint32_t ref;       /* as ref_out */
@@ -277,7 +279,10 @@ int fdfs_gpu_index_slots(fdfs_gpu_index *index, uint64_t *slots);
  * Errors: an argument error or allocation failure on ANY rank is returned by
  * EVERY rank (EINVAL / ENOMEM; fdfs_gpu_last_error names the rank) before
  * any row moves, so no rank is left waiting.  EIO after that point (a failed
- * launch or RCCL call) leaves the communicator unusable: abort it.
+ * launch or RCCL call) leaves the communicator unusable: abort it.  Not
+ * capturable (it synchronises on the announcements): inside a stream capture
+ * it returns EINVAL before any collective is enqueued; every rank must call
+ * it outside a capture.
  * comm: an ncclComm_t (RCCL) of the ranks taking part, each rank's
  * communicator on this context's device.  Replaces the per-file
  * fdht_get_ex1 / fdht_set_ex / fdht_inc_ex round trips
@@ -310,18 +315,23 @@ int fdfs_gpu_dedup_global_local(fdfs_gpu_ctx *ctx, int nranks, const uint8_t *co
  * Inside: CRC32_ex of every piece from CRC32_XINIT (the segmented kernel),
  * each piece's CRC32_ex(piece, 0) advanced to the end of its file by a
  * GF(2) power of the zero-byte step and XORed into a per-file word, one
- * ncclAllGather of those words (12 bytes per file per rank), and the fold
+ * ncclAllGather of those words (20 bytes per file per rank), and the fold
  * M^size CRC32_XINIT ^ (the ranks' words), then CRC32_FINAL -- CRC32_ex is
  * linear over GF(2), so pieces may come in any order from any rank (the
  * reference's CRC32_ex(.., init) chaining, storage/storage_dio.c:467,
  * client/fdfs_crc32.c:67-99, computed for the pieces apart).  The pieces of
  * all ranks must tile each file exactly: a piece outside its file, or a file
- * whose pieces' lengths do not add up to its size, makes every rank return
+ * whose pieces do not tile it (lengths that do not add up to its size, or
+ * overlaps and gaps: checked by a sum of H(end) - H(start) over its pieces,
+ * H a 64-bit position hash, against H(size) - H(0)), makes every rank return
  * EINVAL (crc_out invalid).  An argument error or allocation failure on ANY
  * rank is returned by every rank (first, an all-gather of {nfiles, errno},
  * one host synchronisation).  Synchronous: returns after crc_out is written
- * (a second synchronisation reads the ranks' error words); not capturable.
- * EIO (a failed launch or RCCL call) leaves the communicator unusable. */
+ * (a second synchronisation reads the ranks' error words).  Not capturable:
+ * called inside a stream capture it returns EINVAL before any collective is
+ * enqueued (a captured collective would not run, so no rank could be told);
+ * every rank must call it outside a capture.  EIO (a failed launch or RCCL
+ * call) leaves the communicator unusable. */
 int fdfs_gpu_crc_batch_global(fdfs_gpu_ctx *ctx, void *comm, const fdfs_gpu_batch *pieces,
                               const uint64_t *piece_file, const uint64_t *piece_start,
                               const uint64_t *file_size, uint64_t nfiles, uint32_t *crc_out, void *stream);
@@ -480,6 +490,14 @@ int fdfs_gpu_scrub(fdfs_gpu_ctx *ctx, const fdfs_gpu_batch *batch, const uint32_
 
 /* Last HIP error string of this context (for logging), never NULL. */
 const char *fdfs_gpu_last_error(fdfs_gpu_ctx *ctx);
+
+/* Fault injection for tests of the error path: queues on `stream` what a
+ * signature launch whose size binning went wrong leaves behind (the lane
+ * path's error count raised by one), so that a later call of the context --
+ * the first whose entry check sees it, whatever calls were queued in between
+ * on any stream -- returns EIO once.  The lane path's errors are counted,
+ * not overwritten, so a later launch never hides an earlier one. */
+int fdfs_gpu_inject_error(fdfs_gpu_ctx *ctx, void *stream);
 
 #ifdef __cplusplus
 }

@@ -134,17 +134,21 @@ def hazards(insts: list[str]) -> list[str]:
 
 def check_library(lib_path: str) -> dict:
     """{"functions": n, "mfma": {kernel: [dst kinds]}, "dpp": {kernel: count},
-    "hazards": [..]}."""
-    res = {"functions": 0, "mfma": {}, "dpp": {}, "hazards": []}
+    "setprio": {kernel: count}, "hazards": [..]}."""
+    res = {"names": [], "functions": 0, "mfma": {}, "dpp": {}, "setprio": {}, "hazards": []}
     with tempfile.TemporaryDirectory() as d:
         for co in code_objects(lib_path, d):
             for fn, insts in disassemble(co).items():
                 res["functions"] += 1
+                res["names"].append(fn)
                 kinds = [operands(i)[1][0][0] for i in insts if i.startswith("v_mfma")]
                 if kinds:
                     res["mfma"][fn] = kinds
                 ndpp = sum(1 for i in insts if i.split(None, 1)[0].endswith("_dpp"))
                 if ndpp:
                     res["dpp"][fn] = ndpp
+                nprio = sum(1 for i in insts if i.startswith("s_setprio"))
+                if nprio:
+                    res["setprio"][fn] = nprio
                 res["hazards"] += [f"{fn}: {h}" for h in hazards(insts)]
     return res

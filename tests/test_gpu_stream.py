@@ -346,7 +346,8 @@ def test_crc_batch_global_ranks(oracle, ctxs, world):
 def test_crc_batch_global_rejects_bad_tilings(ctxs):
     """Pieces that do not tile their files make the call fail (EINVAL), not
     return a wrong CRC: a piece past its file's end, a file index past
-    nfiles, a gap, an overlap."""
+    nfiles, a gap, an overlap, and an overlap whose lengths still add up to
+    the file size (a matching gap)."""
     import fastdfs_amd as F
     rng = np.random.default_rng(77)
     sizes = np.array([1000, 5000, 0], np.int64)
@@ -358,7 +359,10 @@ def test_crc_batch_global_rejects_bad_tilings(ctxs):
     bad = {"past end": [[(0, 0, 600), (1, 0, 5000)], [(0, 600, 401)]],
            "file index": [[(0, 0, 600), (1, 0, 5000)], [(0, 600, 400), (3, 0, 0)]],
            "gap": [[(0, 0, 600), (1, 0, 5000)], [(0, 601, 399)]],
-           "overlap": [[(0, 0, 600), (1, 0, 5000)], [(0, 500, 500)]]}
+           "overlap": [[(0, 0, 600), (1, 0, 5000)], [(0, 500, 500)]],
+           # lengths add up (600 + 400) but [500, 600) is covered twice and
+           # [900, 1000) not at all: caught by the boundary sum
+           "overlap+gap": [[(0, 0, 600), (1, 0, 5000)], [(0, 500, 400)]]}
     for name, plan in bad.items():
         pieces = [[(f, a, n) for f, a, n in p if f < 3] for p in plan]
         ranks = [_rank_pieces(files, pieces[r], rng) for r in range(2)]
@@ -458,3 +462,42 @@ def test_update_rejects_repeated_state(ctxs, method):
                      state_idx=torch.randperm(n, device="cuda").to(torch.int32))
     torch.cuda.synchronize()
     assert not torch.equal(states, before)
+
+
+def test_lane_error_is_sticky(oracle):
+    """a lane-path error must reach the caller even when another
+    call is queued behind it before anything synchronises.  The fault is
+    injected on a stream (fdfs_gpu_inject_error: what a corrupt size binning
+    leaves), a HASH batch is queued right behind it, and further calls follow:
+    exactly one of them fails with EIO (the first whose entry check sees the
+    error), the ones after it succeed, and their results are exact."""
+    import errno
+    import fastdfs_amd as F
+    ctx = F.Context(0)
+    dev = torch.device("cuda", 0)
+    s = torch.cuda.Stream(dev)
+    rng = np.random.default_rng(5)
+    sizes = rng.integers(0, 20_000, 3000)
+    offs = np.zeros(len(sizes), np.int64)
+    offs[1:] = np.cumsum(sizes)[:-1]
+    buf = rng.integers(0, 256, int(sizes.sum()) + 1, dtype=np.uint8)
+    d = torch.from_numpy(buf).to(dev)
+    o = torch.from_numpy(offs).to(dev)
+    z = torch.from_numpy(sizes.astype(np.int64)).to(dev)
+    torch.cuda.synchronize()
+    ocrc, osig = oracle.dio_batch(buf, offs, sizes, 1, 0, nthreads=4)
+    rcs = []
+    ctx.inject_error(stream=s)
+    for k in range(4):
+        try:
+            crc, sig, _ = ctx.sig_batch(d, o, z, method=F.SIG_HASH, stream=s, check_bounds=False)
+            rcs.append(0)
+        except F.FdfsGpuError as e:
+            rcs.append(e.errno)
+        if k:  # the first batch is queued behind the fault with no synchronisation
+            s.synchronize()
+    assert rcs.count(errno.EIO) == 1 and rcs[-1] == 0, rcs
+    s.synchronize()
+    assert np.array_equal(crc.cpu().numpy().view(np.uint32), ocrc)
+    assert np.array_equal(sig.cpu().numpy(), osig)
+    ctx.close()

@@ -31,6 +31,17 @@ def test_no_valu_to_dpp_or_mfma_hazard(isa):
     assert isa["hazards"] == []
 
 
+def test_shipped_kernels_carry_no_probe_code(isa):
+    """the probe knobs are compiled into the probe build only.
+    The production md5_pair_kernel is the PM 0 instantiation alone (PM is a
+    template parameter) and no shipped kernel changes its issue priority
+    (s_setprio was a probe of round 3)."""
+    pair = [k for k in isa["names"] if "md5_pair_kernel" in k]
+    assert pair, "md5_pair_kernel not found in the shipped code object"
+    assert all(("Lb1ELi0E" in k or "Lb0ELi0E" in k) for k in pair), pair
+    assert isa["setprio"] == {}, isa["setprio"]
+
+
 DPP = "v_cndmask_b32_dpp v6, v5, v7, vcc quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf"
 MFMA = "v_mfma_i32_16x16x64_i8 a[0:3], v[60:63], v[110:113], a[0:3]"
 
