@@ -332,6 +332,15 @@ __device__ __forceinline__ void pair_barrier()
     asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
 }
 
+#ifdef FDFS_PROBES
+// PM 5 (probe build): per workgroup {start, end} wall clock (s_memrealtime,
+// 100 MHz), chunks taken, 128-byte rounds run, HW_ID and XCC_ID, read back
+// by fdfs_gpu_probe_pairs (scripts/pair_timeline.py): where the batch's time
+// ends, pair by pair.
+constexpr int kPairProbeMax = 8192;
+__device__ uint64_t g_pair_probe[kPairProbeMax * 4];
+#endif
+
 // PM: probe mode, a template parameter so that the production
 // instantiation (PM 0) carries no probe branch; PM != 0 is instantiated only
 // in the probe build (make probes): 1 = MD5 wave at s_setprio 2, 2 = no CRC
@@ -371,14 +380,33 @@ __global__ __launch_bounds__(128) void md5_pair_kernel(
     const uint8_t *safe = reinterpret_cast<const uint8_t *>(tabs);
     const uint32_t K16 = tabs->t.K16;
     const uint64_t big_min = big_min_p ? *big_min_p : ~0ull;
+#ifdef FDFS_PROBES
+    uint64_t pr_t0 = 0, pr_chunks = 0, pr_rounds = 0;
+    if constexpr (PM == 5)
+        pr_t0 = wall_clock64();
+#endif
     for (;;) {
         if (threadIdx.x == 64)
             s_chunk = atomicAdd(queue, 1u);
         __syncthreads();
         const uint32_t chunk = __builtin_amdgcn_readfirstlane(s_chunk);
         __syncthreads();  // s_chunk read by both waves before the next chunk's write
-        if (chunk >= nw)
+        if (chunk >= nw) {
+#ifdef FDFS_PROBES
+            if constexpr (PM == 5) {
+                if (threadIdx.x == 0 && blockIdx.x < kPairProbeMax) {
+                    const uint32_t hw = __builtin_amdgcn_s_getreg((4) | (0 << 6) | (31 << 11));
+                    const uint32_t xcc = __builtin_amdgcn_s_getreg((20) | (0 << 6) | (31 << 11));
+                    uint64_t *o = g_pair_probe + 4ull * blockIdx.x;
+                    o[0] = pr_t0;
+                    o[1] = wall_clock64();
+                    o[2] = pr_chunks | (pr_rounds << 20);
+                    o[3] = (uint64_t)hw | ((uint64_t)xcc << 32);
+                }
+            }
+#endif
             break;
+        }
         if constexpr (PM == 4) {
             if (chunk < nw / 4)
                 __builtin_amdgcn_s_setprio(2);
@@ -403,6 +431,10 @@ __global__ __launch_bounds__(128) void md5_pair_kernel(
         }
         const uint64_t rounds = (mx + BPR - 1) / BPR;
         const uint8_t *tp = p + (nblk << 6);
+#ifdef FDFS_PROBES
+        pr_chunks += 1;
+        pr_rounds += rounds;
+#endif
         if (loader) {
             const bool small = L < big_min && PM != 2;  // else the CRC comes from crc_seg_kernel
             const int piece = lane % PIECES, fsub = lane / PIECES;
@@ -552,6 +584,8 @@ hipError_t launch_md5_stage(bool sar, const uint8_t *base, const uint64_t *offs,
             PAIR_LAUNCH(3);
         else if (pair == 5)
             PAIR_LAUNCH(4);
+        else if (pair == 6)
+            PAIR_LAUNCH(5);
         else
 #endif
             PAIR_LAUNCH(0);
@@ -577,3 +611,13 @@ hipError_t launch_md5_stage(bool sar, const uint8_t *base, const uint64_t *offs,
 }
 
 }  // namespace fdfs
+
+#ifdef FDFS_PROBES
+extern "C" int fdfs_gpu_probe_pairs(uint64_t *host, size_t words)
+{
+    if (words > 4ull * fdfs::kPairProbeMax)
+        words = 4ull * fdfs::kPairProbeMax;
+    return hipMemcpyFromSymbol(host, HIP_SYMBOL(fdfs::g_pair_probe), 8 * words, 0, hipMemcpyDeviceToHost) ==
+                   hipSuccess ? 0 : 5;
+}
+#endif

@@ -14,3 +14,5 @@ tail -3 $O/pytest.log
 if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then exit $rc; fi
 step bench_c2 600 python3 bench.py || exit $?
 tail -1 $O/bench_c2.log | cut -c1-600
+FDFS_GPU_PROBE_LIB=1 FDFS_GPU_MD5_PAIR=6 step pair_timeline 600 python3 -u scripts/pair_timeline.py --out $O/pairs.npz || exit $?
+cat $O/pair_timeline.log | cut -c1-900
