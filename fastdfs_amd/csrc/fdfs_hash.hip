@@ -632,17 +632,26 @@ hipError_t launch_sig_hash(bool sar, const uint8_t *base, const uint64_t *offs,
 #endif
 #ifdef FDFS_PROBES
     const unsigned blk = ((tm >= 2 || mode == 5) && !states) ? 1024 : kHashBlock;
+    // FDFS_GPU_HASH_LDSPAD: dynamic LDS bytes per workgroup that the kernel
+    // does not use, to cap its occupancy (waves per SIMD) for the role-split
+    // bound of DESIGN 4.2
+    static long shm = -1;
+    if (shm < 0) {
+        const char *ev = getenv("FDFS_GPU_HASH_LDSPAD");
+        shm = ev ? atol(ev) : 0;
+    }
 #else
     const unsigned blk = kHashBlock;
+    constexpr unsigned shm = 0;
 #endif
     const unsigned grid = (n + blk - 1) / blk;
 #ifdef FDFS_PROBES
 #define HASH_LAUNCH_TM2(S, M)                                                                            \
     else if (tm == 2)                                                                                    \
-        sig_hash_kernel<S, 2, M, false, false><<<grid, blk, 0, st>>>(base, offs, sizes, order, n, tabs, big_min, \
+        sig_hash_kernel<S, 2, M, false, false><<<grid, blk, (unsigned)shm, st>>>(base, offs, sizes, order, n, tabs, big_min, \
                                                                      crc_out, sig_out, codes_out, nullptr, nullptr); \
     else if (tm == 3)                                                                                    \
-        sig_hash_kernel<S, 2, M, false, true><<<grid, blk, 0, st>>>(base, offs, sizes, order, n, tabs, big_min, \
+        sig_hash_kernel<S, 2, M, false, true><<<grid, blk, (unsigned)shm, st>>>(base, offs, sizes, order, n, tabs, big_min, \
                                                                     crc_out, sig_out, codes_out, nullptr, nullptr);
 #else
 // the rotated-table form (TM 2, VGPR accumulators) exists in the probe
@@ -653,14 +662,14 @@ hipError_t launch_sig_hash(bool sar, const uint8_t *base, const uint64_t *offs,
 #define HASH_LAUNCH(S, M)                                                                                \
     do {                                                                                                 \
         if (states)                                                                                      \
-            sig_hash_kernel<S, 0, M, true, true><<<grid, blk, 0, st>>>(base, offs, sizes, order, n, tabs, big_min, \
+            sig_hash_kernel<S, 0, M, true, true><<<grid, blk, (unsigned)shm, st>>>(base, offs, sizes, order, n, tabs, big_min, \
                                                                  crc_out, sig_out, codes_out, states, sidx); \
         HASH_LAUNCH_TM2(S, M)                                                                            \
         else if (ql)                                                                                     \
-            sig_hash_kernel<S, 0, M, false, true><<<grid, blk, 0, st>>>(base, offs, sizes, order, n, tabs, big_min, \
+            sig_hash_kernel<S, 0, M, false, true><<<grid, blk, (unsigned)shm, st>>>(base, offs, sizes, order, n, tabs, big_min, \
                                                                   crc_out, sig_out, codes_out, nullptr, nullptr); \
         else                                                                                             \
-            sig_hash_kernel<S, 0, M, false, false><<<grid, blk, 0, st>>>(base, offs, sizes, order, n, tabs, big_min, \
+            sig_hash_kernel<S, 0, M, false, false><<<grid, blk, (unsigned)shm, st>>>(base, offs, sizes, order, n, tabs, big_min, \
                                                                   crc_out, sig_out, codes_out, nullptr, nullptr); \
     } while (0)
 #ifdef FDFS_PROBES
