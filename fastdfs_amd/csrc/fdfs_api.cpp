@@ -137,6 +137,7 @@ fdfs::BigCrcWs carve_big(const fdfs_gpu_ctx *ctx, Carve &cv, uint32_t n)
         big.lat_files = (uint32_t)lf;
     // FDFS_GPU_MD5_T_BIN: MD5 batches above lat_files offload the CRC of the
     // files in size bins >= this one; FDFS_GPU_SIDE=1: beside the lane kernel
+    // (2: enqueued after it, on a lowest-priority stream)
     static long mb = -2, sd = -2;
     if (mb == -2) {
         const char *ev = getenv("FDFS_GPU_MD5_T_BIN");
@@ -145,10 +146,11 @@ fdfs::BigCrcWs carve_big(const fdfs_gpu_ctx *ctx, Carve &cv, uint32_t n)
         sd = es ? atol(es) : 0;
     }
     big.md5_bin = (uint32_t)mb;
-    if (sd == 1) {
+    if (sd >= 1) {  // 2: enqueued after the lane kernel
         big.side = ctx->side;
         big.fork = ctx->fork;
         big.join = ctx->join;
+        big.side_late = sd == 2;
     }
 #endif
     return big;
@@ -352,8 +354,11 @@ int fdfs_gpu_open(int device, unsigned flags, fdfs_gpu_ctx **out)
     fdfs::build_poly_mfma_tables(h->pm);
     hipError_t e = hipEventCreateWithFlags(&ctx->ws_ev, hipEventDisableTiming);
 #ifdef FDFS_PROBES  // the side-stream offload measurement (FDFS_GPU_SIDE, carve_big)
+    int prio_lo = 0, prio_hi = 0;  // the side stream at the lowest priority
     if (e == hipSuccess)
-        e = hipStreamCreateWithFlags(&ctx->side, hipStreamNonBlocking);
+        e = hipDeviceGetStreamPriorityRange(&prio_lo, &prio_hi);
+    if (e == hipSuccess)
+        e = hipStreamCreateWithPriority(&ctx->side, hipStreamNonBlocking, prio_lo);
     if (e == hipSuccess)
         e = hipEventCreateWithFlags(&ctx->fork, hipEventDisableTiming);
     if (e == hipSuccess)

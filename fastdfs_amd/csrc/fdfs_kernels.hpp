@@ -51,6 +51,7 @@ struct BigCrcWs {  // device arrays of n entries (seg_first n + 1)
     // the lane kernel (fork after big_plan_kernel, join before the patch)
     hipStream_t side = nullptr;
     hipEvent_t fork = nullptr, join = nullptr;
+    bool side_late = false;  // the segmented kernels enqueued after the lane kernel (host order)
 };
 hipError_t launch_poly_seg(const uint8_t *base, const uint64_t *boffs, const uint64_t *bsizes,
                            const uint64_t *seg_first, const uint32_t *nbig, uint32_t *bpoly,

@@ -927,24 +927,29 @@ hipError_t launch_sig_lane(bool sar, int method, const uint8_t *base, const uint
     uint32_t *err = hist + kLaneErrWord;
     bin_scatter_kernel<<<sb, 1024, 0, st>>>(sizes, n, cursor, order, err);
     const bool offload = big != nullptr;
-    if (offload) {  // CRC (HASH: simple_hash, Time33 too) of the files >= T by the segmented kernels, first
+    // the segmented passes over the files >= T (CRC; HASH: simple_hash,
+    // Time33 too): before the lane kernel on `st`, or on big->side beside it
+    // (forked after big_plan_kernel; side_late: enqueued after the lane
+    // kernel, so the lane kernel's workgroups are dispatched first)
+    auto seg_passes = [&](hipStream_t ss) -> hipError_t {
+        hipError_t e2 = crc_seg_run(sar, base, big->offs, big->sizes, big->seg_first, n, big->nbig, tabs, big->crc,
+                                    seg_grid, ss);
+        if (e2 == hipSuccess && method == 1)
+            e2 = launch_poly_seg(base, big->offs, big->sizes, big->seg_first, big->nbig, big->poly, seg_grid, ss);
+        if (e2 == hipSuccess && big->side)
+            e2 = hipEventRecord(big->join, big->side);
+        return e2;
+    };
+    if (offload) {
         big_plan_kernel<<<1, 1024, 0, st>>>(hist, order, offs, sizes, n, method, big->lat_files, big->md5_bin,
                                             big->nbig, big->big_min, big->offs, big->sizes, big->seg_first,
                                             big->crc, big->poly, err);
-        hipStream_t ss = st;
         if (big->side) {  // fork: the segmented passes beside the lane kernel
             if ((e = hipEventRecord(big->fork, st)) != hipSuccess ||
                 (e = hipStreamWaitEvent(big->side, big->fork, 0)) != hipSuccess)
                 return e;
-            ss = big->side;
         }
-        if ((e = crc_seg_run(sar, base, big->offs, big->sizes, big->seg_first, n, big->nbig, tabs, big->crc,
-                             seg_grid, ss)) != hipSuccess)
-            return e;
-        if (method == 1 && (e = launch_poly_seg(base, big->offs, big->sizes, big->seg_first, big->nbig, big->poly,
-                                                seg_grid, ss)) != hipSuccess)
-            return e;
-        if (big->side && (e = hipEventRecord(big->join, big->side)) != hipSuccess)
+        if (!(big->side && big->side_late) && (e = seg_passes(big->side ? big->side : st)) != hipSuccess)
             return e;
     }
     const uint64_t *bmin = offload ? big->big_min : nullptr;
@@ -958,6 +963,8 @@ hipError_t launch_sig_lane(bool sar, int method, const uint8_t *base, const uint
         return e;
     if (ev1)
         (void)hipEventRecord(ev1, st);
+    if (offload && big->side && big->side_late && (e = seg_passes(big->side)) != hipSuccess)
+        return e;
     if (offload && big->side && (e = hipStreamWaitEvent(st, big->join, 0)) != hipSuccess)
         return e;
     if (offload && states)
