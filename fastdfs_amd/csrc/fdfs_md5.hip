@@ -338,7 +338,7 @@ __device__ __forceinline__ void pair_barrier()
 // by fdfs_gpu_probe_pairs (scripts/pair_timeline.py): where the batch's time
 // ends, pair by pair.
 constexpr int kPairProbeMax = 8192;
-__device__ uint64_t g_pair_probe[kPairProbeMax * 4];
+__device__ uint64_t g_pair_probe[kPairProbeMax * 8];  // [wg][8]: 4 words above, then first chunk, its end, rounds
 #endif
 
 // PM: probe mode, a template parameter so that the production
@@ -397,7 +397,7 @@ __global__ __launch_bounds__(128) void md5_pair_kernel(
                 if (threadIdx.x == 0 && blockIdx.x < kPairProbeMax) {
                     const uint32_t hw = __builtin_amdgcn_s_getreg((4) | (0 << 6) | (31 << 11));
                     const uint32_t xcc = __builtin_amdgcn_s_getreg((20) | (0 << 6) | (31 << 11));
-                    uint64_t *o = g_pair_probe + 4ull * blockIdx.x;
+                    uint64_t *o = g_pair_probe + 8ull * blockIdx.x;
                     o[0] = pr_t0;
                     o[1] = wall_clock64();
                     o[2] = pr_chunks | (pr_rounds << 20);
@@ -432,6 +432,19 @@ __global__ __launch_bounds__(128) void md5_pair_kernel(
         const uint64_t rounds = (mx + BPR - 1) / BPR;
         const uint8_t *tp = p + (nblk << 6);
 #ifdef FDFS_PROBES
+        if constexpr (PM == 5) {
+            if (threadIdx.x == 0 && blockIdx.x < kPairProbeMax) {
+                uint64_t *o = g_pair_probe + 8ull * blockIdx.x;
+                if (pr_chunks == 1)
+                    o[5] = wall_clock64();  // the first chunk ended (this is the second)
+                if (pr_chunks == 0) {
+                    o[4] = chunk;
+                    o[6] = rounds;
+                } else if (pr_chunks == 1) {
+                    o[7] = chunk;
+                }
+            }
+        }
         pr_chunks += 1;
         pr_rounds += rounds;
 #endif
@@ -615,8 +628,8 @@ hipError_t launch_md5_stage(bool sar, const uint8_t *base, const uint64_t *offs,
 #ifdef FDFS_PROBES
 extern "C" int fdfs_gpu_probe_pairs(uint64_t *host, size_t words)
 {
-    if (words > 4ull * fdfs::kPairProbeMax)
-        words = 4ull * fdfs::kPairProbeMax;
+    if (words > 8ull * fdfs::kPairProbeMax)
+        words = 8ull * fdfs::kPairProbeMax;
     return hipMemcpyFromSymbol(host, HIP_SYMBOL(fdfs::g_pair_probe), 8 * words, 0, hipMemcpyDeviceToHost) ==
                    hipSuccess ? 0 : 5;
 }

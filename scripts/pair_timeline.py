@@ -46,9 +46,11 @@ def main():
         ctx.sig_batch(data, offs, szs, method=F.SIG_MD5, check_bounds=False)
         torch.cuda.synchronize()
         kms, _ = ctx.read_timing(_lib.KERNEL_SIG_LANE)
-        buf = np.zeros(4 * nwg, np.uint64)
+        buf = np.zeros(8 * nwg, np.uint64)
+        # the per-chunk words are written only when a second chunk starts
         assert L.fdfs_gpu_probe_pairs(buf.ctypes.data, buf.size) == 0
-        r = buf.reshape(nwg, 4)
+        r8 = buf.reshape(nwg, 8)
+        r = r8[:, :4]
         t0 = r[:, 0].astype(np.float64)
         t1 = r[:, 1].astype(np.float64)
         base = t0.min()
@@ -86,8 +88,11 @@ def main():
         res.append(d)
         print(json.dumps(d), flush=True)
         if a.out and rep == a.reps - 1:
+            first_end = np.where(chunks > 1, (r8[:, 5].astype(np.float64) - base) / hz * 1e3, end_ms)
             np.savez_compressed(a.out, start_ms=start_ms, end_ms=end_ms, chunks=chunks, rounds=rounds,
-                                hw=hw, xcc=xcc)
+                                hw=hw, xcc=xcc, first_chunk=r8[:, 4].astype(np.int64),
+                                first_rounds=r8[:, 6].astype(np.int64), first_end_ms=first_end,
+                                second_chunk=np.where(chunks > 1, r8[:, 7].astype(np.int64), -1))
     ctx.close()
 
 
