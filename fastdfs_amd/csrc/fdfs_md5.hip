@@ -327,6 +327,23 @@ __global__ __launch_bounds__(64 * kMd5Waves) void md5_stage_kernel(
 // loads stays in flight across it (__syncthreads would wait for them).
 // Four workgroups per CU (35.8 KB of LDS each), the same 64 MD5 lanes per
 // SIMD as the fused form's one wave per SIMD.
+// Issue priority from a wave-uniform count of remaining 128-byte rounds
+// (probe PM 6): the pairs with the most work left issue first on their
+// SIMDs, against the hardware's oldest-wave-first default (which starves the
+// workgroups dispatched last, scripts/pair_timeline.py).
+__device__ __forceinline__ void prio_by_remaining(uint64_t rem)
+{
+    const uint32_t q = __builtin_amdgcn_readfirstlane((uint32_t)(rem >> 13));  // 8K-round units
+    if (q >= 3)
+        __builtin_amdgcn_s_setprio(3);
+    else if (q == 2)
+        __builtin_amdgcn_s_setprio(2);
+    else if (q == 1)
+        __builtin_amdgcn_s_setprio(1);
+    else
+        __builtin_amdgcn_s_setprio(0);
+}
+
 __device__ __forceinline__ void pair_barrier()
 {
     asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
@@ -413,6 +430,17 @@ __global__ __launch_bounds__(128) void md5_pair_kernel(
             else
                 __builtin_amdgcn_s_setprio(0);
         }
+        if constexpr (PM == 7) {  // the last-dispatched first chunks and every later chunk first
+            const uint32_t q = chunk < gridDim.x ? chunk * 4 / gridDim.x : 3;
+            if (q >= 3)
+                __builtin_amdgcn_s_setprio(3);
+            else if (q == 2)
+                __builtin_amdgcn_s_setprio(2);
+            else if (q == 1)
+                __builtin_amdgcn_s_setprio(1);
+            else
+                __builtin_amdgcn_s_setprio(0);
+        }
         const uint32_t i = chunk * 64 + lane;
         bool valid = i < n;
         uint32_t f = valid ? order[i] : 0;
@@ -489,6 +517,10 @@ __global__ __launch_bounds__(128) void md5_pair_kernel(
             };
             issue(RA, 0);
             for (uint64_t r = 0; r < rounds; r += 2) {
+                if constexpr (PM == 6) {
+                    if ((r & 255) == 0)
+                        prio_by_remaining(rounds - r);
+                }
                 issue(RB, r + 1);
                 stage(RA, sbuf[0]);
                 pair_barrier();
@@ -514,6 +546,10 @@ __global__ __launch_bounds__(128) void md5_pair_kernel(
             uint32_t st[4] = {0x67452301u, 0xefcdab89u, 0x98badcfeu, 0x10325476u};  // my_md5_init
             const uint8_t *mine = &sbuf[0][0] + lane * STRIDE;
             for (uint64_t r = 0; r < rounds; r++) {
+                if constexpr (PM == 6) {
+                    if ((r & 255) == 0)
+                        prio_by_remaining(rounds - r);
+                }
                 pair_barrier();
                 const uint4 *q = reinterpret_cast<const uint4 *>(mine + (r & 1) * (64 * STRIDE));
                 // block b + 1's words are read from LDS (for every lane,
@@ -599,6 +635,10 @@ hipError_t launch_md5_stage(bool sar, const uint8_t *base, const uint64_t *offs,
             PAIR_LAUNCH(4);
         else if (pair == 6)
             PAIR_LAUNCH(5);
+        else if (pair == 7)
+            PAIR_LAUNCH(6);
+        else if (pair == 8)
+            PAIR_LAUNCH(7);
         else
 #endif
             PAIR_LAUNCH(0);
