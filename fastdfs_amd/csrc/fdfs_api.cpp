@@ -137,7 +137,8 @@ fdfs::BigCrcWs carve_big(const fdfs_gpu_ctx *ctx, Carve &cv, uint32_t n)
         big.lat_files = (uint32_t)lf;
     // FDFS_GPU_MD5_T_BIN: MD5 batches above lat_files offload the CRC of the
     // files in size bins >= this one; FDFS_GPU_SIDE=1: beside the lane kernel
-    // (2: enqueued after it, on a lowest-priority stream)
+    // (2: enqueued after it, on a lowest-priority stream; 3: items of the
+    // pair kernel's queue)
     static long mb = -2, sd = -2;
     if (mb == -2) {
         const char *ev = getenv("FDFS_GPU_MD5_T_BIN");
@@ -146,7 +147,9 @@ fdfs::BigCrcWs carve_big(const fdfs_gpu_ctx *ctx, Carve &cv, uint32_t n)
         sd = es ? atol(es) : 0;
     }
     big.md5_bin = (uint32_t)mb;
-    if (sd >= 1) {  // 2: enqueued after the lane kernel
+    if (sd == 3) {  // 3: the CRC segments as md5_pair_kernel queue items
+        big.md5_inline = true;
+    } else if (sd >= 1) {  // 2: enqueued after the lane kernel
         big.side = ctx->side;
         big.fork = ctx->fork;
         big.join = ctx->join;

@@ -285,6 +285,7 @@ struct DpOut {
 // K1: keys, the singleton answer (rep = own gidx, ref = 1) of every record,
 // and the tile's entries sorted by digit (top d1 bits; unstable: order inside
 // a partition does not matter) written back as one contiguous run.
+template <bool DEF>
 __global__ __launch_bounds__(kDpTileThreads) void dp_tile_kernel(
     const uint8_t *__restrict__ sig, uint32_t stride, const uint64_t *__restrict__ gidx,
     uint32_t gstride, uint64_t n, int d1, uint64_t tiles, uint64_t *__restrict__ ent1,
@@ -311,8 +312,10 @@ __global__ __launch_bounds__(kDpTileThreads) void dp_tile_kernel(
             load_sig(sig + r * stride, a, b, c);
             key[it] = (uint32_t)sig_hash(a, b, c);
             // every record starts as its own class; dp_group overwrites the
-            // records of classes with more than one member
-            out.store(r, gstride ? gidx[r * gstride] : r, 1u, true);
+            // records of classes with more than one member (!DEF: dp_split
+            // writes these instead)
+            if constexpr (DEF)
+                out.store(r, gstride ? gidx[r * gstride] : r, 1u, true);
         }
     }
 #pragma unroll
@@ -408,12 +411,26 @@ __device__ __forceinline__ uint32_t dp_sw(uint32_t i) { return i ^ (((i >> 4) & 
 
 // NB: digit bins (1 << d2 <= NB); 1024 bins keep the LDS at 72 KB, two
 // workgroups per CU.
-template <int NB>
+// DEF: the singleton answers of records [g * kDpChunk, (g + 1) * kDpChunk)
+// are written here (coalesced, beside the chunk's gather) instead of by
+// dp_tile; every chunk index below ceil(n / kDpChunk) is a real chunk (the
+// buckets' chunk counts sum to at least that).
+template <int NB, bool DEF>
 __global__ __launch_bounds__(kDpSplitThreads) void dp_split_kernel(
     const uint64_t *__restrict__ ent1, int d1, int d2, uint64_t tiles, const uint64_t *__restrict__ off1,
     const uint32_t *__restrict__ loc1, const uint32_t *__restrict__ cb, const uint32_t *__restrict__ chunk_ta,
-    const uint4 *__restrict__ chunk_hd, uint64_t *__restrict__ ent2, uint16_t *__restrict__ cdo)
+    const uint4 *__restrict__ chunk_hd, uint64_t *__restrict__ ent2, uint16_t *__restrict__ cdo,
+    DpOut out, const uint64_t *__restrict__ gidx, uint32_t gstride, uint64_t n)
 {
+    if constexpr (DEF) {
+        const uint64_t r0 = (uint64_t)blockIdx.x * kDpChunk;
+#pragma unroll
+        for (int q = 0; q < kDpSplitPer; q++) {
+            const uint64_t r = r0 + (uint64_t)q * kDpSplitThreads + threadIdx.x;
+            if (r < n)
+                out.store(r, gstride ? gidx[r * gstride] : r, 1u, true);
+        }
+    }
     constexpr int NT = kDpSplitThreads;
     constexpr int PER = NB / NT;
     static_assert(NB % NT == 0, "bins per thread");
@@ -1051,18 +1068,36 @@ hipError_t launch_dedup_group(const uint8_t *sig, uint32_t sig_stride, const uin
     hipError_t e;
     if (ev0)
         (void)hipEventRecord(ev0, st);
-    dp_tile_kernel<<<(unsigned)pl.tiles, kDpTileThreads, 0, st>>>(sig, sig_stride, gidx, gidx_stride, n, pl.d1,
-                                                                  pl.tiles, ent1, out, cnt1, loc1);
+#ifdef FDFS_PROBES
+    // measurement build only: FDFS_GPU_DEDUP_DEF=1 -> the singleton answers
+    // are written by dp_split instead of dp_tile
+    static int defs = -1;
+    if (defs < 0) {
+        const char *ev = getenv("FDFS_GPU_DEDUP_DEF");
+        defs = ev ? atoi(ev) : 0;
+    }
+    const bool split_def = defs == 1;
+#else
+    constexpr bool split_def = false;
+#endif
+    if (split_def)
+        dp_tile_kernel<false><<<(unsigned)pl.tiles, kDpTileThreads, 0, st>>>(sig, sig_stride, gidx, gidx_stride, n,
+                                                                             pl.d1, pl.tiles, ent1, out, cnt1, loc1);
+    else
+        dp_tile_kernel<true><<<(unsigned)pl.tiles, kDpTileThreads, 0, st>>>(sig, sig_stride, gidx, gidx_stride, n,
+                                                                            pl.d1, pl.tiles, ent1, out, cnt1, loc1);
     if ((e = launch_exclusive_scan(cnt1, ncnt, off1, bsum, st)) != hipSuccess)
         return e;
     dp_chunks_kernel<<<1, 256, 0, st>>>(off1, pl.d1, pl.tiles, cb, slow);
     dp_chunk_ta_kernel<<<grid_for(ncnt, 256), 256, 0, st>>>(off1, pl.tiles, ncnt, cb, chunk_ta, chunk_hd);
+#define DP_SPLIT(NB, D)                                                                                  \
+    dp_split_kernel<NB, D><<<(unsigned)pl.chunks, kDpSplitThreads, 0, st>>>(                             \
+        ent1, pl.d1, pl.d2, pl.tiles, off1, loc1, cb, chunk_ta, chunk_hd, ent2, cdo, out, gidx, gidx_stride, n)
     if (pl.d2 <= 10)
-        dp_split_kernel<1024><<<(unsigned)pl.chunks, kDpSplitThreads, 0, st>>>(ent1, pl.d1, pl.d2, pl.tiles, off1,
-                                                                              loc1, cb, chunk_ta, chunk_hd, ent2, cdo);
+        split_def ? DP_SPLIT(1024, true) : DP_SPLIT(1024, false);
     else
-        dp_split_kernel<1 << kDpMaxD2><<<(unsigned)pl.chunks, kDpSplitThreads, 0, st>>>(
-            ent1, pl.d1, pl.d2, pl.tiles, off1, loc1, cb, chunk_ta, chunk_hd, ent2, cdo);
+        split_def ? DP_SPLIT(1 << kDpMaxD2, true) : DP_SPLIT(1 << kDpMaxD2, false);
+#undef DP_SPLIT
     const int gmode = !gidx_stride ? GM_INDEX
                       : (gidx == reinterpret_cast<const uint64_t *>(sig + 24) && 8 * gidx_stride == sig_stride)
                           ? GM_ROW

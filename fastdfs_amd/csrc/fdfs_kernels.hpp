@@ -52,6 +52,18 @@ struct BigCrcWs {  // device arrays of n entries (seg_first n + 1)
     hipStream_t side = nullptr;
     hipEvent_t fork = nullptr, join = nullptr;
     bool side_late = false;  // the segmented kernels enqueued after the lane kernel (host order)
+    // MD5 batches above lat_files: the offloaded files' CRC segments are items
+    // of md5_pair_kernel's own queue after its MD5 chunks (no crc_seg launch)
+    bool md5_inline = false;
+};
+// The CRC segment items md5_pair_kernel takes once its MD5 chunks are gone
+// (nbig == nullptr: none): the 64 KiB segments of big_plan_kernel's list
+// (the files >= T, whose loader lanes skipped their CRC), each XORed into
+// crc[i] advanced to its file's end (crc zeroed by big_plan_kernel).
+struct PairSegs {
+    const uint32_t *nbig = nullptr;
+    const uint64_t *offs = nullptr, *sizes = nullptr, *seg_first = nullptr;
+    uint32_t *crc = nullptr;
 };
 hipError_t launch_poly_seg(const uint8_t *base, const uint64_t *boffs, const uint64_t *bsizes,
                            const uint64_t *seg_first, const uint32_t *nbig, uint32_t *bpoly,
@@ -74,7 +86,7 @@ hipError_t launch_md5_stage(bool sar, const uint8_t *base, const uint64_t *offs,
                             const uint64_t *sizes, uint32_t n, const uint32_t *order,
                             const DevTables *tabs, const uint64_t *big_min, uint32_t *queue, uint32_t *crc_out,
                             uint8_t *sig_out, int32_t *codes_out, fdfs_gpu_file_state *states,
-                            const uint32_t *sidx, unsigned ncu, hipStream_t st);
+                            const uint32_t *sidx, unsigned ncu, const PairSegs *segs, hipStream_t st);
 hipError_t launch_sig_hash(bool sar, const uint8_t *base, const uint64_t *offs,
                            const uint64_t *sizes, uint32_t n, const uint32_t *order,
                            const DevTables *tabs, const uint64_t *big_min, uint32_t *crc_out, uint8_t *sig_out,

@@ -7,6 +7,7 @@
 #include "fdfs_device.hpp"
 #include "fdfs_kernels.hpp"
 #include "fdfs_md5.hpp"
+#include "fdfs_segcrc.hpp"
 
 #include <cstdlib>
 
@@ -358,6 +359,70 @@ constexpr int kPairProbeMax = 8192;
 __device__ uint64_t g_pair_probe[kPairProbeMax * 8];  // [wg][8]: 4 words above, then first chunk, its end, rounds
 #endif
 
+// CRC segment items (PairSegs): after the MD5 chunks the workgroup's waves
+// take 64 KiB segments of the offloaded files from the same queue, one per
+// wave at a time -- queue index nw + s is segment s -- so the CRC of the
+// largest files (whose loader lanes skipped it) is computed by the pairs
+// whose chunks ended first, while the largest MD5 chains still run, instead
+// of beside those chains on their SIMDs.  Each segment's
+// zero-init CRC (crc_segment, the wave's 64 lanes over 1 KiB each) is
+// advanced to its file's end and XORed into segs.crc[i] (CRC32_ex is linear
+// over GF(2); big_patch_kernel writes the files' crc_out).  Called by both
+// waves right after the chunk fetch that found no MD5 chunk (that fetch's
+// barriers end every use of sD / sbuf); `first` = that fetch's item, taken by
+// the MD5 wave.  The segmented kernel's tables replace the pair's: the
+// complemented slice tables for SAR (crc_seg_kernel's domain) and ADV4032 in
+// the staging buffer; the reduction tables are read from global memory.
+template <bool SAR>
+__device__ __forceinline__ void pair_crc_items(const PairSegs &segs, const uint8_t *base, const DevTables *tabs,
+                                               uint32_t *queue, uint32_t nw, uint32_t first, bool loader,
+                                               uint32_t *sD, const uint32_t *sT, uint32_t *sA)
+{
+    const uint32_t nb = *segs.nbig;
+    const uint64_t total = segs.seg_first[nb];
+    if (total == 0)
+        return;  // workgroup-uniform
+    if (SAR)
+        lds_fill(sD, &tabs->Dc[0][0], 16 * 256);
+    lds_fill(sA, &tabs->t.ADV4032[0][0], 4 * 256);
+    __syncthreads();
+    const int lane = threadIdx.x & 63;
+    const Rep8Lane R8 = rep8_lane(lane);  // unused by the TM 0 tables
+    const uint32_t K16 = tabs->t.K16;
+    const uint32_t *sR = &tabs->t.ADVRED[0][0][0];
+    uint64_t s = first;
+    if (loader) {  // the MD5 wave keeps the workgroup's item, the loader fetches its own
+        uint32_t got = 0;
+        if (lane == 0)
+            got = atomicAdd(queue, 1u);
+        s = (uint64_t)__shfl(got, 0) - nw;
+    }
+    while (s < total) {
+        uint32_t lo = 0, hi = nb;  // last i with seg_first[i] <= s
+        while (hi - lo > 1) {
+            const uint32_t mid = (lo + hi) >> 1;
+            if (segs.seg_first[mid] <= s)
+                lo = mid;
+            else
+                hi = mid;
+        }
+        const uint32_t i = lo;
+        const uint64_t k = s - segs.seg_first[i];
+        const uint64_t L = segs.sizes[i];
+        const uint64_t lo_b = k * kSegBytes;
+        const uint64_t hi_b = (L < lo_b + kSegBytes) ? L : lo_b + kSegBytes;
+        const uint32_t v = crc_segment<SAR, 0>(sD, sT, sA, sR, R8, K16, base + segs.offs[i] + lo_b, hi_b - lo_b,
+                                               k == 0, lane);
+        const uint32_t adv = advance_any(tabs, v, L - hi_b, lane);
+        if (lane == 0)
+            atomicXor(&segs.crc[i], adv ^ (k == 0 ? crc_final_const<SAR>(L) : 0u));
+        uint32_t got = 0;
+        if (lane == 0)
+            got = atomicAdd(queue, 1u);
+        s = (uint64_t)__shfl(got, 0) - nw;
+    }
+}
+
 // PM: probe mode, a template parameter so that the production
 // instantiation (PM 0) carries no probe branch; PM != 0 is instantiated only
 // in the probe build (make probes): 1 = MD5 wave at s_setprio 2, 2 = no CRC
@@ -369,7 +434,8 @@ __global__ __launch_bounds__(128) void md5_pair_kernel(
     const uint8_t *__restrict__ base, const uint64_t *__restrict__ offs,
     const uint64_t *__restrict__ sizes, const uint32_t *__restrict__ order, uint32_t n,
     const DevTables *__restrict__ tabs, const uint64_t *__restrict__ big_min_p, uint32_t *__restrict__ queue,
-    uint32_t *__restrict__ crc_out, uint8_t *__restrict__ sig_out, int32_t *__restrict__ codes_out)
+    uint32_t *__restrict__ crc_out, uint8_t *__restrict__ sig_out, int32_t *__restrict__ codes_out,
+    PairSegs segs)
 {
     constexpr int CH = kMd5Chunk;
     constexpr int PIECES = CH / 16;
@@ -402,6 +468,7 @@ __global__ __launch_bounds__(128) void md5_pair_kernel(
     if constexpr (PM == 5)
         pr_t0 = wall_clock64();
 #endif
+    uint32_t first_item = 0;  // the queue index past the MD5 chunks that ended the loop
     for (;;) {
         if (threadIdx.x == 64)
             s_chunk = atomicAdd(queue, 1u);
@@ -422,6 +489,7 @@ __global__ __launch_bounds__(128) void md5_pair_kernel(
                 }
             }
 #endif
+            first_item = chunk - nw;
             break;
         }
         if constexpr (PM == 4) {
@@ -586,13 +654,16 @@ __global__ __launch_bounds__(128) void md5_pair_kernel(
             }
         }
     }
+    if (segs.nbig)
+        pair_crc_items<SAR>(segs, base, tabs, queue, nw, first_item, loader, sD, sT,
+                            reinterpret_cast<uint32_t *>(&sbuf[0][0]));
 }
 
 hipError_t launch_md5_stage(bool sar, const uint8_t *base, const uint64_t *offs,
                             const uint64_t *sizes, uint32_t n, const uint32_t *order,
                             const DevTables *tabs, const uint64_t *big_min, uint32_t *queue, uint32_t *crc_out,
                             uint8_t *sig_out, int32_t *codes_out, fdfs_gpu_file_state *states,
-                            const uint32_t *sidx, unsigned ncu, hipStream_t st)
+                            const uint32_t *sidx, unsigned ncu, const PairSegs *segs, hipStream_t st)
 {
     if (ncu == 0)
         return hipErrorInvalidValue;
@@ -619,11 +690,12 @@ hipError_t launch_md5_stage(bool sar, const uint8_t *base, const uint64_t *offs,
     if (pair != 0 && mode != 0 && queue && !states) {  // queue zeroed by the caller
         const unsigned g = 4u * ncu;
         const unsigned grid2 = g < nw ? g : nw;
+        const PairSegs ps = segs ? *segs : PairSegs{};
 #define PAIR_LAUNCH(PM)                                                                                       \
     (sar ? md5_pair_kernel<true, PM><<<grid2, 128, 0, st>>>(base, offs, sizes, order, n, tabs, big_min, queue, \
-                                                           crc_out, sig_out, codes_out)                      \
+                                                           crc_out, sig_out, codes_out, ps)                  \
          : md5_pair_kernel<false, PM><<<grid2, 128, 0, st>>>(base, offs, sizes, order, n, tabs, big_min, queue, \
-                                                            crc_out, sig_out, codes_out))
+                                                            crc_out, sig_out, codes_out, ps))
 #ifdef FDFS_PROBES
         if (pair == 2)
             PAIR_LAUNCH(1);

@@ -75,7 +75,14 @@ def test_config3_full_batch(oracle, ctxs):
         assert c == crc_np[i] and s == sig_np[i].tobytes(), i
         assert sig_np[i, 8:].tobytes() == hashlib.md5(d.tobytes()).digest(), i
         assert int.from_bytes(sig_np[i, :8].tobytes(), "big") == sizes[i]
-    del data, crc, sig
+    # every file's CRC (the pair kernel's loader lanes, or for the largest
+    # files the CRC segment items its queue hands out after the MD5 chunks)
+    # equals the segmented CRC-only path's
+    crc0, _, _ = ctxs[0].sig_batch(data, offs_t, sizes_t, method=0, check_bounds=False)
+    torch.cuda.synchronize()
+    bad = np.flatnonzero(crc0.cpu().numpy().view(np.uint32) != crc_np)
+    assert bad.size == 0, (bad.size, bad[:8], sizes[bad[:8]])
+    del data, crc, sig, crc0
     torch.cuda.empty_cache()
 
 
