@@ -329,9 +329,15 @@ __global__ __launch_bounds__(64 * kMd5Waves) void md5_stage_kernel(
 // Four workgroups per CU (35.8 KB of LDS each), the same 64 MD5 lanes per
 // SIMD as the fused form's one wave per SIMD.
 // Issue priority from a wave-uniform count of remaining 128-byte rounds
-// (probe PM 6): the pairs with the most work left issue first on their
-// SIMDs, against the hardware's oldest-wave-first default (which starves the
-// workgroups dispatched last, scripts/pair_timeline.py).
+// (production; probe PM 6 leaves it out): the waves with the most work left
+// issue first on their SIMDs -- longest-remaining-first, the LPT rule applied
+// to the SIMD's issue arbiter -- against the hardware's oldest-wave-first
+// default, which favours the workgroups dispatched first whatever they have
+// left.  Every SIMD holds an MD5 wave and a loader wave of two different
+// chunks, so a chunk with 3 MiB to go outranks one about to end.
+// Config 3: 80.0 / 80.6 against 83.4 / 83.0 ms, alternating on one box
+// (profiles/r04/probes_r04b.txt, c3_p7 against c3_p1).  Re-evaluated every
+// 256 rounds (32 KiB per file), in 1 MiB units.
 __device__ __forceinline__ void prio_by_remaining(uint64_t rem)
 {
     const uint32_t q = __builtin_amdgcn_readfirstlane((uint32_t)(rem >> 13));  // 8K-round units
@@ -428,7 +434,9 @@ __device__ __forceinline__ void pair_crc_items(const PairSegs &segs, const uint8
 // in the probe build (make probes): 1 = MD5 wave at s_setprio 2, 2 = no CRC
 // arithmetic, 3 = no MD5 arithmetic (wrong results), 4 = both waves at
 // s_setprio 2 while their chunk is among the largest quarter (the chunks
-// that end the batch), 0 after.
+// that end the batch), 0 after; 5 = per-workgroup timeline; 6 = no issue
+// priority (round 3's production form); 7 = young chunks first.  PM 0
+// (production) sets the longest-remaining-first priority (prio_by_remaining).
 template <bool SAR, int PM>
 __global__ __launch_bounds__(128) void md5_pair_kernel(
     const uint8_t *__restrict__ base, const uint64_t *__restrict__ offs,
@@ -585,7 +593,7 @@ __global__ __launch_bounds__(128) void md5_pair_kernel(
             };
             issue(RA, 0);
             for (uint64_t r = 0; r < rounds; r += 2) {
-                if constexpr (PM == 6) {
+                if constexpr (PM == 0) {
                     if ((r & 255) == 0)
                         prio_by_remaining(rounds - r);
                 }
@@ -614,7 +622,7 @@ __global__ __launch_bounds__(128) void md5_pair_kernel(
             uint32_t st[4] = {0x67452301u, 0xefcdab89u, 0x98badcfeu, 0x10325476u};  // my_md5_init
             const uint8_t *mine = &sbuf[0][0] + lane * STRIDE;
             for (uint64_t r = 0; r < rounds; r++) {
-                if constexpr (PM == 6) {
+                if constexpr (PM == 0) {
                     if ((r & 255) == 0)
                         prio_by_remaining(rounds - r);
                 }

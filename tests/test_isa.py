@@ -34,12 +34,14 @@ def test_no_valu_to_dpp_or_mfma_hazard(isa):
 def test_shipped_kernels_carry_no_probe_code(isa):
     """the probe knobs are compiled into the probe build only.
     The production md5_pair_kernel is the PM 0 instantiation alone (PM is a
-    template parameter) and no shipped kernel changes its issue priority
-    (s_setprio was a probe of round 3)."""
+    template parameter).  Round 4 made its longest-remaining-first issue
+    priority production (prio_by_remaining): md5_pair_kernel is
+    the only shipped kernel that changes its priority."""
     pair = [k for k in isa["names"] if "md5_pair_kernel" in k]
     assert pair, "md5_pair_kernel not found in the shipped code object"
     assert all(("Lb1ELi0E" in k or "Lb0ELi0E" in k) for k in pair), pair
-    assert isa["setprio"] == {}, isa["setprio"]
+    assert isa["setprio"], "the pair kernel's priority policy is missing"
+    assert all("md5_pair_kernel" in k for k in isa["setprio"]), isa["setprio"]
 
 
 DPP = "v_cndmask_b32_dpp v6, v5, v7, vcc quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf"
