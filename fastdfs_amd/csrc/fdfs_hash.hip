@@ -514,6 +514,295 @@ __global__ __launch_bounds__(TM == 2 || MODE == 5 ? 1024 : kHashBlock) __attribu
         reinterpret_cast<int4 *>(codes_out)[f] = make_int4((int)c, (int)e, (int)s, (int)t);
 }
 
+// ---------------------------------------------------------------------------
+// sig_split_kernel: the role-split form of sig_hash_kernel (VERDICT r03 item
+// 2).  A 1024-thread workgroup per CU: waves 0-3 are loaders (one per SIMD:
+// a workgroup's waves are dealt to the SIMDs cyclically), waves 4-15 hash
+// 12 x 64 files of the size-sorted order.  Every 128-byte step ("round") of
+// the 768 files: each loader has its three hash waves' lines in registers
+// (24 x 16 B per lane, cooperative: 8 lanes read one file's whole line, one
+// load instruction reads the lines of 8 files), writes them to one LDS row
+// per file (144-byte stride: ds_write_b128 and ds_read_b128 conflict-free),
+// and issues the next round's loads; the hash waves read their rows and run
+// CRC (slice-by-16), ELF and the MFMA polynomial planes exactly as
+// sig_hash_kernel's step does -- but never wait on HBM, carry no load
+// registers and no quad transposes.  Two barriers per round (rows full, rows
+// read), lgkmcnt only, so the loaders' next loads stay in flight across them;
+// the 768 files of a workgroup are consecutive in the size order (near-equal
+// sizes), so the lockstep costs little.  Bound (profiles/r04/probes_r04b.txt):
+// the compute-only hash kernel at three waves per SIMD without transposes
+// takes 6.22 ms on config 2, the loads alone ~6.1 ms, sig_hash_kernel 8.8 ms.
+// The head (to 16-byte alignment), lead (to 128-byte alignment) and tail
+// bytes are lane-serial from global memory, as in sig_hash_kernel, so the
+// loaders' lines are whole aligned 128-byte lines.
+// chain16 with the XORs as __builtin_amdgcn_bitop3_b32 instead of the xor3
+// asm statement: the split kernel's hash loop holds no inline asm at all, so
+// hipcc sees every instruction between its MFMAs and pads every hazard itself
+// (its accumulators are VGPRs: a 1024-thread workgroup leaves 128 registers
+// per wave, and hipcc then picks the VGPR form of the MFMAs).
+template <bool SAR>
+__device__ __forceinline__ uint32_t chain16_b(const uint32_t *__restrict__ D, uint32_t c, uint4 w, uint32_t K16)
+{
+    auto x3 = [](uint32_t a, uint32_t b, uint32_t d) { return __builtin_amdgcn_bitop3_b32(a, b, d, 0x96); };
+    const uint32_t x = c ^ w.x;
+    uint32_t r0 = x3(D[0 * 256 + (x & 0xFFu)], D[1 * 256 + ((x >> 8) & 0xFFu)], D[2 * 256 + ((x >> 16) & 0xFFu)]);
+    uint32_t r1 = x3(D[3 * 256 + (x >> 24)], D[4 * 256 + (w.y & 0xFFu)], D[5 * 256 + ((w.y >> 8) & 0xFFu)]);
+    uint32_t r2 = x3(D[6 * 256 + ((w.y >> 16) & 0xFFu)], D[7 * 256 + (w.y >> 24)], D[8 * 256 + (w.z & 0xFFu)]);
+    uint32_t r3 = x3(D[9 * 256 + ((w.z >> 8) & 0xFFu)], D[10 * 256 + ((w.z >> 16) & 0xFFu)], D[11 * 256 + (w.z >> 24)]);
+    r0 = x3(r0, D[12 * 256 + (w.w & 0xFFu)], D[13 * 256 + ((w.w >> 8) & 0xFFu)]);
+    r1 = x3(r1, D[14 * 256 + ((w.w >> 16) & 0xFFu)], D[15 * 256 + (w.w >> 24)]);
+    uint32_t r = x3(r0, r1, r2) ^ r3;
+    if (SAR)
+        r ^= (uint32_t)((int32_t)c >> 31) & K16;
+    return r;
+}
+
+constexpr int kSplitHash = 12;                     // hash waves per workgroup
+constexpr int kSplitLoad = 4;                      // loader waves
+constexpr int kSplitThreads = 64 * (kSplitHash + kSplitLoad);
+constexpr uint32_t kSplitFiles = 64 * kSplitHash;  // files per workgroup
+constexpr int kSplitRow = 144;                     // LDS row stride (128 B + 16 pad)
+static_assert(kSplitHash == 3 * kSplitLoad, "each loader serves three hash waves");
+
+__device__ __forceinline__ void split_barrier()
+{
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+}
+
+template <bool SAR>
+__global__ __launch_bounds__(kSplitThreads) void sig_split_kernel(
+    const uint8_t *__restrict__ base, const uint64_t *__restrict__ offs,
+    const uint64_t *__restrict__ sizes, const uint32_t *__restrict__ order, uint32_t n,
+    const DevTables *__restrict__ tabs, const uint64_t *__restrict__ big_min_p,
+    uint32_t *__restrict__ crc_out, uint8_t *__restrict__ sig_out, int32_t *__restrict__ codes_out)
+{
+    constexpr int SV = 8;
+    __shared__ uint32_t sD[16 * 256];
+    __shared__ uint32_t sT[256];
+    __shared__ uint4 sB[2 * SV * 64];
+    __shared__ __attribute__((aligned(16))) uint8_t rows[kSplitHash][64 * kSplitRow];
+    __shared__ ulonglong2 wins[kSplitFiles];  // per file: {first line, end of the last whole line}
+    __shared__ uint32_t s_nround;
+    lds_fill(sD, &tabs->t.D[0][0], 16 * 256);
+    lds_fill(sT, tabs->t.T, 256);
+#pragma unroll
+    for (int h = 0; h < 2; h++)
+        lds_fill(reinterpret_cast<uint32_t *>(sB + h * SV * 64),
+                 reinterpret_cast<const uint32_t *>(&tabs->pm.B[h][0][0][0]), SV * 64 * 4);
+    if (threadIdx.x == 0)
+        s_nround = 0;
+    __syncthreads();
+
+    typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+    const int lane = threadIdx.x & 63;
+    const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const uint8_t *safe = reinterpret_cast<const uint8_t *>(tabs);  // >= 128 readable bytes
+    const uint32_t f0 = blockIdx.x * kSplitFiles;
+
+    if (wv < kSplitLoad) {  // ---------------------------------------- loader
+        split_barrier();  // the hash waves' windows are in `wins`
+        const uint32_t nround = s_nround;
+        const int piece = lane & 7, fsub = lane >> 3;
+        u32x4 R[3][8];
+        auto issue = [&](uint32_t r) {
+#pragma unroll
+            for (int j = 0; j < 3; j++) {
+#pragma unroll
+                for (int k = 0; k < 8; k++) {
+                    const ulonglong2 wd = wins[(wv + kSplitLoad * j) * 64 + 8 * k + fsub];
+                    const uint64_t a = wd.x + 128ull * r;
+                    const uint8_t *ln = (a < wd.y ? reinterpret_cast<const uint8_t *>(a) : safe) + 16 * piece;
+                    asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(R[j][k]) : "v"(ln) : "memory");
+                }
+            }
+        };
+        if (nround)
+            issue(0);
+        for (uint32_t r = 0; r < nround; r++) {
+            asm volatile("s_waitcnt vmcnt(0)"
+                         : "+v"(R[0][0]), "+v"(R[0][1]), "+v"(R[0][2]), "+v"(R[0][3]), "+v"(R[0][4]),
+                           "+v"(R[0][5]), "+v"(R[0][6]), "+v"(R[0][7]), "+v"(R[1][0]), "+v"(R[1][1]),
+                           "+v"(R[1][2]), "+v"(R[1][3]), "+v"(R[1][4]), "+v"(R[1][5]), "+v"(R[1][6]),
+                           "+v"(R[1][7]), "+v"(R[2][0]), "+v"(R[2][1]), "+v"(R[2][2]), "+v"(R[2][3]),
+                           "+v"(R[2][4]), "+v"(R[2][5]), "+v"(R[2][6]), "+v"(R[2][7])
+                         :: "memory");
+#pragma unroll
+            for (int j = 0; j < 3; j++) {
+                uint8_t *tile = rows[wv + kSplitLoad * j];
+#pragma unroll
+                for (int k = 0; k < 8; k++)
+                    *reinterpret_cast<u32x4 *>(tile + (8 * k + fsub) * kSplitRow + 16 * piece) = R[j][k];
+            }
+            split_barrier();  // X: rows of round r full (and R free: lgkmcnt(0))
+            if (r + 1 < nround)
+                issue(r + 1);
+            split_barrier();  // Y: the hash waves have read round r
+        }
+        return;
+    }
+
+    // ------------------------------------------------------------------ hash
+    const int hw = wv - kSplitLoad;
+    const uint32_t i = f0 + hw * 64 + lane;
+    bool valid = i < n;
+    const uint32_t K16 = tabs->t.K16;
+    const Rep8Lane R8 = rep8_lane(lane);  // unused by the TM 0 tables
+    uint32_t f = valid ? order[i] : 0;
+    if (f >= n) {  // a stale order entry (the binning flagged it): no file
+        valid = false;
+        f = 0;
+    }
+    const uint64_t L = valid ? sizes[f] : 0;
+    const uint8_t *p = valid ? base + offs[f] : safe;
+    uint32_t c = 0xFFFFFFFFu;      // CRC32_XINIT (storage/storage_service.c:7149)
+    uint32_t e = 0, s = 0, t = 0;  // INIT_HASH_CODES4 (storage/storage_service.c:7156)
+    const uint64_t big_min = big_min_p ? *big_min_p : ~0ull;
+    const bool small = L < big_min;
+    uint64_t head = (16u - ((uintptr_t)p & 15u)) & 15u;
+    if (head > L)
+        head = L;
+    for (uint64_t k = 0; k < head; k++) {
+        const uint32_t b = p[k];
+        if (small)
+            c = crc_byte<SAR>(sT, c, b);
+        h3_byte<SAR>(b, e, s, t);
+    }
+    const uint4 *v = reinterpret_cast<const uint4 *>(p + head);
+    const uint64_t nvec = (L - head) >> 4;
+    uint64_t lead = ((128u - ((uintptr_t)v & 127u)) & 127u) >> 4;
+    if (lead > nvec)
+        lead = nvec;
+    for (uint64_t j = 0; j < lead; j++)
+        h4_lane<SAR, 0>(sD, R8, K16, v[j], small, c, e, s, t);
+    const uint32_t nsteps = (uint32_t)((nvec - lead) / SV);
+    {
+        const uint64_t w0 = reinterpret_cast<uint64_t>(v + lead);
+        wins[hw * 64 + lane] = make_ulonglong2(w0, w0 + 128ull * nsteps);
+    }
+    uint32_t nmax = nsteps, nfull = small ? nsteps : 0;
+#pragma unroll
+    for (int o = 32; o; o >>= 1) {
+        const uint32_t y = __shfl_xor(nmax, o), z = __shfl_xor(nfull, o);
+        nmax = y > nmax ? y : nmax;
+        nfull = z > nfull ? z : nfull;
+    }
+    if (lane == 0)
+        atomicMax(&s_nround, nmax);
+    split_barrier();
+    const uint32_t nround = s_nround;
+
+    const uint32_t m31 = tabs->pm.m128[0], m33 = tabs->pm.m128[1];
+    const int col = lane & 15, jj = col & 3, g = col >> 2;
+    const int32_t kk31 = tabs->pm.K[0][jj], kk33 = tabs->pm.K[1][jj];
+    const i32x4 k31 = {kk31, kk31, kk31, kk31};
+    const i32x4 k33 = {kk33, kk33, kk33, kk33};
+    i32x4 C31 = {0, 0, 0, 0}, C33 = {0, 0, 0, 0};
+#pragma unroll
+    for (int r = 0; r < 4; r++) {
+        const int src = 16 * g + 4 * (lane >> 4) + r;
+        const uint32_t s0 = __shfl(s, src), t0 = __shfl(t, src);
+        C31[r] = jj == 0 ? (int)s0 : 0;
+        C33[r] = jj == 0 ? (int)t0 : 0;
+    }
+    uint32_t nexec = 0;
+    const uint8_t *mine = rows[hw] + lane * kSplitRow;
+    for (uint32_t r = 0; r < nround; r++) {
+        split_barrier();  // X: round r's rows are in LDS
+        uint4 a[SV];
+        if (r < nmax) {
+#pragma unroll
+            for (int q = 0; q < SV; q++)
+                a[q] = *reinterpret_cast<const uint4 *>(mine + 16 * q);
+        }
+        split_barrier();  // Y: rows read (lgkmcnt(0)); the loaders may refill
+        if (r >= nmax)
+            continue;
+        const bool ok = r < nsteps;
+        if (r < nfull) {
+            const bool mon = __any(ok && small);
+            nexec += mon ? 1u : 0u;
+            if (mon) {
+#pragma unroll
+                for (int k = 0; k < 4; k++) {
+                    C31[k] = (int)((uint32_t)C31[k] * m31) + k31[k];
+                    C33[k] = (int)((uint32_t)C33[k] * m33) + k33[k];
+                }
+            }
+#pragma unroll
+            for (int q = 0; q < SV; q++) {
+                const uint4 aq = a[q];
+                if (ok) {  // no inline asm here (see chain16_b)
+                    if (small)
+                        c = chain16_b<SAR>(sD, c, aq, K16);
+                    elf_word4_chain<SAR, false>(aq.x, e);
+                    elf_word4_chain<SAR, false>(aq.y, e);
+                    elf_word4_chain<SAR, false>(aq.z, e);
+                    elf_word4_chain<SAR, true>(aq.w, e);
+                }
+                if (!mon)
+                    continue;
+                const uint32_t msk = ok ? 0xFFFFFFFFu : 0u;
+                const i32x4 A = {(int)and_xor80(aq.x, msk), (int)and_xor80(aq.y, msk),
+                                 (int)and_xor80(aq.z, msk), (int)and_xor80(aq.w, msk)};
+                const uint4 b31 = sB[(0 * SV + q) * 64 + lane], b33 = sB[(1 * SV + q) * 64 + lane];
+                const i32x4 B31 = {(int)b31.x, (int)b31.y, (int)b31.z, (int)b31.w};
+                const i32x4 B33 = {(int)b33.x, (int)b33.y, (int)b33.z, (int)b33.w};
+                C31 = __builtin_amdgcn_mfma_i32_16x16x64_i8(A, B31, C31, 0, 0, 0);
+                C33 = __builtin_amdgcn_mfma_i32_16x16x64_i8(A, B33, C33, 0, 0, 0);
+            }
+        } else if (ok) {  // waves of big files past their small lanes: ELF alone
+#pragma unroll
+            for (int q = 0; q < SV; q++) {
+                elf_word4_chain<SAR, false>(a[q].x, e);
+                elf_word4_chain<SAR, false>(a[q].y, e);
+                elf_word4_chain<SAR, false>(a[q].z, e);
+                elf_word4_chain<SAR, true>(a[q].w, e);
+            }
+        }
+    }
+    if (nmax) {  // planes -> value, back to the file's lane, padded steps undone
+        uint32_t s31 = 0, s33 = 0;
+#pragma unroll
+        for (int r = 0; r < 4; r++) {
+            uint32_t x = (uint32_t)C31[r] << (8 * jj), y = (uint32_t)C33[r] << (8 * jj);
+            x += __shfl_xor(x, 1);
+            y += __shfl_xor(y, 1);
+            x += __shfl_xor(x, 2);
+            y += __shfl_xor(y, 2);
+            const int src = 4 * (lane >> 4) + 16 * ((lane & 15) >> 2);
+            const uint32_t xs = __shfl(x, src), ys = __shfl(y, src);
+            if ((lane & 3) == r) {
+                s31 = xs;
+                s33 = ys;
+            }
+        }
+        const uint32_t pad = nexec - nsteps;  // (garbage for big-file lanes: patched)
+        s = s31 * pow_dev(tabs->pm.inv128[0], pad);
+        t = s33 * pow_dev(tabs->pm.inv128[1], pad);
+    }
+    for (uint64_t jv = lead + SV * (uint64_t)nsteps; jv < nvec; jv++)
+        h4_lane<SAR, 0>(sD, R8, K16, v[jv], small, c, e, s, t);
+    for (uint64_t k = head + (nvec << 4); k < L; k++) {  // the last (L - head) & 15 bytes
+        const uint32_t b = p[k];
+        if (small)
+            c = crc_byte<SAR>(sT, c, b);
+        h3_byte<SAR>(b, e, s, t);
+    }
+    if (!valid)
+        return;
+    c ^= 0xFFFFFFFFu;  // CRC32_FINAL / FINISH_HASH_CODES4 (storage/storage_dio.c:500,508)
+    if (small)
+        crc_out[f] = c;  // else big_patch_kernel puts the segmented CRC in all three outputs
+    if (sig_out) {  // STORAGE_GEN_FILE_SIGNATURE (storage/storage_service.c:106-120)
+        uint2 *sp = reinterpret_cast<uint2 *>(sig_out + 24ull * f);
+        sp[0] = make_uint2(bswap32((uint32_t)(L >> 32)), bswap32((uint32_t)L));
+        sp[1] = make_uint2(bswap32(c), bswap32(e));
+        sp[2] = make_uint2(bswap32(s), bswap32(t));
+    }
+    if (codes_out)
+        reinterpret_cast<int4 *>(codes_out)[f] = make_int4((int)c, (int)e, (int)s, (int)t);
+}
+
 // simple_hash_ex / Time33Hash_ex of the big files (>= T), segment-parallel
 // (INIT_HASH_CODES4 starts both at 0, so a file's hash is the polynomial
 // sum_pos b_pos M^(L-1-pos) mod 2^32 and splits over any cut).  One wave per
@@ -620,6 +909,7 @@ hipError_t launch_sig_hash(bool sar, const uint8_t *base, const uint64_t *offs,
     }
 #else
     [[maybe_unused]] constexpr int tm = 0;
+    [[maybe_unused]] constexpr int mode = 0;
 #endif
 #ifdef FDFS_PROBES
     static int ql = -1;  // FDFS_GPU_HASH_QUAD=0: round-2 lane-per-file loads
@@ -645,6 +935,25 @@ hipError_t launch_sig_hash(bool sar, const uint8_t *base, const uint64_t *offs,
     constexpr unsigned shm = 0;
 #endif
     const unsigned grid = (n + blk - 1) / blk;
+#ifdef FDFS_PROBES
+    static int split = -1;  // FDFS_GPU_HASH_SPLIT=1: the role-split kernel (one-shot batches)
+    if (split < 0) {
+        const char *ev = getenv("FDFS_GPU_HASH_SPLIT");
+        split = ev ? atoi(ev) : 0;
+    }
+#else
+    constexpr int split = 0;
+#endif
+    if (split && !states && mode == 0 && tm == 0) {
+        const unsigned g2 = (n + kSplitFiles - 1) / kSplitFiles;
+        if (sar)
+            sig_split_kernel<true><<<g2, kSplitThreads, 0, st>>>(base, offs, sizes, order, n, tabs, big_min, crc_out,
+                                                               sig_out, codes_out);
+        else
+            sig_split_kernel<false><<<g2, kSplitThreads, 0, st>>>(base, offs, sizes, order, n, tabs, big_min, crc_out,
+                                                                sig_out, codes_out);
+        return hipGetLastError();
+    }
 #ifdef FDFS_PROBES
 #define HASH_LAUNCH_TM2(S, M)                                                                            \
     else if (tm == 2)                                                                                    \
