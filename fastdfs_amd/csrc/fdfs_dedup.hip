@@ -1077,13 +1077,11 @@ hipError_t launch_dedup_group(const uint8_t *sig, uint32_t sig_stride, const uin
         defs = ev ? atoi(ev) : 0;
     }
     const bool split_def = defs == 1;
-#else
-    constexpr bool split_def = false;
-#endif
     if (split_def)
         dp_tile_kernel<false><<<(unsigned)pl.tiles, kDpTileThreads, 0, st>>>(sig, sig_stride, gidx, gidx_stride, n,
                                                                              pl.d1, pl.tiles, ent1, out, cnt1, loc1);
     else
+#endif
         dp_tile_kernel<true><<<(unsigned)pl.tiles, kDpTileThreads, 0, st>>>(sig, sig_stride, gidx, gidx_stride, n,
                                                                             pl.d1, pl.tiles, ent1, out, cnt1, loc1);
     if ((e = launch_exclusive_scan(cnt1, ncnt, off1, bsum, st)) != hipSuccess)
@@ -1093,10 +1091,17 @@ hipError_t launch_dedup_group(const uint8_t *sig, uint32_t sig_stride, const uin
 #define DP_SPLIT(NB, D)                                                                                  \
     dp_split_kernel<NB, D><<<(unsigned)pl.chunks, kDpSplitThreads, 0, st>>>(                             \
         ent1, pl.d1, pl.d2, pl.tiles, off1, loc1, cb, chunk_ta, chunk_hd, ent2, cdo, out, gidx, gidx_stride, n)
+#ifdef FDFS_PROBES
     if (pl.d2 <= 10)
         split_def ? DP_SPLIT(1024, true) : DP_SPLIT(1024, false);
     else
         split_def ? DP_SPLIT(1 << kDpMaxD2, true) : DP_SPLIT(1 << kDpMaxD2, false);
+#else  // dp_tile writes the singleton answers (the DEF form measured neutral)
+    if (pl.d2 <= 10)
+        DP_SPLIT(1024, false);
+    else
+        DP_SPLIT(1 << kDpMaxD2, false);
+#endif
 #undef DP_SPLIT
     const int gmode = !gidx_stride ? GM_INDEX
                       : (gidx == reinterpret_cast<const uint64_t *>(sig + 24) && 8 * gidx_stride == sig_stride)

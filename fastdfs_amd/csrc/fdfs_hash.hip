@@ -514,6 +514,7 @@ __global__ __launch_bounds__(TM == 2 || MODE == 5 ? 1024 : kHashBlock) __attribu
         reinterpret_cast<int4 *>(codes_out)[f] = make_int4((int)c, (int)e, (int)s, (int)t);
 }
 
+#ifdef FDFS_PROBES  // measured, not kept: the probe build only
 // ---------------------------------------------------------------------------
 // sig_split_kernel: the role-split form of sig_hash_kernel (VERDICT r03 item
 // 2).  A 1024-thread workgroup per CU: waves 0-3 are loaders (one per SIMD:
@@ -802,6 +803,7 @@ __global__ __launch_bounds__(kSplitThreads) void sig_split_kernel(
     if (codes_out)
         reinterpret_cast<int4 *>(codes_out)[f] = make_int4((int)c, (int)e, (int)s, (int)t);
 }
+#endif
 
 // simple_hash_ex / Time33Hash_ex of the big files (>= T), segment-parallel
 // (INIT_HASH_CODES4 starts both at 0, so a file's hash is the polynomial
@@ -941,9 +943,8 @@ hipError_t launch_sig_hash(bool sar, const uint8_t *base, const uint64_t *offs,
         const char *ev = getenv("FDFS_GPU_HASH_SPLIT");
         split = ev ? atoi(ev) : 0;
     }
-#else
-    constexpr int split = 0;
 #endif
+#ifdef FDFS_PROBES
     if (split && !states && mode == 0 && tm == 0) {
         const unsigned g2 = (n + kSplitFiles - 1) / kSplitFiles;
         if (sar)
@@ -954,6 +955,7 @@ hipError_t launch_sig_hash(bool sar, const uint8_t *base, const uint64_t *offs,
                                                                 sig_out, codes_out);
         return hipGetLastError();
     }
+#endif
 #ifdef FDFS_PROBES
 #define HASH_LAUNCH_TM2(S, M)                                                                            \
     else if (tm == 2)                                                                                    \
