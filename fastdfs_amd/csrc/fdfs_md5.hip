@@ -435,7 +435,8 @@ __device__ __forceinline__ void pair_crc_items(const PairSegs &segs, const uint8
 // arithmetic, 3 = no MD5 arithmetic (wrong results), 4 = both waves at
 // s_setprio 2 while their chunk is among the largest quarter (the chunks
 // that end the batch), 0 after; 5 = per-workgroup timeline; 6 = no issue
-// priority (round 3's production form); 7 = young chunks first.  PM 0
+// priority (round 3's production form); 7 = young chunks first; 8 = static
+// boustrophedon chunk pairing (chunk w, then 2G - 1 - w).  PM 0
 // (production) sets the longest-remaining-first priority (prio_by_remaining).
 template <bool SAR, int PM>
 __global__ __launch_bounds__(128) void md5_pair_kernel(
@@ -477,9 +478,21 @@ __global__ __launch_bounds__(128) void md5_pair_kernel(
         pr_t0 = wall_clock64();
 #endif
     uint32_t first_item = 0;  // the queue index past the MD5 chunks that ended the loop
+    uint32_t kch = 0;         // chunks this workgroup has taken
     for (;;) {
-        if (threadIdx.x == 64)
-            s_chunk = atomicAdd(queue, 1u);
+        if (threadIdx.x == 64) {
+            if constexpr (PM == 8) {
+                // static boustrophedon pairing: workgroup w takes chunk w,
+                // then chunk 2G - 1 - w (the largest first chunks get no
+                // second one, the smallest get the largest of the rest), then
+                // the queue from 2G (batches of more than 2G chunks)
+                const uint32_t G = gridDim.x, c2 = 2 * G - 1 - blockIdx.x;
+                s_chunk = kch == 0 ? blockIdx.x : (kch == 1 && c2 < nw) ? c2 : 2 * G + atomicAdd(queue, 1u);
+            } else {
+                s_chunk = atomicAdd(queue, 1u);
+            }
+        }
+        kch++;
         __syncthreads();
         const uint32_t chunk = __builtin_amdgcn_readfirstlane(s_chunk);
         __syncthreads();  // s_chunk read by both waves before the next chunk's write
@@ -535,6 +548,21 @@ __global__ __launch_bounds__(128) void md5_pair_kernel(
         }
         const uint64_t rounds = (mx + BPR - 1) / BPR;
         const uint8_t *tp = p + (nblk << 6);
+        uint64_t after = 0;  // PM 8: rounds of the chunk this workgroup takes next (its priority counts them)
+        if constexpr (PM == 8) {
+            const uint32_t c2 = 2 * gridDim.x - 1 - blockIdx.x;
+            if (kch == 1 && c2 < nw) {
+                const uint32_t i2 = c2 * 64 + lane;
+                const uint32_t f2 = i2 < n ? order[i2] : n;
+                uint64_t m2 = f2 < n ? (sizes[f2] >> 6) : 0;
+#pragma unroll
+                for (int o = 32; o; o >>= 1) {
+                    const uint64_t y = __shfl_xor(m2, o);
+                    m2 = y > m2 ? y : m2;
+                }
+                after = (m2 + BPR - 1) / BPR;
+            }
+        }
 #ifdef FDFS_PROBES
         if constexpr (PM == 5) {
             if (threadIdx.x == 0 && blockIdx.x < kPairProbeMax) {
@@ -593,9 +621,9 @@ __global__ __launch_bounds__(128) void md5_pair_kernel(
             };
             issue(RA, 0);
             for (uint64_t r = 0; r < rounds; r += 2) {
-                if constexpr (PM == 0) {
+                if constexpr (PM == 0 || PM == 8) {
                     if ((r & 255) == 0)
-                        prio_by_remaining(rounds - r);
+                        prio_by_remaining(rounds - r + after);
                 }
                 issue(RB, r + 1);
                 stage(RA, sbuf[0]);
@@ -622,9 +650,9 @@ __global__ __launch_bounds__(128) void md5_pair_kernel(
             uint32_t st[4] = {0x67452301u, 0xefcdab89u, 0x98badcfeu, 0x10325476u};  // my_md5_init
             const uint8_t *mine = &sbuf[0][0] + lane * STRIDE;
             for (uint64_t r = 0; r < rounds; r++) {
-                if constexpr (PM == 0) {
+                if constexpr (PM == 0 || PM == 8) {
                     if ((r & 255) == 0)
-                        prio_by_remaining(rounds - r);
+                        prio_by_remaining(rounds - r + after);
                 }
                 pair_barrier();
                 const uint4 *q = reinterpret_cast<const uint4 *>(mine + (r & 1) * (64 * STRIDE));
@@ -671,219 +699,6 @@ __global__ __launch_bounds__(128) void md5_pair_kernel(
 #endif
 }
 
-#ifdef FDFS_PROBES
-// md5_multi_kernel (probe build, FDFS_GPU_MD5_PAIR 9 / 10): NP pairs per
-// workgroup sharing one copy of the slice tables, so more pairs fit a CU
-// (NP = 3: two workgroups, six pairs, three waves per SIMD; NP = 7: one
-// workgroup, seven pairs) -- config 3 is issue-throughput bound at two waves
-// per SIMD.  The pairs of a workgroup work on different chunks,
-// so they cannot share s_barrier: each pair synchronises through monotone
-// LDS counters instead (rounds staged by its loader, rounds read by its MD5
-// wave, chunks published / taken), polled with s_sleep.  A poll that runs
-// past ~0.5 s sets bit 1 of the lane error word and ends the wave (the call
-// then returns EIO) instead of hanging the GPU.
-__device__ __forceinline__ uint32_t lds_load(const uint32_t *p) { return __atomic_load_n(p, __ATOMIC_RELAXED); }
-__device__ __forceinline__ void lds_publish(uint32_t *p, uint32_t v)
-{
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // this wave's row writes / reads are done
-    __atomic_store_n(p, v, __ATOMIC_RELAXED);
-}
-__device__ __forceinline__ bool lds_wait_ge(const uint32_t *p, uint32_t target, uint32_t *err)
-{
-    for (uint32_t it = 0;; it++) {
-        if (lds_load(p) >= target)
-            return true;
-        if (it > (1u << 23)) {
-            atomicOr(err, 2u);
-            return false;
-        }
-        __builtin_amdgcn_s_sleep(1);
-    }
-}
-
-template <bool SAR, int NP>
-__global__ __launch_bounds__(128 * NP) void md5_multi_kernel(
-    const uint8_t *__restrict__ base, const uint64_t *__restrict__ offs,
-    const uint64_t *__restrict__ sizes, const uint32_t *__restrict__ order, uint32_t n,
-    const DevTables *__restrict__ tabs, const uint64_t *__restrict__ big_min_p, uint32_t *__restrict__ queue,
-    uint32_t *__restrict__ err, uint32_t *__restrict__ crc_out, uint8_t *__restrict__ sig_out,
-    int32_t *__restrict__ codes_out)
-{
-    constexpr int CH = kMd5Chunk;
-    constexpr int PIECES = CH / 16;
-    constexpr int FPI = 64 / PIECES;
-    constexpr int NLD = 64 / FPI;
-    constexpr int STRIDE = CH + 16;
-    constexpr int BPR = CH / 64;
-    static_assert(NLD == 8 && BPR == 2, "the asm waits below name 8 registers");
-    __shared__ uint32_t sD[16 * 256];
-    __shared__ uint32_t sT[256];
-    __shared__ __attribute__((aligned(16))) uint8_t sbuf[NP][2][64 * STRIDE];
-    __shared__ uint32_t stg[NP], rdn[NP], cseq[NP], cack[NP], cval[NP][2];
-    lds_fill(sD, &tabs->t.D[0][0], 16 * 256);
-    lds_fill(sT, tabs->t.T, 256);
-    if (threadIdx.x < NP) {
-        stg[threadIdx.x] = rdn[threadIdx.x] = cseq[threadIdx.x] = cack[threadIdx.x] = 0;
-    }
-    __syncthreads();
-    typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
-    const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const bool loader = wv >= NP;  // waves 0..NP-1: MD5 of pair wv; NP..2NP-1: loader of pair wv - NP
-    const int pr = loader ? wv - NP : wv;
-    const int lane = threadIdx.x & 63;
-    const uint32_t nw = (n + 63) / 64;
-    const uint8_t *safe = reinterpret_cast<const uint8_t *>(tabs);
-    const uint32_t K16 = tabs->t.K16;
-    const uint64_t big_min = big_min_p ? *big_min_p : ~0ull;
-    uint32_t g = 0;  // rounds of this pair so far (monotone across its chunks)
-    for (uint32_t k = 0;; k++) {
-        uint32_t chunk;
-        if (loader) {
-            uint32_t got = 0;
-            if (lane == 0)
-                got = atomicAdd(queue, 1u);
-            chunk = __shfl(got, 0);
-            if (k >= 1 && !lds_wait_ge(&cack[pr], k - 1, err))  // slot k & 1 free (chunk k - 2 taken)
-                return;
-            if (lane == 0)
-                cval[pr][k & 1] = chunk;
-            lds_publish(&cseq[pr], k + 1);
-        } else {
-            if (!lds_wait_ge(&cseq[pr], k + 1, err))
-                return;
-            chunk = __builtin_amdgcn_readfirstlane(lds_load(&cval[pr][k & 1]));
-            lds_publish(&cack[pr], k + 1);
-        }
-        if (chunk >= nw)
-            return;
-        const uint32_t i = chunk * 64 + lane;
-        bool valid = i < n;
-        uint32_t f = valid ? order[i] : 0;
-        if (f >= n) {
-            valid = false;
-            f = 0;
-        }
-        const uint64_t L = valid ? sizes[f] : 0;
-        const uint8_t *p = valid ? base + offs[f] : safe;
-        const uint64_t nblk = L >> 6;
-        uint64_t mx = nblk;
-#pragma unroll
-        for (int o = 32; o; o >>= 1) {
-            const uint64_t y = __shfl_xor(mx, o);
-            mx = y > mx ? y : mx;
-        }
-        const uint64_t rounds = (mx + BPR - 1) / BPR;
-        const uint8_t *tp = p + (nblk << 6);
-        if (loader) {
-            const bool small = L < big_min;
-            const int piece = lane % PIECES, fsub = lane / PIECES;
-            const uint8_t *lp[NLD];
-            uint64_t lim[NLD];
-#pragma unroll
-            for (int q = 0; q < NLD; q++) {
-                const int src = q * FPI + fsub;
-                lp[q] = reinterpret_cast<const uint8_t *>(__shfl((uintptr_t)p, src)) + piece * 16;
-                lim[q] = __shfl(nblk, src) * 4;
-            }
-            u32x4 RA[NLD], RB[NLD];
-            auto issue = [&](u32x4 (&R)[NLD], uint64_t r) {
-                const uint64_t rp = r * PIECES + piece;
-#pragma unroll
-                for (int q = 0; q < NLD; q++) {
-                    const uint8_t *a = (rp < lim[q]) ? lp[q] + r * CH : safe;
-                    asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(R[q]) : "v"(a) : "memory");
-                }
-            };
-            uint32_t c = 0xFFFFFFFFu;
-            bool ok = true;
-            // stage round r (global round gg) into sbuf[pr][gg & 1] once the
-            // MD5 wave has read round gg - 2 from it, then publish it
-            auto stage = [&](u32x4 (&R)[NLD], uint64_t r) -> bool {
-                const uint32_t gg = g + (uint32_t)r;
-                if (gg >= 2 && !lds_wait_ge(&rdn[pr], gg - 1, err))
-                    return false;
-                asm volatile("s_waitcnt vmcnt(8)" : "+v"(R[0]), "+v"(R[1]), "+v"(R[2]), "+v"(R[3]) :: "memory");
-                asm volatile("" : "+v"(R[4]), "+v"(R[5]), "+v"(R[6]), "+v"(R[7]));
-                uint8_t *tile = sbuf[pr][gg & 1];
-#pragma unroll
-                for (int q = 0; q < NLD; q++)
-                    *reinterpret_cast<u32x4 *>(tile + (q * FPI + fsub) * STRIDE + piece * 16) = R[q];
-                lds_publish(&stg[pr], gg + 1);
-                const uint4 *qv = reinterpret_cast<const uint4 *>(tile + lane * STRIDE);
-#pragma unroll
-                for (int b = 0; b < BPR; b++)
-                    if (small && r * BPR + b < nblk) {
-                        c = chain16<SAR>(sD, c, qv[4 * b + 0], K16);
-                        c = chain16<SAR>(sD, c, qv[4 * b + 1], K16);
-                        c = chain16<SAR>(sD, c, qv[4 * b + 2], K16);
-                        c = chain16<SAR>(sD, c, qv[4 * b + 3], K16);
-                    }
-                return true;
-            };
-            issue(RA, 0);
-            for (uint64_t r = 0; r < rounds && ok; r += 2) {
-                if ((r & 255) == 0)
-                    prio_by_remaining(rounds - r);
-                issue(RB, r + 1);
-                ok = stage(RA, r);
-                issue(RA, r + 2);
-                if (ok && r + 1 < rounds)
-                    ok = stage(RB, r + 1);
-            }
-            asm volatile("s_waitcnt vmcnt(0)"
-                         : "+v"(RA[0]), "+v"(RA[1]), "+v"(RA[2]), "+v"(RA[3]), "+v"(RA[4]), "+v"(RA[5]),
-                           "+v"(RA[6]), "+v"(RA[7]), "+v"(RB[0]), "+v"(RB[1]), "+v"(RB[2]), "+v"(RB[3]),
-                           "+v"(RB[4]), "+v"(RB[5]), "+v"(RB[6]), "+v"(RB[7]) :: "memory");
-            if (!ok)
-                return;
-            if (valid && small) {
-                const uint32_t rt = (uint32_t)(L & 63u);
-                for (uint32_t q = 0; q < rt; q++)
-                    c = crc_byte<SAR>(sT, c, tp[q]);
-                crc_out[f] = c ^ 0xFFFFFFFFu;  // CRC32_FINAL (storage/storage_dio.c:500)
-            }
-        } else {
-            uint32_t st[4] = {0x67452301u, 0xefcdab89u, 0x98badcfeu, 0x10325476u};  // my_md5_init
-            const uint8_t *mine = &sbuf[pr][0][0] + lane * STRIDE;
-            for (uint64_t r = 0; r < rounds; r++) {
-                if ((r & 255) == 0)
-                    prio_by_remaining(rounds - r);
-                const uint32_t gg = g + (uint32_t)r;
-                if (!lds_wait_ge(&stg[pr], gg + 1, err))
-                    return;
-                const uint4 *q = reinterpret_cast<const uint4 *>(mine + (gg & 1) * (64 * STRIDE));
-                uint4 blk[2][4];
-#pragma unroll
-                for (int b = 0; b < BPR; b++)
-#pragma unroll
-                    for (int kk = 0; kk < 4; kk++)
-                        blk[b][kk] = q[4 * b + kk];
-                lds_publish(&rdn[pr], gg + 1);  // this round's rows are in registers
-#pragma unroll
-                for (int b = 0; b < BPR; b++) {
-                    if (r * BPR + b < nblk) {
-                        const uint32_t m[16] = {blk[b][0].x, blk[b][0].y, blk[b][0].z, blk[b][0].w,
-                                                blk[b][1].x, blk[b][1].y, blk[b][1].z, blk[b][1].w,
-                                                blk[b][2].x, blk[b][2].y, blk[b][2].z, blk[b][2].w,
-                                                blk[b][3].x, blk[b][3].y, blk[b][3].z, blk[b][3].w};
-                        md5_compress(st, m);
-                    }
-                }
-            }
-            if (valid) {
-                md5_finish(st, tp, L);
-                if (sig_out)  // memcpy(sig + 8, md5 digest, 16) (storage/storage_service.c:119)
-                    store_sig(sig_out + 24ull * f, L, st[0], st[1], st[2], st[3]);
-                if (codes_out)
-                    reinterpret_cast<int4 *>(codes_out)[f] =
-                        make_int4((int)st[0], (int)st[1], (int)st[2], (int)st[3]);
-            }
-        }
-        g += (uint32_t)rounds;
-    }
-}
-#endif
-
 hipError_t launch_md5_stage(bool sar, const uint8_t *base, const uint64_t *offs,
                             const uint64_t *sizes, uint32_t n, const uint32_t *order,
                             const DevTables *tabs, const uint64_t *big_min, uint32_t *queue, uint32_t *crc_out,
@@ -922,21 +737,6 @@ hipError_t launch_md5_stage(bool sar, const uint8_t *base, const uint64_t *offs,
          : md5_pair_kernel<false, PM><<<grid2, 128, 0, st>>>(base, offs, sizes, order, n, tabs, big_min, queue, \
                                                             crc_out, sig_out, codes_out, ps))
 #ifdef FDFS_PROBES
-        if (pair == 9 || pair == 10) {  // md5_multi_kernel: 3 pairs x 2 workgroups / 7 pairs x 1 per CU
-            uint32_t *errw = queue + (kLaneErrWord - 2 * kSizeBins);
-            const unsigned gm = pair == 9 ? 2u * ncu : ncu;
-#define MULTI_LAUNCH(NP) \
-    (sar ? md5_multi_kernel<true, NP><<<gm, 128 * NP, 0, st>>>(base, offs, sizes, order, n, tabs, big_min, queue, errw, \
-                                                              crc_out, sig_out, codes_out) \
-         : md5_multi_kernel<false, NP><<<gm, 128 * NP, 0, st>>>(base, offs, sizes, order, n, tabs, big_min, queue, errw, \
-                                                               crc_out, sig_out, codes_out))
-            if (pair == 9)
-                MULTI_LAUNCH(3);
-            else
-                MULTI_LAUNCH(7);
-#undef MULTI_LAUNCH
-            return hipGetLastError();
-        }
         if (pair == 2)
             PAIR_LAUNCH(1);
         else if (pair == 3)
@@ -951,6 +751,8 @@ hipError_t launch_md5_stage(bool sar, const uint8_t *base, const uint64_t *offs,
             PAIR_LAUNCH(6);
         else if (pair == 8)
             PAIR_LAUNCH(7);
+        else if (pair == 9)
+            PAIR_LAUNCH(8);
         else
 #endif
             PAIR_LAUNCH(0);
