@@ -147,8 +147,9 @@ fdfs::BigCrcWs carve_big(const fdfs_gpu_ctx *ctx, Carve &cv, uint32_t n)
         sd = es ? atol(es) : 0;
     }
     big.md5_bin = (uint32_t)mb;
-    if (sd == 3) {  // 3: the CRC segments as md5_pair_kernel queue items
+    if (sd == 3 || sd == 4) {  // 3: the CRC segments as md5_pair_kernel queue items; 4: of the tail chunks
         big.md5_inline = true;
+        big.md5_tail = sd == 4;
     } else if (sd >= 1) {  // 2: enqueued after the lane kernel
         big.side = ctx->side;
         big.fork = ctx->fork;

@@ -55,6 +55,9 @@ struct BigCrcWs {  // device arrays of n entries (seg_first n + 1)
     // MD5 batches above lat_files: the offloaded files' CRC segments are items
     // of md5_pair_kernel's own queue after its MD5 chunks (no crc_seg launch)
     bool md5_inline = false;
+    // with md5_inline: offload the CRC of the tail chunks (those after the
+    // pair kernel's first G = its grid) instead of the files >= T
+    bool md5_tail = false;
 };
 // The CRC segment items md5_pair_kernel takes once its MD5 chunks are gone
 // (nbig == nullptr: none): the 64 KiB segments of big_plan_kernel's list
@@ -64,6 +67,10 @@ struct PairSegs {
     const uint32_t *nbig = nullptr;
     const uint64_t *offs = nullptr, *sizes = nullptr, *seg_first = nullptr;
     uint32_t *crc = nullptr;
+    // the loader lanes of chunks >= crc_chunks skip the CRC too (tail
+    // offload: the chunks taken after the first G, whose files big_plan's
+    // tail form lists)
+    uint32_t crc_chunks = ~0u;
 };
 hipError_t launch_poly_seg(const uint8_t *base, const uint64_t *boffs, const uint64_t *bsizes,
                            const uint64_t *seg_first, const uint32_t *nbig, uint32_t *bpoly,

@@ -581,7 +581,8 @@ __global__ __launch_bounds__(128) void md5_pair_kernel(
         pr_rounds += rounds;
 #endif
         if (loader) {
-            const bool small = L < big_min && PM != 2;  // else the CRC comes from crc_seg_kernel
+            // else the CRC comes from crc_seg_kernel or the CRC segment items
+            const bool small = L < big_min && chunk < segs.crc_chunks && PM != 2;
             const int piece = lane % PIECES, fsub = lane / PIECES;
             const uint8_t *lp[NLD];
             uint64_t lim[NLD];

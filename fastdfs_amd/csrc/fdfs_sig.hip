@@ -579,6 +579,66 @@ __global__ __launch_bounds__(1024) void big_plan_kernel(
         seg_first[nbig] = carry;
 }
 
+#ifdef FDFS_PROBES
+// Tail form of the list (probe, BigCrcWs::md5_tail): the files at order
+// positions [p0, n) -- the MD5 chunks taken after the pair kernel's first
+// G -- listed like big_plan_kernel lists the files >= T: compacted offsets
+// and sizes, the exclusive scan of their 64 KiB segment counts, zeroed CRC
+// slots; *nbig_out = n - p0 (one block).
+__global__ __launch_bounds__(1024) void tail_plan_kernel(
+    const uint32_t *__restrict__ order, const uint64_t *__restrict__ offs, const uint64_t *__restrict__ sizes,
+    uint32_t n, uint32_t p0, uint32_t *__restrict__ nbig_out, uint64_t *__restrict__ big_min,
+    uint64_t *__restrict__ boffs, uint64_t *__restrict__ bsizes, uint64_t *__restrict__ seg_first,
+    uint32_t *__restrict__ bcrc, uint32_t *__restrict__ err)
+{
+    __shared__ uint64_t wsum64[16];
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    const uint32_t m = n > p0 ? n - p0 : 0;
+    if (threadIdx.x == 0) {
+        *nbig_out = m;
+        *big_min = ~0ull;  // no size threshold
+    }
+    uint64_t carry = 0;
+    for (uint32_t i0 = 0; i0 < m; i0 += blockDim.x) {
+        const uint32_t i = i0 + threadIdx.x;
+        uint64_t ns = 0;
+        if (i < m) {
+            const uint32_t f = order[p0 + i];
+            const bool ok = f < n;
+            if (!ok)
+                atomicOr(err, 1u);
+            const uint64_t L = ok ? sizes[f] : 0;
+            boffs[i] = ok ? offs[f] : 0;
+            bsizes[i] = L;
+            bcrc[i] = 0;
+            ns = (L + kSegBytes - 1) / kSegBytes;
+        }
+        uint64_t x = ns;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const uint64_t y = __shfl_up(x, o);
+            if (lane >= o)
+                x += y;
+        }
+        if (lane == 63)
+            wsum64[wid] = x;
+        __syncthreads();
+        uint64_t before = carry;
+        for (int k = 0; k < wid; k++)
+            before += wsum64[k];
+        if (i < m)
+            seg_first[i] = before + x - ns;
+        uint64_t tot = 0;
+        for (int k = 0; k < (int)(blockDim.x >> 6); k++)
+            tot += wsum64[k];
+        carry += tot;
+        __syncthreads();
+    }
+    if (threadIdx.x == 0)
+        seg_first[m] = carry;
+}
+#endif
+
 // After the lane kernel: the big files' segmented CRC, simple_hash and
 // Time33 into crc_out, their signature fields and codes[0], [2], [3].
 __global__ void big_patch_kernel(const uint32_t *__restrict__ nbig, const uint32_t *__restrict__ order,
@@ -772,12 +832,18 @@ hipError_t launch_sig_lane(bool sar, int method, const uint8_t *base, const uint
     // CRC segments are md5_pair_kernel's own queue items (no segmented launch)
     const bool inline_segs = offload && method == 2 && !states && big->md5_inline && n > big->lat_files;
     PairSegs ps;
+    uint32_t tail_p0 = 0;  // md5_tail: the order position of the first offloaded file
     if (inline_segs) {
         ps.nbig = big->nbig;
         ps.offs = big->offs;
         ps.sizes = big->sizes;
         ps.seg_first = big->seg_first;
         ps.crc = big->crc;
+        if (big->md5_tail) {
+            const uint32_t nw = (n + 63) / 64, G = 4 * big->ncu < nw ? 4 * big->ncu : nw;
+            ps.crc_chunks = G;
+            tail_p0 = 64 * G < n ? 64 * G : n;
+        }
     }
     // the segmented passes over the files >= T (CRC; HASH: simple_hash,
     // Time33 too): before the lane kernel on `st`, or on big->side beside it
@@ -793,6 +859,12 @@ hipError_t launch_sig_lane(bool sar, int method, const uint8_t *base, const uint
         return e2;
     };
     if (offload) {
+#ifdef FDFS_PROBES
+        if (inline_segs && big->md5_tail)
+            tail_plan_kernel<<<1, 1024, 0, st>>>(order, offs, sizes, n, tail_p0, big->nbig, big->big_min, big->offs,
+                                                 big->sizes, big->seg_first, big->crc, err);
+        else
+#endif
         big_plan_kernel<<<1, 1024, 0, st>>>(hist, order, offs, sizes, n, method, big->lat_files, big->md5_bin,
                                             big->nbig, big->big_min, big->offs, big->sizes, big->seg_first,
                                             big->crc, big->poly, err);
@@ -825,8 +897,8 @@ hipError_t launch_sig_lane(bool sar, int method, const uint8_t *base, const uint
         big_patch_state_kernel<<<256, 256, 0, st>>>(big->nbig, order, n, big->crc, big->poly, sizes, sidx,
                                                     method == 2, states, tabs);
     else if (offload)
-        big_patch_kernel<<<256, 256, 0, st>>>(big->nbig, order, n, big->crc, big->poly, method == 2, crc_out,
-                                              sig_out, codes_out);
+        big_patch_kernel<<<256, 256, 0, st>>>(big->nbig, order + tail_p0, n, big->crc, big->poly, method == 2,
+                                              crc_out, sig_out, codes_out);
     return hipGetLastError();
 }
 
