@@ -190,14 +190,14 @@ __device__ __forceinline__ uint32_t size_bin(uint64_t L)
 }
 
 __global__ void bin_hist_kernel(const uint64_t *__restrict__ sizes, uint32_t n,
-                                uint32_t *__restrict__ hist)
+                                uint32_t *__restrict__ hist, uint32_t bmask)
 {
     __shared__ uint32_t h[kSizeBins];
     for (int b = threadIdx.x; b < kSizeBins; b += blockDim.x)
         h[b] = 0;
     __syncthreads();
     for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x)
-        atomicAdd(&h[size_bin(sizes[i])], 1u);
+        atomicAdd(&h[size_bin(sizes[i]) & bmask], 1u);
     __syncthreads();
     for (int b = threadIdx.x; b < kSizeBins; b += blockDim.x)
         if (h[b])
@@ -239,7 +239,8 @@ constexpr int kBinItems = 8;
 
 __global__ __launch_bounds__(1024) void bin_scatter_kernel(const uint64_t *__restrict__ sizes,
                                                            uint32_t n, uint32_t *__restrict__ cursor,
-                                                           uint32_t *__restrict__ order, uint32_t *__restrict__ err)
+                                                           uint32_t *__restrict__ order, uint32_t *__restrict__ err,
+                                                           uint32_t bmask)
 {
     __shared__ uint32_t cnt[kSizeBins];
     __shared__ uint32_t bas[kSizeBins];
@@ -251,7 +252,7 @@ __global__ __launch_bounds__(1024) void bin_scatter_kernel(const uint64_t *__res
 #pragma unroll
     for (int k = 0; k < kBinItems; k++) {
         const uint32_t i = i0 + k * blockDim.x;
-        bin[k] = i < n ? size_bin(sizes[i]) : 0u;
+        bin[k] = i < n ? (size_bin(sizes[i]) & bmask) : 0u;
     }
 #pragma unroll
     for (int k = 0; k < kBinItems; k++)
@@ -823,10 +824,22 @@ hipError_t launch_sig_lane(bool sar, int method, const uint8_t *base, const uint
         return e;
     uint32_t *cursor = hist + kSizeBins;
     const unsigned hb = (n + 1023) / 1024, sb = (n + 1024 * kBinItems - 1) / (1024 * kBinItems);
-    bin_hist_kernel<<<hb < 128 ? hb : 128, 1024, 0, st>>>(sizes, n, hist);
+    // bmask: the bins' low mantissa bits cleared (probe FDFS_GPU_BIN_SHIFT:
+    // 2^s sub-octave bins merged, so a wave's 64 files come from a narrower
+    // index range of the batch; the production bins are 1/32 octave)
+    uint32_t bmask = ~0u;
+#ifdef FDFS_PROBES
+    static int bsh = -1;
+    if (bsh < 0) {
+        const char *ev = getenv("FDFS_GPU_BIN_SHIFT");
+        bsh = ev ? atoi(ev) : 0;
+    }
+    bmask = ~((1u << (bsh & 7)) - 1u);
+#endif
+    bin_hist_kernel<<<hb < 128 ? hb : 128, 1024, 0, st>>>(sizes, n, hist, bmask);
     bin_scan_kernel<<<1, 1024, 0, st>>>(hist, cursor);
     uint32_t *err = hist + kLaneErrWord;
-    bin_scatter_kernel<<<sb, 1024, 0, st>>>(sizes, n, cursor, order, err);
+    bin_scatter_kernel<<<sb, 1024, 0, st>>>(sizes, n, cursor, order, err, bmask);
     const bool offload = big != nullptr;
     // MD5 one-shot batches above lat_files with md5_inline: the offloaded
     // CRC segments are md5_pair_kernel's own queue items (no segmented launch)
