@@ -42,6 +42,9 @@ def test_shipped_kernels_carry_no_probe_code(isa):
     assert all(("Lb1ELi0E" in k or "Lb0ELi0E" in k) for k in pair), pair
     assert isa["setprio"], "the pair kernel's priority policy is missing"
     assert all("md5_pair_kernel" in k for k in isa["setprio"]), isa["setprio"]
+    # round 4's measured-and-not-kept variants live in the probe build only
+    for probe in ("sig_split_kernel", "tail_plan_kernel", "dp_tile_kernelILb0E", "dp_split_kernelILi1024ELb1E"):
+        assert not any(probe in k for k in isa["names"]), probe
 
 
 DPP = "v_cndmask_b32_dpp v6, v5, v7, vcc quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf"
