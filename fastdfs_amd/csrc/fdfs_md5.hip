@@ -338,9 +338,10 @@ __global__ __launch_bounds__(64 * kMd5Waves) void md5_stage_kernel(
 // Config 3: 80.0 / 80.6 against 83.4 / 83.0 ms, alternating on one box
 // (profiles/r04/probes_r04b.txt, c3_p7 against c3_p1).  Re-evaluated every
 // 256 rounds (32 KiB per file), in 1 MiB units.
+template <int SH = 13>
 __device__ __forceinline__ void prio_by_remaining(uint64_t rem)
 {
-    const uint32_t q = __builtin_amdgcn_readfirstlane((uint32_t)(rem >> 13));  // 8K-round units
+    const uint32_t q = __builtin_amdgcn_readfirstlane((uint32_t)(rem >> SH));  // 8K-round units (SH 13)
     if (q >= 3)
         __builtin_amdgcn_s_setprio(3);
     else if (q == 2)
@@ -436,7 +437,8 @@ __device__ __forceinline__ void pair_crc_items(const PairSegs &segs, const uint8
 // s_setprio 2 while their chunk is among the largest quarter (the chunks
 // that end the batch), 0 after; 5 = per-workgroup timeline; 6 = no issue
 // priority (round 3's production form); 7 = young chunks first; 8 = static
-// boustrophedon chunk pairing (chunk w, then 2G - 1 - w).  PM 0
+// boustrophedon chunk pairing (chunk w, then 2G - 1 - w); 9 / 10 = the
+// priority in 512 KiB / 2 MiB units; 11 = re-evaluated every 64 rounds.  PM 0
 // (production) sets the longest-remaining-first priority (prio_by_remaining).
 template <bool SAR, int PM>
 __global__ __launch_bounds__(128) void md5_pair_kernel(
@@ -625,6 +627,15 @@ __global__ __launch_bounds__(128) void md5_pair_kernel(
                 if constexpr (PM == 0 || PM == 8) {
                     if ((r & 255) == 0)
                         prio_by_remaining(rounds - r + after);
+                } else if constexpr (PM == 9) {  // 512 KiB units
+                    if ((r & 255) == 0)
+                        prio_by_remaining<12>(rounds - r);
+                } else if constexpr (PM == 10) {  // 2 MiB units
+                    if ((r & 255) == 0)
+                        prio_by_remaining<14>(rounds - r);
+                } else if constexpr (PM == 11) {  // re-evaluated every 64 rounds
+                    if ((r & 63) == 0)
+                        prio_by_remaining(rounds - r);
                 }
                 issue(RB, r + 1);
                 stage(RA, sbuf[0]);
@@ -654,6 +665,15 @@ __global__ __launch_bounds__(128) void md5_pair_kernel(
                 if constexpr (PM == 0 || PM == 8) {
                     if ((r & 255) == 0)
                         prio_by_remaining(rounds - r + after);
+                } else if constexpr (PM == 9) {  // 512 KiB units
+                    if ((r & 255) == 0)
+                        prio_by_remaining<12>(rounds - r);
+                } else if constexpr (PM == 10) {  // 2 MiB units
+                    if ((r & 255) == 0)
+                        prio_by_remaining<14>(rounds - r);
+                } else if constexpr (PM == 11) {  // re-evaluated every 64 rounds
+                    if ((r & 63) == 0)
+                        prio_by_remaining(rounds - r);
                 }
                 pair_barrier();
                 const uint4 *q = reinterpret_cast<const uint4 *>(mine + (r & 1) * (64 * STRIDE));
@@ -754,6 +774,12 @@ hipError_t launch_md5_stage(bool sar, const uint8_t *base, const uint64_t *offs,
             PAIR_LAUNCH(7);
         else if (pair == 9)
             PAIR_LAUNCH(8);
+        else if (pair == 10)
+            PAIR_LAUNCH(9);
+        else if (pair == 11)
+            PAIR_LAUNCH(10);
+        else if (pair == 12)
+            PAIR_LAUNCH(11);
         else
 #endif
             PAIR_LAUNCH(0);
