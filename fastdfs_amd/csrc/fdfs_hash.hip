@@ -88,40 +88,6 @@ __device__ __forceinline__ uint32_t and_xor80(uint32_t a, uint32_t m)
     return __builtin_amdgcn_bitop3_b32(a, m, 0x80808080u, 0x6a);
 }
 
-// Quad transpose of one dword position: lane j of a lane quad holds r_k =
-// dword of piece j of quad-file k; afterwards r_k = dword of piece k of its
-// own file j.  Two butterfly stages (lane xor 1, lane xor 2); each output is
-// one v_cndmask_b32 whose src0 is the partner lane's register read through
-// DPP quad_perm, with VCC = the lanes that keep their own value: 8 VALU per
-// 4 x 4 block.  The leading s_nop covers the VALU-write -> DPP-read hazard
-// for inputs written just before the block, the middle one the same hazard
-// between the stages (hipcc does not look inside an asm statement).
-__device__ __forceinline__ void quad_transpose(uint32_t &r0, uint32_t &r1, uint32_t &r2, uint32_t &r3)
-{
-    uint32_t o0, o1, o2, o3;
-#define QDPP(D, S0, S1, P) "v_cndmask_b32_dpp %[" D "], %[" S0 "], %[" S1 "], vcc quad_perm:" P " row_mask:0xf bank_mask:0xf\n\t"
-    asm volatile(
-        "s_nop 1\n\t"
-        "s_mov_b32 vcc_lo, 0x55555555\n\t"  // even lanes keep
-        "s_mov_b32 vcc_hi, 0x55555555\n\t"
-        QDPP("o0", "r1", "r0", "[1,0,3,2]") QDPP("o2", "r3", "r2", "[1,0,3,2]")
-        "s_mov_b32 vcc_lo, 0xaaaaaaaa\n\t"  // odd lanes keep
-        "s_mov_b32 vcc_hi, 0xaaaaaaaa\n\t"
-        QDPP("o1", "r0", "r1", "[1,0,3,2]") QDPP("o3", "r2", "r3", "[1,0,3,2]")
-        "s_mov_b32 vcc_lo, 0x33333333\n\t"  // lanes 0, 1 of the quad keep
-        "s_mov_b32 vcc_hi, 0x33333333\n\t"
-        "s_nop 1\n\t"
-        QDPP("r0", "o2", "o0", "[2,3,0,1]") QDPP("r1", "o3", "o1", "[2,3,0,1]")
-        "s_mov_b32 vcc_lo, 0xcccccccc\n\t"  // lanes 2, 3 keep
-        "s_mov_b32 vcc_hi, 0xcccccccc\n\t"
-        QDPP("r2", "o0", "o2", "[2,3,0,1]") QDPP("r3", "o1", "o3", "[2,3,0,1]")
-        : [r0] "+v"(r0), [r1] "+v"(r1), [r2] "+v"(r2), [r3] "+v"(r3), [o0] "=&v"(o0), [o1] "=&v"(o1),
-          [o2] "=&v"(o2), [o3] "=&v"(o3)
-        :
-        : "vcc");
-#undef QDPP
-}
-
 // ST (fdfs_gpu_update_batch): the lane continues the chunk's
 // StorageFileContext-shaped state (crc32, file_hash_codes) instead of
 // INIT_HASH_CODES4 and writes it back unfinalised; every step above is a

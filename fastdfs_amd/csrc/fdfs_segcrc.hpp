@@ -57,7 +57,13 @@ __device__ __forceinline__ uint32_t chain16x(const uint32_t *sD, uint32_t lb, co
         return chain16<SAR>(sD, c, w, K);
 }
 
-template <bool SAR, int TM>
+// QL: quad-cooperative loads -- in instruction q lane 4m + j reads vector
+// 16m + 4q + j of the block, so one instruction reads 16 contiguous 64-byte
+// pieces instead of 64 scattered 16-byte ones (half the lines per
+// instruction), and a 4 x 4 transpose per dword position within the lane
+// quad (quad_transpose, 8 VALU per 4 vectors) gives every lane its own
+// contiguous 64 bytes again -- the load pattern sig_hash_kernel uses.
+template <bool SAR, int TM, bool QL = false>
 __device__ __forceinline__ uint32_t crc_segment(const uint32_t *sD, const uint32_t *sT,
                                                 const uint32_t *sA, const uint32_t *sR,
                                                 const Rep8Lane &R8, uint32_t K16,
@@ -75,13 +81,33 @@ __device__ __forceinline__ uint32_t crc_segment(const uint32_t *sD, const uint32
         const int64_t J = (nvec + 255) >> 8;
         const uint4 neutral = SAR ? make_uint4(~0u, ~0u, ~0u, ~0u) : make_uint4(0, 0, 0, 0);
         uint32_t acc = 0;
+        // QL: the vector lane `lane` loads as piece q (its quad's
+        // cooperative pattern); else its own vector q
+        const int qm = lane & ~3, qj = lane & 3;
+        auto lidx = [&](int64_t blk0, int q) -> int64_t {
+            return QL ? blk0 + 4 * qm + 4 * q + qj : blk0 + 4 * lane + q;
+        };
+        auto untangle = [&](uint4 (&w)[4]) {
+            if constexpr (QL) {
+                quad_transpose(w[0].x, w[1].x, w[2].x, w[3].x);
+                quad_transpose(w[0].y, w[1].y, w[2].y, w[3].y);
+                quad_transpose(w[0].z, w[1].z, w[2].z, w[3].z);
+                quad_transpose(w[0].w, w[1].w, w[2].w, w[3].w);
+            }
+        };
         {  // first (partial) block: vectors before index 0 are neutral
-            const int64_t vb = nvec - 256 * J + 4 * lane;
+            const int64_t b0 = nvec - 256 * J;
+            const int64_t vb = b0 + 4 * lane;
             uint4 w[4];
 #pragma unroll
             for (int q = 0; q < 4; q++) {
+                const int64_t li = lidx(b0, q);
+                w[q] = v[li < 0 ? 0 : li];
+            }
+            untangle(w);
+#pragma unroll
+            for (int q = 0; q < 4; q++) {
                 const int64_t vi = vb + q;
-                w[q] = v[vi < 0 ? 0 : vi];
                 if (vi < 0)
                     w[q] = neutral;
                 else if (16 * vi < a0 + 4)
@@ -95,10 +121,9 @@ __device__ __forceinline__ uint32_t crc_segment(const uint32_t *sD, const uint32
         // one is folded (index clamped on the last block: no branch)
         uint4 nx[4];
         if (J > 1) {
-            const uint4 *vp = v + (nvec - 256 * (J - 1) + 4 * lane);
 #pragma unroll
             for (int q = 0; q < 4; q++)
-                nx[q] = vp[q];
+                nx[q] = v[lidx(nvec - 256 * (J - 1), q)];
         }
         for (int64_t jb = 1; jb < J; jb++) {
             uint4 w[4];
@@ -106,10 +131,10 @@ __device__ __forceinline__ uint32_t crc_segment(const uint32_t *sD, const uint32
             for (int q = 0; q < 4; q++)
                 w[q] = nx[q];
             const int64_t jn = (jb + 1 < J) ? jb + 1 : jb;
-            const uint4 *vp = v + (nvec - 256 * (J - jn) + 4 * lane);
 #pragma unroll
             for (int q = 0; q < 4; q++)
-                nx[q] = vp[q];
+                nx[q] = v[lidx(nvec - 256 * (J - jn), q)];
+            untangle(w);
             acc = apply4(sA, acc);  // advance 4032 B to this lane's next piece
             if (jb == 1 && nvec - 256 * (J - 1) == 1 && lane == 0)
                 w[0] = seg_fix_vector<SAR>(w[0], 16, a0, xor4);  // vector 1 opens block 1
