@@ -115,17 +115,23 @@ __global__ __launch_bounds__(TM == 2 || MODE == 5 ? 1024 : kHashBlock) __attribu
     // the same 64 VGPRs as two 128-byte sets but 192 bytes of lookahead
     constexpr int NSETS = MODE == 7 ? 4 : 2;
     constexpr uint32_t SB = 16 * SV;  // bytes per step
-    __shared__ uint4 sB[2 * SV * 64];
+    // The MFMA B operands, compacted: lane l's 16 bytes for (hash h, vector
+    // q) are digit plane l & 3 of that vector's coefficients when l lies on
+    // the block diagonal ((l >> 4) == ((l & 15) >> 2), fdfs_tables.cpp) and
+    // zero otherwise -- five distinct 16-byte rows per (h, q): 1.25 KB of
+    // LDS instead of 16 KB (rows 0-3 = lanes 0-3's B, row 4 = zero).
+    __shared__ uint4 sB[2 * SV * 5];
     if constexpr (TM == 2)
         lds_fill_rep8(sD, &tabs->t.D[0][0]);
     else
         lds_fill(sD, &tabs->t.D[0][0], 16 * 256);
     lds_fill(sT, tabs->t.T, 256);
-#pragma unroll
-    for (int h = 0; h < 2; h++)
-        lds_fill(reinterpret_cast<uint32_t *>(sB + h * SV * 64),
-                 reinterpret_cast<const uint32_t *>(&tabs->pm.B[h][8 - SV][0][0]), SV * 64 * 4);
+    for (int i = threadIdx.x; i < 2 * SV * 5; i += blockDim.x) {
+        const int h = i / (SV * 5), q = (i / 5) % SV, r = i % 5;
+        sB[i] = r < 4 ? *reinterpret_cast<const uint4 *>(&tabs->pm.B[h][8 - SV + q][r][0]) : make_uint4(0, 0, 0, 0);
+    }
     __syncthreads();
+    const int brow = ((threadIdx.x & 63) >> 4) == ((threadIdx.x & 15) >> 2) ? (threadIdx.x & 3) : 4;
 
     const int lane = threadIdx.x & 63;
     const uint32_t wave0 = blockIdx.x * blockDim.x + (threadIdx.x & ~63u);
@@ -292,7 +298,7 @@ __global__ __launch_bounds__(TM == 2 || MODE == 5 ? 1024 : kHashBlock) __attribu
                 const i32x4 A = {(int)and_xor80(aq.x, msk), (int)and_xor80(aq.y, msk),
                                  (int)and_xor80(aq.z, msk), (int)and_xor80(aq.w, msk)};
                 // the step's vector q carries coefficients M^(SB-1-pos): B's vectors 8 - SV + q
-                const uint4 b31 = sB[(0 * SV + q) * 64 + lane], b33 = sB[(1 * SV + q) * 64 + lane];
+                const uint4 b31 = sB[(0 * SV + q) * 5 + brow], b33 = sB[(1 * SV + q) * 5 + brow];
                 const i32x4 B31 = {(int)b31.x, (int)b31.y, (int)b31.z, (int)b31.w};
                 const i32x4 B33 = {(int)b33.x, (int)b33.y, (int)b33.z, (int)b33.w};
                 C31 = __builtin_amdgcn_mfma_i32_16x16x64_i8(A, B31, C31, 0, 0, 0);
@@ -889,7 +895,7 @@ hipError_t launch_sig_hash(bool sar, const uint8_t *base, const uint64_t *offs,
     constexpr int ql = 1;
 #endif
 #ifdef FDFS_PROBES
-    const unsigned blk = ((tm >= 2 || mode == 5) && !states) ? 1024 : kHashBlock;
+    const unsigned blk0 = ((tm >= 2 || mode == 5) && !states) ? 1024 : kHashBlock;
     // FDFS_GPU_HASH_LDSPAD: dynamic LDS bytes per workgroup that the kernel
     // does not use, to cap its occupancy (waves per SIMD) for the role-split
     // bound of DESIGN 4.2
@@ -898,6 +904,12 @@ hipError_t launch_sig_hash(bool sar, const uint8_t *base, const uint64_t *offs,
         const char *ev = getenv("FDFS_GPU_HASH_LDSPAD");
         shm = ev ? atol(ev) : 0;
     }
+    static int hb = -1;  // FDFS_GPU_HASH_BLOCK: workgroup size (the LDS now fits eight per CU)
+    if (hb < 0) {
+        const char *ev = getenv("FDFS_GPU_HASH_BLOCK");
+        hb = ev ? atoi(ev) : 0;
+    }
+    const unsigned blk = hb == 128 || hb == 64 ? (unsigned)hb : blk0;
 #else
     const unsigned blk = kHashBlock;
     constexpr unsigned shm = 0;
