@@ -38,7 +38,7 @@
 
 namespace fdfs {
 
-// 256 threads: four workgroups (33 KB of tables each) per CU at 4 waves per
+// 256 threads: four workgroups (18 KB of tables each) per CU at 4 waves per
 // SIMD; 512-thread workgroups ran 4 % slower (profiles/r01/hash_block_ab.txt).
 constexpr int kHashBlock = 256;
 
