@@ -284,14 +284,19 @@ __global__ __launch_bounds__(TM == 2 || MODE == 5 ? 1024 : kHashBlock) __attribu
                         elf_word4_chain<SAR, true>(aq.w, e);
                     }
                 } else if (ok) {
-                    if (small)
+                    // PROBE ablations (wrong results): MODE 10 no ELF, MODE 11 no CRC
+                    if (small && MODE != 11)
                         c = crc16<SAR, TM>(sD, R8, K16, c, aq);
-                    elf_word4<SAR, false>(aq.x, e);
-                    elf_word4<SAR, false>(aq.y, e);
-                    elf_word4<SAR, false>(aq.z, e);
-                    elf_word4<SAR, true>(aq.w, e);
+                    if constexpr (MODE != 10) {
+                        elf_word4<SAR, false>(aq.x, e);
+                        elf_word4<SAR, false>(aq.y, e);
+                        elf_word4<SAR, false>(aq.z, e);
+                        elf_word4<SAR, true>(aq.w, e);
+                    } else {
+                        e += aq.x ^ aq.y ^ aq.z ^ aq.w;
+                    }
                 }
-                if (!mon)
+                if (!mon || MODE == 9)  // PROBE MODE 9: no MFMA planes (wrong results)
                     continue;
                 // b - 128 as int8 (b ^ 0x80); a padded step is all-zero data
                 const uint32_t msk = ok ? 0xFFFFFFFFu : 0u;
@@ -909,7 +914,7 @@ hipError_t launch_sig_hash(bool sar, const uint8_t *base, const uint64_t *offs,
         const char *ev = getenv("FDFS_GPU_HASH_BLOCK");
         hb = ev ? atoi(ev) : 0;
     }
-    const unsigned blk = hb == 128 || hb == 64 ? (unsigned)hb : blk0;
+    const unsigned blk = hb == 128 || hb == 64 || (hb == 512 && !states) ? (unsigned)hb : blk0;
 #else
     const unsigned blk = kHashBlock;
     constexpr unsigned shm = 0;
@@ -978,7 +983,17 @@ hipError_t launch_sig_hash(bool sar, const uint8_t *base, const uint64_t *offs,
         HASH_LAUNCH(true, 7);
     else if (mode == 8)  // the step's loads issued at s_setprio 2
         HASH_LAUNCH(true, 8);
-    else
+    else if (mode >= 9 && mode <= 11 && !states && ql) {  // power ablations: no MFMA / no ELF / no CRC
+        if (mode == 9)
+            sig_hash_kernel<true, 0, 9, false, true><<<grid, blk, (unsigned)shm, st>>>(
+                base, offs, sizes, order, n, tabs, big_min, crc_out, sig_out, codes_out, nullptr, nullptr);
+        else if (mode == 10)
+            sig_hash_kernel<true, 0, 10, false, true><<<grid, blk, (unsigned)shm, st>>>(
+                base, offs, sizes, order, n, tabs, big_min, crc_out, sig_out, codes_out, nullptr, nullptr);
+        else
+            sig_hash_kernel<true, 0, 11, false, true><<<grid, blk, (unsigned)shm, st>>>(
+                base, offs, sizes, order, n, tabs, big_min, crc_out, sig_out, codes_out, nullptr, nullptr);
+    } else
 #endif
     if (sar)
         HASH_LAUNCH(true, 0);
