@@ -333,9 +333,14 @@ __global__ __launch_bounds__(TM == 2 || MODE == 5 ? 1024 : kHashBlock) __attribu
             const uint32_t lo = (uint32_t)a, hi = (uint32_t)(a >> 32);
             auto ld = [&](int k, uint32_t lk, uint32_t hk) {
                 const uint8_t *pk = reinterpret_cast<const uint8_t *>(((uint64_t)hk << 32 | lk) + 16u * (lane & 3));
-                asm volatile("global_load_dwordx4 %0, %1, off offset:0" : "=v"(R[k]) : "v"(pk) : "memory");
-                if constexpr (SV == 8)
-                    asm volatile("global_load_dwordx4 %0, %1, off offset:64" : "=v"(R[k + 4]) : "v"(pk) : "memory");
+                if constexpr (MODE == 12) {  // PROBE: non-temporal loads
+                    asm volatile("global_load_dwordx4 %0, %1, off offset:0 nt" : "=v"(R[k]) : "v"(pk) : "memory");
+                    asm volatile("global_load_dwordx4 %0, %1, off offset:64 nt" : "=v"(R[k + 4]) : "v"(pk) : "memory");
+                } else {
+                    asm volatile("global_load_dwordx4 %0, %1, off offset:0" : "=v"(R[k]) : "v"(pk) : "memory");
+                    if constexpr (SV == 8)
+                        asm volatile("global_load_dwordx4 %0, %1, off offset:64" : "=v"(R[k + 4]) : "v"(pk) : "memory");
+                }
             };
 #define QBC(K) (uint32_t) __builtin_amdgcn_mov_dpp((int)lo, 0x55 * K, 0xF, 0xF, false), \
                (uint32_t) __builtin_amdgcn_mov_dpp((int)hi, 0x55 * K, 0xF, 0xF, false)
@@ -983,8 +988,14 @@ hipError_t launch_sig_hash(bool sar, const uint8_t *base, const uint64_t *offs,
         HASH_LAUNCH(true, 7);
     else if (mode == 8)  // the step's loads issued at s_setprio 2
         HASH_LAUNCH(true, 8);
-    else if (mode >= 9 && mode <= 11 && !states && ql) {  // power ablations: no MFMA / no ELF / no CRC
-        if (mode == 9)
+    else if (mode >= 9 && mode <= 12 && !states && ql) {  // power ablations: no MFMA / no ELF / no CRC; nt loads
+        if (mode == 12 && !sar)
+            sig_hash_kernel<false, 0, 12, false, true><<<grid, blk, (unsigned)shm, st>>>(
+                base, offs, sizes, order, n, tabs, big_min, crc_out, sig_out, codes_out, nullptr, nullptr);
+        else if (mode == 12)
+            sig_hash_kernel<true, 0, 12, false, true><<<grid, blk, (unsigned)shm, st>>>(
+                base, offs, sizes, order, n, tabs, big_min, crc_out, sig_out, codes_out, nullptr, nullptr);
+        else if (mode == 9)
             sig_hash_kernel<true, 0, 9, false, true><<<grid, blk, (unsigned)shm, st>>>(
                 base, offs, sizes, order, n, tabs, big_min, crc_out, sig_out, codes_out, nullptr, nullptr);
         else if (mode == 10)

@@ -63,7 +63,20 @@ __device__ __forceinline__ uint32_t chain16x(const uint32_t *sD, uint32_t lb, co
 // instruction), and a 4 x 4 transpose per dword position within the lane
 // quad (quad_transpose, 8 VALU per 4 vectors) gives every lane its own
 // contiguous 64 bytes again -- the load pattern sig_hash_kernel uses.
-template <bool SAR, int TM, bool QL = false>
+// NT (probe): the block loads as non-temporal loads.
+template <bool NT>
+__device__ __forceinline__ uint4 seg_load(const uint4 *p)
+{
+    if constexpr (NT) {
+        typedef uint32_t v4 __attribute__((ext_vector_type(4)));
+        const v4 r = __builtin_nontemporal_load(reinterpret_cast<const v4 *>(p));
+        return make_uint4(r.x, r.y, r.z, r.w);
+    } else {
+        return *p;
+    }
+}
+
+template <bool SAR, int TM, bool QL = false, bool NT = false>
 __device__ __forceinline__ uint32_t crc_segment(const uint32_t *sD, const uint32_t *sT,
                                                 const uint32_t *sA, const uint32_t *sR,
                                                 const Rep8Lane &R8, uint32_t K16,
@@ -102,7 +115,7 @@ __device__ __forceinline__ uint32_t crc_segment(const uint32_t *sD, const uint32
 #pragma unroll
             for (int q = 0; q < 4; q++) {
                 const int64_t li = lidx(b0, q);
-                w[q] = v[li < 0 ? 0 : li];
+                w[q] = seg_load<NT>(&v[li < 0 ? 0 : li]);
             }
             untangle(w);
 #pragma unroll
@@ -123,7 +136,7 @@ __device__ __forceinline__ uint32_t crc_segment(const uint32_t *sD, const uint32
         if (J > 1) {
 #pragma unroll
             for (int q = 0; q < 4; q++)
-                nx[q] = v[lidx(nvec - 256 * (J - 1), q)];
+                nx[q] = seg_load<NT>(&v[lidx(nvec - 256 * (J - 1), q)]);
         }
         for (int64_t jb = 1; jb < J; jb++) {
             uint4 w[4];
@@ -133,7 +146,7 @@ __device__ __forceinline__ uint32_t crc_segment(const uint32_t *sD, const uint32
             const int64_t jn = (jb + 1 < J) ? jb + 1 : jb;
 #pragma unroll
             for (int q = 0; q < 4; q++)
-                nx[q] = v[lidx(nvec - 256 * (J - jn), q)];
+                nx[q] = seg_load<NT>(&v[lidx(nvec - 256 * (J - jn), q)]);
             untangle(w);
             acc = apply4(sA, acc);  // advance 4032 B to this lane's next piece
             if (jb == 1 && nvec - 256 * (J - 1) == 1 && lane == 0)
