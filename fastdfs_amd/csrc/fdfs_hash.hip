@@ -240,7 +240,7 @@ __global__ __launch_bounds__(TM == 2 || MODE == 5 ? 1024 : kHashBlock) __attribu
             nexec += mon ? 1u : 0u;
 #pragma unroll
             for (int r = 0; r < 4; r++) {
-                if (!mon)
+                if (!mon || MODE == 13)  // PROBE MODE 13: no Horner step (wrong results)
                     break;
                 C31[r] = (int)((uint32_t)C31[r] * m31) + k31[r];
                 C33[r] = (int)((uint32_t)C33[r] * m33) + k33[r];
@@ -988,8 +988,11 @@ hipError_t launch_sig_hash(bool sar, const uint8_t *base, const uint64_t *offs,
         HASH_LAUNCH(true, 7);
     else if (mode == 8)  // the step's loads issued at s_setprio 2
         HASH_LAUNCH(true, 8);
-    else if (mode >= 9 && mode <= 12 && !states && ql) {  // power ablations: no MFMA / no ELF / no CRC; nt loads
-        if (mode == 12 && !sar)
+    else if (mode >= 9 && mode <= 13 && !states && ql) {  // ablations: no MFMA / no ELF / no CRC / no Horner; nt loads
+        if (mode == 13)
+            sig_hash_kernel<true, 0, 13, false, true><<<grid, blk, (unsigned)shm, st>>>(
+                base, offs, sizes, order, n, tabs, big_min, crc_out, sig_out, codes_out, nullptr, nullptr);
+        else if (mode == 12 && !sar)
             sig_hash_kernel<false, 0, 12, false, true><<<grid, blk, (unsigned)shm, st>>>(
                 base, offs, sizes, order, n, tabs, big_min, crc_out, sig_out, codes_out, nullptr, nullptr);
         else if (mode == 12)
