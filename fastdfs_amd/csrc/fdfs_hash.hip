@@ -21,10 +21,11 @@
 //    the 64 lanes' vectors as A (lane l's 16 bytes are row l & 15 of k-block
 //    l >> 4) and a block-diagonal B (fdfs_tables.cpp), giving the 4 planes
 //    of every file's dot.  The running hash lives in the accumulator layout
-//    as 4 planes per file: once per step the planes are multiplied by M^128
-//    (and the 128 * sum(digits) bias of the b ^ 0x80 = b - 128 encoding is
-//    added), which is Horner's rule on each plane (multiplying by M is
-//    linear mod 2^32).  At the end the planes are summed (sum P_j << 8j),
+//    as 4 planes per file: once per group of 8 steps the planes are
+//    multiplied by M^1024 (and the 128 * sum(digits) bias of the
+//    b ^ 0x80 = b - 128 encoding is added), which is Horner's rule on each
+//    plane (multiplying by M is linear mod 2^32); B carries the group's
+//    1024 coefficients.  At the end the planes are summed (sum P_j << 8j),
 //    moved back to the file's lane, and the zero-padded steps of files
 //    shorter than the wave's longest are undone with M^-128 powers.
 //
@@ -115,20 +116,25 @@ __global__ __launch_bounds__(TM == 2 || MODE == 5 ? 1024 : kHashBlock) __attribu
     // the same 64 VGPRs as two 128-byte sets but 192 bytes of lookahead
     constexpr int NSETS = MODE == 7 ? 4 : 2;
     constexpr uint32_t SB = 16 * SV;  // bytes per step
+    // 128-byte steps per Horner multiply of the accumulators (the B operands
+    // then carry the coefficients of the whole group: fdfs_tables.hpp BG)
+    constexpr int HG = SV == 8 ? kHornerGroup : 1;
     // The MFMA B operands, compacted: lane l's 16 bytes for (hash h, vector
     // q) are digit plane l & 3 of that vector's coefficients when l lies on
     // the block diagonal ((l >> 4) == ((l & 15) >> 2), fdfs_tables.cpp) and
     // zero otherwise -- five distinct 16-byte rows per (h, q): 1.25 KB of
-    // LDS instead of 16 KB (rows 0-3 = lanes 0-3's B, row 4 = zero).
-    __shared__ uint4 sB[2 * SV * 5];
+    // LDS per step instead of 16 KB (rows 0-3 = lanes 0-3's B, row 4 = zero),
+    // for the HG steps of a Horner group.
+    __shared__ uint4 sB[2 * SV * HG * 5];
     if constexpr (TM == 2)
         lds_fill_rep8(sD, &tabs->t.D[0][0]);
     else
         lds_fill(sD, &tabs->t.D[0][0], 16 * 256);
     lds_fill(sT, tabs->t.T, 256);
-    for (int i = threadIdx.x; i < 2 * SV * 5; i += blockDim.x) {
-        const int h = i / (SV * 5), q = (i / 5) % SV, r = i % 5;
-        sB[i] = r < 4 ? *reinterpret_cast<const uint4 *>(&tabs->pm.B[h][8 - SV + q][r][0]) : make_uint4(0, 0, 0, 0);
+    for (int i = threadIdx.x; i < 2 * SV * HG * 5; i += blockDim.x) {
+        const int h = i / (SV * HG * 5), q = (i / 5) % (SV * HG), r = i % 5;
+        const int8_t *row = HG > 1 ? &tabs->pm.BG[h][q][r & 3][0] : &tabs->pm.B[h][8 - SV + q][r & 3][0];
+        sB[i] = r < 4 ? *reinterpret_cast<const uint4 *>(row) : make_uint4(0, 0, 0, 0);
     }
     __syncthreads();
     const int brow = ((threadIdx.x & 63) >> 4) == ((threadIdx.x & 15) >> 2) ? (threadIdx.x & 3) : 4;
@@ -197,11 +203,11 @@ __global__ __launch_bounds__(TM == 2 || MODE == 5 ? 1024 : kHashBlock) __attribu
         nmax = y > nmax ? y : nmax;
     }
     if (nmax) {
-        const uint32_t m31 = SV == 8 ? tabs->pm.m128[0] : tabs->pm.m64[0];
-        const uint32_t m33 = SV == 8 ? tabs->pm.m128[1] : tabs->pm.m64[1];
+        const uint32_t m31 = SV == 8 ? tabs->pm.m1024[0] : tabs->pm.m64[0];
+        const uint32_t m33 = SV == 8 ? tabs->pm.m1024[1] : tabs->pm.m64[1];
         const int col = lane & 15, j = col & 3, g = col >> 2;
-        const int32_t kk31 = SV == 8 ? tabs->pm.K[0][j] : tabs->pm.K64[0][j];
-        const int32_t kk33 = SV == 8 ? tabs->pm.K[1][j] : tabs->pm.K64[1][j];
+        const int32_t kk31 = SV == 8 ? tabs->pm.KG[0][j] : tabs->pm.K64[0][j];
+        const int32_t kk33 = SV == 8 ? tabs->pm.KG[1][j] : tabs->pm.K64[1][j];
         const i32x4 k31 = {kk31, kk31, kk31, kk31};
         const i32x4 k33 = {kk33, kk33, kk33, kk33};
         // accumulator element r of this lane: plane j of the file in lane
@@ -221,6 +227,9 @@ __global__ __launch_bounds__(TM == 2 || MODE == 5 ? 1024 : kHashBlock) __attribu
         // still hashing (big files get simple/Time33 from poly_seg_kernel):
         // nexec counts them for the padding undo below.
         uint32_t nexec = 0;
+        // steps of the last Horner group that ran their MFMAs (< HG: the
+        // group's bias for the steps after them is taken back at the end)
+        uint32_t egrp = HG;
         // QL: the step's pieces arrive quad-interleaved (issue_q below) and
         // are transposed back to their files' lanes, one half line at a time
         // just before its four vectors are hashed.
@@ -235,12 +244,19 @@ __global__ __launch_bounds__(TM == 2 || MODE == 5 ? 1024 : kHashBlock) __attribu
                 a[4 * h + 3][d] = r3;
             }
         };
-        auto step = [&](u32x4 (&a)[SV], bool ok) {
+        auto step = [&](u32x4 (&a)[SV], bool ok, uint32_t stp) {
             const bool mon = __any(ok && small);
-            nexec += mon ? 1u : 0u;
+            // position of the step in its Horner group (wave-uniform); the
+            // group's first step scales the planes by M^(128 HG) and adds the
+            // group's bias, and counts the group's HG steps for the undo
+            const uint32_t sg = stp & (HG - 1);
+            if (mon) {
+                nexec += sg == 0 ? (uint32_t)HG : 0u;
+                egrp = sg + 1;
+            }
 #pragma unroll
             for (int r = 0; r < 4; r++) {
-                if (!mon || MODE == 13)  // PROBE MODE 13: no Horner step (wrong results)
+                if (!mon || sg != 0 || MODE == 13)  // PROBE MODE 13: no Horner step (wrong results)
                     break;
                 C31[r] = (int)((uint32_t)C31[r] * m31) + k31[r];
                 C33[r] = (int)((uint32_t)C33[r] * m33) + k33[r];
@@ -303,7 +319,8 @@ __global__ __launch_bounds__(TM == 2 || MODE == 5 ? 1024 : kHashBlock) __attribu
                 const i32x4 A = {(int)and_xor80(aq.x, msk), (int)and_xor80(aq.y, msk),
                                  (int)and_xor80(aq.z, msk), (int)and_xor80(aq.w, msk)};
                 // the step's vector q carries coefficients M^(SB-1-pos): B's vectors 8 - SV + q
-                const uint4 b31 = sB[(0 * SV + q) * 5 + brow], b33 = sB[(1 * SV + q) * 5 + brow];
+                const uint4 b31 = sB[(0 * SV * HG + sg * SV + q) * 5 + brow];
+                const uint4 b33 = sB[(1 * SV * HG + sg * SV + q) * 5 + brow];
                 const i32x4 B31 = {(int)b31.x, (int)b31.y, (int)b31.z, (int)b31.w};
                 const i32x4 B33 = {(int)b33.x, (int)b33.y, (int)b33.z, (int)b33.w};
                 C31 = __builtin_amdgcn_mfma_i32_16x16x64_i8(A, B31, C31, 0, 0, 0);
@@ -386,7 +403,7 @@ __global__ __launch_bounds__(TM == 2 || MODE == 5 ? 1024 : kHashBlock) __attribu
                     iss_fn(RS[(k + NSETS - 1) % NSETS], st + k + NSETS - 1);
                     wait_older(RS[k]);
                     if (k == 0 || st + k < end)
-                        step_fn(RS[k], st + k < nsteps);
+                        step_fn(RS[k], st + k < nsteps, st + k);
                 }
             }
             drain();
@@ -421,7 +438,7 @@ __global__ __launch_bounds__(TM == 2 || MODE == 5 ? 1024 : kHashBlock) __attribu
         // lookahead in the same registers) measured 906-962 against 826-940
         // ms on config 1, within that config's run-to-run spread
         // (profiles/r03/hash_pipeline_ab.txt): not kept.
-        auto step_chain = [&](u32x4 (&a)[SV], bool ok) {
+        auto step_chain = [&](u32x4 (&a)[SV], bool ok, uint32_t) {
             if (MODE == 1 || !ok)
                 return;
 #pragma unroll
@@ -434,6 +451,13 @@ __global__ __launch_bounds__(TM == 2 || MODE == 5 ? 1024 : kHashBlock) __attribu
         };
         if (nfull < nmax)
             pipeline(issue, step_chain, nfull, nmax);
+        if (nexec && egrp < HG) {  // the last group ran egrp of its HG steps
+#pragma unroll
+            for (int r = 0; r < 4; r++) {
+                C31[r] -= tabs->pm.KGtail[0][egrp][j];
+                C33[r] -= tabs->pm.KGtail[1][egrp][j];
+            }
+        }
         // planes -> value: sum_j P_j << 8j over the lane quad (j = lane & 3),
         // then back to the file's lane; undo the padded steps (M^-SB each)
         uint32_t s31 = 0, s33 = 0;

@@ -172,6 +172,26 @@ void build_poly_mfma_tables(PolyMfmaTables &t)
             t.K[h][j] = (int32_t)(uint32_t)(128 * ksum[j]);
             t.K64[h][j] = (int32_t)(uint32_t)(128 * ksum64[j]);
         }
+        // grouped form: 8 steps = 1024 positions per Horner multiply
+        int64_t kg[kHornerGroup + 1][4] = {};  // kg[s][j]: digits of plane j over steps >= s
+        for (int pos = 1024 - 1; pos >= 0; pos--) {
+            int d[4];
+            digits4(pow_u32(M[h], 1023 - pos), d);
+            const int v = pos >> 4, e = pos & 15;
+            for (int j = 0; j < 4; j++) {
+                t.BG[h][v][j][e] = (int8_t)d[j];
+                kg[pos >> 7][j] += d[j];
+            }
+        }
+        for (int s = kHornerGroup - 2; s >= 0; s--)
+            for (int j = 0; j < 4; j++)
+                kg[s][j] += kg[s + 1][j];
+        for (int j = 0; j < 4; j++) {
+            t.KG[h][j] = (int32_t)(uint32_t)(128 * kg[0][j]);
+            for (int e = 0; e < kHornerGroup; e++)
+                t.KGtail[h][e][j] = (int32_t)(uint32_t)(128 * kg[e][j]);
+        }
+        t.m1024[h] = pow_u32(M[h], 1024);
         t.m128[h] = pow_u32(M[h], 128);
         t.inv128[h] = inv_u32(t.m128[h]);
         t.m64[h] = pow_u32(M[h], 64);

@@ -43,7 +43,18 @@ struct PolyMfmaTables {
     int32_t K64[2][4];
     uint32_t m64[2];
     uint32_t inv64[2];
+    // Horner once per group of kHornerGroup 128-byte steps (sig_hash_kernel):
+    // BG[h][v][j] = digit plane j of the 16 coefficients M^(1023 - 16 v - e)
+    // of vector v of the group (the block-diagonal lane rows, compacted),
+    // KG = 128 * sum of a plane's digits over the group, m1024 = M^1024, and
+    // KGtail[h][e][j] = the part of KG that belongs to the steps after the
+    // first e, taken back when the last group ran only e steps.
+    int8_t BG[2][64][4][16];
+    int32_t KG[2][4];
+    int32_t KGtail[2][8][4];
+    uint32_t m1024[2];
 };
+constexpr int kHornerGroup = 8;  // 128-byte steps per Horner multiply
 
 void build_poly_mfma_tables(PolyMfmaTables &t);
 
