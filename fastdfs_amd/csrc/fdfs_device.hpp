@@ -228,8 +228,35 @@ __device__ __forceinline__ void elf_word4(uint32_t w, uint32_t &e)
                 ELF_STEP("v_lshrrev_b32", "BYTE_2") ELF_STEP("v_lshrrev_b32", "BYTE_3")
             : "+v"(e), "=&v"(t), "=&v"(y) : "v"(w), "s"(M));
 }
+// The same four dirty-form steps, with the last byte's t >> 24 (arithmetic
+// for SAR) left in y: its sign is the last t's, which is all the exact fold
+// of the final state needs (elf_exact_after).
+template <bool SAR>
+__device__ __forceinline__ void elf_word4y(uint32_t w, uint32_t &e, uint32_t &y)
+{
+    uint32_t t;
+    const uint32_t M = 0xFFFFFFF0u;
+    if constexpr (SAR)
+        asm(ELF_STEP("v_ashrrev_i32", "BYTE_0") ELF_STEP("v_ashrrev_i32", "BYTE_1")
+                ELF_STEP("v_ashrrev_i32", "BYTE_2") ELF_STEP("v_ashrrev_i32", "BYTE_3")
+            : "+v"(e), "=&v"(t), "=&v"(y) : "v"(w), "s"(M));
+    else
+        asm(ELF_STEP("v_lshrrev_b32", "BYTE_0") ELF_STEP("v_lshrrev_b32", "BYTE_1")
+                ELF_STEP("v_lshrrev_b32", "BYTE_2") ELF_STEP("v_lshrrev_b32", "BYTE_3")
+            : "+v"(e), "=&v"(t), "=&v"(y) : "v"(w), "s"(M));
+}
 #undef ELF_STEP
 #undef ELF_LAST
+
+// The exact ELFHash_ex state from a dirty-form one.  The two differ in bits
+// 28-31 only.  The exact step leaves them ~t's top nibble when the last t was
+// negative (SAR: x >> 24 sign-extends into them) -- as the dirty form does --
+// and clear otherwise.  y = the last step's t >> 24, or any negative value
+// when the state is already exact.
+__device__ __forceinline__ uint32_t elf_exact_after(uint32_t e, uint32_t y)
+{
+    return (int32_t)y < 0 ? e : (e & 0x0FFFFFFFu);
+}
 
 // The same word of ELF steps in plain C, for waves bound by ELF's dependent
 // chain rather than by issue: hipcc emits v_lshl_add_u32 (shift + byte add in
@@ -248,6 +275,20 @@ __device__ __forceinline__ void elf_word4_chain(uint32_t w, uint32_t &e)
         } else {
             e = t ^ ((SAR ? (uint32_t)((int32_t)t >> 24) : (t >> 24)) & 0xFFFFFFF0u);
         }
+    }
+}
+
+// elf_word4_chain<SAR, false> that also leaves the last byte's t >> 24 in y.
+template <bool SAR>
+__device__ __forceinline__ void elf_word4_chain_y(uint32_t w, uint32_t &e, uint32_t &y)
+{
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+        const uint32_t t = (e << 4) + ((w >> (8 * k)) & 0xFFu);
+        const uint32_t yt = SAR ? (uint32_t)((int32_t)t >> 24) : (t >> 24);
+        e = t ^ (yt & 0xFFFFFFF0u);
+        if (k == 3)
+            y = yt;
     }
 }
 

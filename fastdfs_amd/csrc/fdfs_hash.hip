@@ -230,6 +230,8 @@ __global__ __launch_bounds__(TM == 2 || MODE == 5 ? 1024 : kHashBlock) __attribu
         // steps of the last Horner group that ran their MFMAs (< HG: the
         // group's bias for the steps after them is taken back at the end)
         uint32_t egrp = HG;
+        // the last ELF step's t >> 24 (negative: e is exact as it stands)
+        uint32_t ylast = 0x80000000u;
         // QL: the step's pieces arrive quad-interleaved (issue_q below) and
         // are transposed back to their files' lanes, one half line at a time
         // just before its four vectors are hashed.
@@ -304,10 +306,13 @@ __global__ __launch_bounds__(TM == 2 || MODE == 5 ? 1024 : kHashBlock) __attribu
                     if (small && MODE != 11)
                         c = crc16<SAR, TM>(sD, R8, K16, c, aq);
                     if constexpr (MODE != 10) {
+                        // the top nibble stays dirty across vectors (each
+                        // step shifts it out); made exact once after the
+                        // steps from the last t's sign (elf_exact_after)
                         elf_word4<SAR, false>(aq.x, e);
                         elf_word4<SAR, false>(aq.y, e);
                         elf_word4<SAR, false>(aq.z, e);
-                        elf_word4<SAR, true>(aq.w, e);
+                        elf_word4y<SAR>(aq.w, e, ylast);
                     } else {
                         e += aq.x ^ aq.y ^ aq.z ^ aq.w;
                     }
@@ -446,11 +451,12 @@ __global__ __launch_bounds__(TM == 2 || MODE == 5 ? 1024 : kHashBlock) __attribu
                 elf_word4_chain<SAR, false>(a[q][0], e);
                 elf_word4_chain<SAR, false>(a[q][1], e);
                 elf_word4_chain<SAR, false>(a[q][2], e);
-                elf_word4_chain<SAR, true>(a[q][3], e);
+                elf_word4_chain_y<SAR>(a[q][3], e, ylast);
             }
         };
         if (nfull < nmax)
             pipeline(issue, step_chain, nfull, nmax);
+        e = elf_exact_after(e, ylast);
         if (nexec && egrp < HG) {  // the last group ran egrp of its HG steps
 #pragma unroll
             for (int r = 0; r < 4; r++) {
