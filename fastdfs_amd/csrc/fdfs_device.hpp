@@ -111,6 +111,9 @@ template <bool SAR>
 __device__ __forceinline__ uint32_t chain16(const uint32_t *__restrict__ D, uint32_t c, uint4 w,
                                             uint32_t K16)
 {
+    // the XORs as v_bitop3_b32 builtins, not asm statements: hipcc schedules
+    // them with the lookups and pads nothing around them
+    auto xor3 = [](uint32_t a, uint32_t b, uint32_t d) { return __builtin_amdgcn_bitop3_b32(a, b, d, 0x96); };
     const uint32_t x = c ^ w.x;
     uint32_t r0 = xor3(D[0 * 256 + (x & 0xFFu)], D[1 * 256 + ((x >> 8) & 0xFFu)],
                        D[2 * 256 + ((x >> 16) & 0xFFu)]);
@@ -247,6 +250,33 @@ __device__ __forceinline__ void elf_word4y(uint32_t w, uint32_t &e, uint32_t &y)
 }
 #undef ELF_STEP
 #undef ELF_LAST
+
+// A whole 16-byte vector of dirty-form steps in one asm statement (hipcc
+// pads the boundary between two asm statements with an s_nop: one boundary
+// per vector instead of four); y as in elf_word4y.
+#define ELF_WORD(SH, W) \
+    ELF_STEP_W(SH, "BYTE_0", W) ELF_STEP_W(SH, "BYTE_1", W) ELF_STEP_W(SH, "BYTE_2", W) ELF_STEP_W(SH, "BYTE_3", W)
+#define ELF_STEP_W(SH, BYTE, W)                                                   \
+    "v_lshlrev_b32 %1, 4, %0\n\t"                                                  \
+    "v_add_u32_sdwa %1, %1, %" W " dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:" BYTE "\n\t" \
+    SH " %2, 24, %1\n\t"                                                           \
+    "v_bitop3_b32 %0, %2, %1, %7 bitop3:0x6c\n\t"
+template <bool SAR>
+__device__ __forceinline__ void elf_vec16y(uint4 q, uint32_t &e, uint32_t &y)
+{
+    uint32_t t;
+    const uint32_t M = 0xFFFFFFF0u;
+    if constexpr (SAR)
+        asm(ELF_WORD("v_ashrrev_i32", "3") ELF_WORD("v_ashrrev_i32", "4") ELF_WORD("v_ashrrev_i32", "5")
+                ELF_WORD("v_ashrrev_i32", "6")
+            : "+v"(e), "=&v"(t), "=&v"(y) : "v"(q.x), "v"(q.y), "v"(q.z), "v"(q.w), "s"(M));
+    else
+        asm(ELF_WORD("v_lshrrev_b32", "3") ELF_WORD("v_lshrrev_b32", "4") ELF_WORD("v_lshrrev_b32", "5")
+                ELF_WORD("v_lshrrev_b32", "6")
+            : "+v"(e), "=&v"(t), "=&v"(y) : "v"(q.x), "v"(q.y), "v"(q.z), "v"(q.w), "s"(M));
+}
+#undef ELF_WORD
+#undef ELF_STEP_W
 
 // The exact ELFHash_ex state from a dirty-form one.  The two differ in bits
 // 28-31 only.  The exact step leaves them ~t's top nibble when the last t was

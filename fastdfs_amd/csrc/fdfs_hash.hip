@@ -309,10 +309,7 @@ __global__ __launch_bounds__(TM == 2 || MODE == 5 ? 1024 : kHashBlock) __attribu
                         // the top nibble stays dirty across vectors (each
                         // step shifts it out); made exact once after the
                         // steps from the last t's sign (elf_exact_after)
-                        elf_word4<SAR, false>(aq.x, e);
-                        elf_word4<SAR, false>(aq.y, e);
-                        elf_word4<SAR, false>(aq.z, e);
-                        elf_word4y<SAR>(aq.w, e, ylast);
+                        elf_vec16y<SAR>(aq, e, ylast);
                     } else {
                         e += aq.x ^ aq.y ^ aq.z ^ aq.w;
                     }
