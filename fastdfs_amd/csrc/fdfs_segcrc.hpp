@@ -76,7 +76,9 @@ __device__ __forceinline__ uint4 seg_load(const uint4 *p)
     }
 }
 
-template <bool SAR, int TM, bool QL = false, bool NT = false>
+// PF (probe): 2 = two blocks in flight (the next two blocks' loads issued
+// before the first block is folded) instead of one.
+template <bool SAR, int TM, bool QL = false, bool NT = false, int PF = 1>
 __device__ __forceinline__ uint32_t crc_segment(const uint32_t *sD, const uint32_t *sT,
                                                 const uint32_t *sA, const uint32_t *sR,
                                                 const Rep8Lane &R8, uint32_t K16,
@@ -108,6 +110,7 @@ __device__ __forceinline__ uint32_t crc_segment(const uint32_t *sD, const uint32
                 quad_transpose(w[0].w, w[1].w, w[2].w, w[3].w);
             }
         };
+        uint4 nx[4], nx2[4];
         {  // first (partial) block: vectors before index 0 are neutral
             const int64_t b0 = nvec - 256 * J;
             const int64_t vb = b0 + 4 * lane;
@@ -116,6 +119,17 @@ __device__ __forceinline__ uint32_t crc_segment(const uint32_t *sD, const uint32
             for (int q = 0; q < 4; q++) {
                 const int64_t li = lidx(b0, q);
                 w[q] = seg_load<NT>(&v[li < 0 ? 0 : li]);
+            }
+            if (PF == 2 && J > 1) {  // blocks 1 and 2 in flight while block 0 is folded
+                // (block 0 may start before the segment: only blocks >= 1 are
+                // loaded here, the second clamped to the last block)
+                const int64_t j2 = J > 2 ? 2 : 1;
+#pragma unroll
+                for (int q = 0; q < 4; q++)
+                    nx[q] = seg_load<NT>(&v[lidx(nvec - 256 * (J - 1), q)]);
+#pragma unroll
+                for (int q = 0; q < 4; q++)
+                    nx2[q] = seg_load<NT>(&v[lidx(nvec - 256 * (J - j2), q)]);
             }
             untangle(w);
 #pragma unroll
@@ -132,8 +146,7 @@ __device__ __forceinline__ uint32_t crc_segment(const uint32_t *sD, const uint32
         }
         // blocks 1..J-1: the next block's 64 B per lane is loaded while this
         // one is folded (index clamped on the last block: no branch)
-        uint4 nx[4];
-        if (J > 1) {
+        if (PF == 1 && J > 1) {
 #pragma unroll
             for (int q = 0; q < 4; q++)
                 nx[q] = seg_load<NT>(&v[lidx(nvec - 256 * (J - 1), q)]);
@@ -143,10 +156,19 @@ __device__ __forceinline__ uint32_t crc_segment(const uint32_t *sD, const uint32
 #pragma unroll
             for (int q = 0; q < 4; q++)
                 w[q] = nx[q];
-            const int64_t jn = (jb + 1 < J) ? jb + 1 : jb;
+            if constexpr (PF == 2) {
+                const int64_t jn = (jb + 2 < J) ? jb + 2 : J - 1;
 #pragma unroll
-            for (int q = 0; q < 4; q++)
-                nx[q] = seg_load<NT>(&v[lidx(nvec - 256 * (J - jn), q)]);
+                for (int q = 0; q < 4; q++) {
+                    nx[q] = nx2[q];
+                    nx2[q] = seg_load<NT>(&v[lidx(nvec - 256 * (J - jn), q)]);
+                }
+            } else {
+                const int64_t jn = (jb + 1 < J) ? jb + 1 : jb;
+#pragma unroll
+                for (int q = 0; q < 4; q++)
+                    nx[q] = seg_load<NT>(&v[lidx(nvec - 256 * (J - jn), q)]);
+            }
             untangle(w);
             acc = apply4(sA, acc);  // advance 4032 B to this lane's next piece
             if (jb == 1 && nvec - 256 * (J - 1) == 1 && lane == 0)

@@ -25,7 +25,7 @@ namespace fdfs {
 // ------------------------------------------------------- segmented CRC path
 // (device helpers in fdfs_segcrc.hpp)
 
-template <bool SAR, int TM, bool QL = false, bool NT = false>
+template <bool SAR, int TM, bool QL = false, bool NT = false, int PF = 1>
 __global__ __launch_bounds__(kSegBlock) void crc_seg_kernel(
     const uint8_t *__restrict__ base, const uint64_t *__restrict__ offs,
     const uint64_t *__restrict__ sizes, const uint64_t *__restrict__ seg_first, uint32_t n_host,
@@ -109,7 +109,7 @@ __global__ __launch_bounds__(kSegBlock) void crc_seg_kernel(
         const uint8_t *fp = base + offs[f];
         const uint64_t lo_b = k * kSegBytes;
         const uint64_t hi_b = (L < lo_b + kSegBytes) ? L : lo_b + kSegBytes;
-        const uint32_t v = crc_segment<SAR, TM, QL, NT>(sD, sT, sA, sR, R8, K16, fp + lo_b, hi_b - lo_b, k == 0, lane);
+        const uint32_t v = crc_segment<SAR, TM, QL, NT, PF>(sD, sT, sA, sR, R8, K16, fp + lo_b, hi_b - lo_b, k == 0, lane);
         if (run_f == f) {
             const uint64_t len = hi_b - lo_b;
             const uint32_t adv = (len == kSegBytes) ? apply4(sS, run_state)
@@ -939,6 +939,20 @@ static hipError_t crc_seg_run(bool sar, const uint8_t *base, const uint64_t *off
     if (nt < 0) {
         const char *ev = getenv("FDFS_GPU_SEG_NT");
         nt = ev ? atoi(ev) : 0;
+    }
+    static int pf = -1;  // FDFS_GPU_SEG_PF=2: two blocks in flight per wave
+    if (pf < 0) {
+        const char *ev = getenv("FDFS_GPU_SEG_PF");
+        pf = ev ? atoi(ev) : 1;
+    }
+    if (pf == 2 && tm == 2) {
+        if (sar)
+            crc_seg_kernel<true, 2, false, false, 2><<<grid, kSegBlock, 0, st>>>(base, offs, sizes, seg_first, n,
+                                                                                n_dev, tabs, crc_out);
+        else
+            crc_seg_kernel<false, 2, false, false, 2><<<grid, kSegBlock, 0, st>>>(base, offs, sizes, seg_first, n,
+                                                                                 n_dev, tabs, crc_out);
+        return hipGetLastError();
     }
     if (nt && tm == 2) {
         if (sar)
