@@ -15,7 +15,7 @@ from pmc_summary import load  # noqa: E402
 
 BENCH_KERNEL = {"c2": ("sig_hash_kernel<true, 0, 0, false", "sig_hash_kernel<SAR>"),
                 "c3": ("md5_pair_kernel<true", "md5_pair_kernel<SAR>"),
-                "c4": ("crc_seg_kernel<true, 2>", "crc_seg_kernel<SAR,2>")}
+                "c4": ("crc_seg_kernel<true, 2", "crc_seg_kernel<SAR,2>")}
 
 
 BENCH_C5_KERNEL = "dedup_group (dp_tile + scan + chunks + dp_split + dp_group)"
