@@ -413,6 +413,26 @@ __device__ __forceinline__ void quad_transpose(uint32_t &r0, uint32_t &r1, uint3
 #undef QDPP
 }
 
+// Pair transpose of one quarter line (probe, sig_hash_kernel MODE 14): lane
+// j of a lane pair holds in r0 / r1 piece j of pair-file 0 / 1; afterwards
+// lane j holds pieces 0 and 1 of its own file, in r0 and t.  One stage (lane
+// xor 1): 8 VALU per two vectors instead of the quad form's 16.
+__device__ __forceinline__ void pair_transpose(uint32_t (&r0)[4], const uint32_t (&r1)[4], uint32_t (&t)[4])
+{
+#define PD(D, S0, S1) "v_cndmask_b32_dpp %[" D "], %[" S0 "], %[" S1 "], vcc quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf\n\t"
+    asm volatile(
+        "s_nop 1\n\t"
+        "s_mov_b32 vcc_lo, 0xaaaaaaaa\n\ts_mov_b32 vcc_hi, 0xaaaaaaaa\n\t"  // odd lanes keep r1
+        PD("t0", "a0", "b0") PD("t1", "a1", "b1") PD("t2", "a2", "b2") PD("t3", "a3", "b3")
+        "s_mov_b32 vcc_lo, 0x55555555\n\ts_mov_b32 vcc_hi, 0x55555555\n\t"  // even lanes keep r0
+        PD("a0", "b0", "a0") PD("a1", "b1", "a1") PD("a2", "b2", "a2") PD("a3", "b3", "a3")
+        : [a0] "+v"(r0[0]), [a1] "+v"(r0[1]), [a2] "+v"(r0[2]), [a3] "+v"(r0[3]),
+          [t0] "=&v"(t[0]), [t1] "=&v"(t[1]), [t2] "=&v"(t[2]), [t3] "=&v"(t[3])
+        : [b0] "v"(r1[0]), [b1] "v"(r1[1]), [b2] "v"(r1[2]), [b3] "v"(r1[3])
+        : "vcc");
+#undef PD
+}
+
 // Cooperative global -> LDS copy of `ndw` dwords.
 __device__ __forceinline__ void lds_fill(uint32_t *dst, const uint32_t *__restrict__ src, int ndw)
 {

@@ -232,9 +232,9 @@ __global__ __launch_bounds__(TM == 2 || MODE == 5 ? 1024 : kHashBlock) __attribu
         uint32_t egrp = HG;
         // the last ELF step's t >> 24 (negative: e is exact as it stands)
         uint32_t ylast = 0x80000000u;
-        // QL: the step's pieces arrive quad-interleaved (issue_q below) and
-        // are transposed back to their files' lanes, one half line at a time
-        // just before its four vectors are hashed.
+        // QL: the step's pieces arrive interleaved over lane pairs (issue_p
+        // below; probe MODE 15: over lane quads, issue_q) and are transposed
+        // back to their files' lanes.
         auto qtr = [](u32x4 (&a)[SV], int h) {
 #pragma unroll
             for (int d = 0; d < 4; d++) {
@@ -244,6 +244,24 @@ __global__ __launch_bounds__(TM == 2 || MODE == 5 ? 1024 : kHashBlock) __attribu
                 a[4 * h + 1][d] = r1;
                 a[4 * h + 2][d] = r2;
                 a[4 * h + 3][d] = r3;
+            }
+        };
+        // Pair-cooperative loads (issue_p; probe MODE 15: the round-2 quad
+        // form, issue_q + qtr): one transpose stage per quarter line, just
+        // before its two vectors are hashed.
+        constexpr bool PAIR = MODE != 15;
+        auto ptr = [](u32x4 (&a)[SV], int p) {
+            uint32_t r0[4], r1[4], t[4];
+#pragma unroll
+            for (int d = 0; d < 4; d++) {
+                r0[d] = a[2 * p][d];
+                r1[d] = a[2 * p + 1][d];
+            }
+            pair_transpose(r0, r1, t);
+#pragma unroll
+            for (int d = 0; d < 4; d++) {
+                a[2 * p][d] = r0[d];
+                a[2 * p + 1][d] = t[d];
             }
         };
         auto step = [&](u32x4 (&a)[SV], bool ok, uint32_t stp) {
@@ -265,7 +283,13 @@ __global__ __launch_bounds__(TM == 2 || MODE == 5 ? 1024 : kHashBlock) __attribu
             }
 #pragma unroll
             for (int q = 0; q < SV; q++) {
-                if constexpr (QL && MODE != 1) {
+                if constexpr (QL && PAIR && MODE != 1) {
+                    if ((q & 1) == 0) {
+                        __builtin_amdgcn_sched_barrier(0);
+                        ptr(a, q >> 1);
+                        __builtin_amdgcn_sched_barrier(0);
+                    }
+                } else if constexpr (QL && MODE != 1) {
                     if ((q & 3) == 0) {
                         __builtin_amdgcn_sched_barrier(0);
                         qtr(a, q >> 2);
@@ -340,12 +364,13 @@ __global__ __launch_bounds__(TM == 2 || MODE == 5 ? 1024 : kHashBlock) __attribu
             for (int q = 0; q < SV; q++)
                 asm volatile("global_load_dwordx4 %0, %1, off offset:%2" : "=v"(R[q]) : "v"(ln), "i"(16 * q) : "memory");
         };
-        // Quad-cooperative form (QL): lane j of quad Q loads 16-byte piece
-        // 4h + j of quad-file k's line into R[4h + k], so each instruction
-        // reads 16 half lines of 64 contiguous bytes instead of 64 scattered
-        // 16-byte pieces (4x fewer lines and pages per instruction; loads
-        // alone 6.8 -> 6.0 ms on config 2, profiles/r02/hash_quad_ab.md).
-        // The quad's line addresses are broadcast by DPP quad_perm.
+        // Quad-cooperative form (probe MODE 15, production in rounds 2-4):
+        // lane j of quad Q loads 16-byte piece 4h + j of quad-file k's line
+        // into R[4h + k], so each instruction reads 16 half lines of 64
+        // contiguous bytes instead of 64 scattered 16-byte pieces (loads alone
+        // 6.8 -> 6.0 ms on config 2, profiles/r02/hash_quad_ab.md), at 8 VALU
+        // of transposes per vector.  MODE 12 (non-temporal) was measured on
+        // this form.  The quad's line addresses are broadcast by DPP quad_perm.
         auto issue_q = [&](u32x4 (&R)[SV], uint32_t stp) {
             const uint8_t *ln = (MODE != 2 && stp < nsteps) ? reinterpret_cast<const uint8_t *>(w + SV * (uint64_t)stp) : safe;
             const uint64_t a = reinterpret_cast<uint64_t>(ln);
@@ -368,6 +393,29 @@ __global__ __launch_bounds__(TM == 2 || MODE == 5 ? 1024 : kHashBlock) __attribu
             ld(2, QBC(2));
             ld(3, QBC(3));
 #undef QBC
+        };
+        // Pair-cooperative form (production since round 4): lane j of pair P
+        // loads piece 2p + j of pair-file k's line into R[2p + k]: 32
+        // contiguous bytes per lane pair per instruction, one transpose stage
+        // (4 VALU per vector instead of the quad form's 8): 8.41 against
+        // 8.58-8.60 ms (profiles/r04/pair_loads_ab.txt).  The pair's line
+        // addresses are broadcast by DPP quad_perm [k,k,2+k,2+k].
+        auto issue_p = [&](u32x4 (&R)[SV], uint32_t stp) {
+            const uint8_t *ln = stp < nsteps ? reinterpret_cast<const uint8_t *>(w + SV * (uint64_t)stp) : safe;
+            const uint64_t a = reinterpret_cast<uint64_t>(ln);
+            const uint32_t lo = (uint32_t)a, hi = (uint32_t)(a >> 32);
+            auto ld = [&](int k, uint32_t lk, uint32_t hk) {
+                const uint8_t *pk = reinterpret_cast<const uint8_t *>(((uint64_t)hk << 32 | lk) + 16u * (lane & 1));
+                asm volatile("global_load_dwordx4 %0, %1, off offset:0" : "=v"(R[k]) : "v"(pk) : "memory");
+                asm volatile("global_load_dwordx4 %0, %1, off offset:32" : "=v"(R[2 + k]) : "v"(pk) : "memory");
+                asm volatile("global_load_dwordx4 %0, %1, off offset:64" : "=v"(R[4 + k]) : "v"(pk) : "memory");
+                asm volatile("global_load_dwordx4 %0, %1, off offset:96" : "=v"(R[6 + k]) : "v"(pk) : "memory");
+            };
+#define PBC(S) (uint32_t) __builtin_amdgcn_mov_dpp((int)lo, S, 0xF, 0xF, false), \
+               (uint32_t) __builtin_amdgcn_mov_dpp((int)hi, S, 0xF, 0xF, false)
+            ld(0, PBC(0xA0));
+            ld(1, PBC(0xF5));
+#undef PBC
         };
         // R is the oldest of the NSETS sets in flight
         auto wait_older = [&](u32x4 (&R)[SV]) {
@@ -426,7 +474,9 @@ __global__ __launch_bounds__(TM == 2 || MODE == 5 ? 1024 : kHashBlock) __attribu
                 // priority, so they leave ahead of the other waves' VALU
                 if constexpr (MODE == 8)
                     __builtin_amdgcn_s_setprio(2);
-                if constexpr (QL)
+                if constexpr (QL && PAIR)
+                    issue_p(R, stp);
+                else if constexpr (QL)
                     issue_q(R, stp);
                 else
                     issue(R, stp);
@@ -1015,8 +1065,14 @@ hipError_t launch_sig_hash(bool sar, const uint8_t *base, const uint64_t *offs,
         HASH_LAUNCH(true, 7);
     else if (mode == 8)  // the step's loads issued at s_setprio 2
         HASH_LAUNCH(true, 8);
-    else if (mode >= 9 && mode <= 13 && !states && ql) {  // ablations: no MFMA / no ELF / no CRC / no Horner; nt loads
-        if (mode == 13)
+    else if (((mode >= 9 && mode <= 13) || mode == 15) && !states && ql) {  // ablations: no MFMA / no ELF / no CRC / no Horner; nt loads; quad loads
+        if (mode == 15 && !sar)
+            sig_hash_kernel<false, 0, 15, false, true><<<grid, blk, (unsigned)shm, st>>>(
+                base, offs, sizes, order, n, tabs, big_min, crc_out, sig_out, codes_out, nullptr, nullptr);
+        else if (mode == 15)
+            sig_hash_kernel<true, 0, 15, false, true><<<grid, blk, (unsigned)shm, st>>>(
+                base, offs, sizes, order, n, tabs, big_min, crc_out, sig_out, codes_out, nullptr, nullptr);
+        else if (mode == 13)
             sig_hash_kernel<true, 0, 13, false, true><<<grid, blk, (unsigned)shm, st>>>(
                 base, offs, sizes, order, n, tabs, big_min, crc_out, sig_out, codes_out, nullptr, nullptr);
         else if (mode == 12 && !sar)
