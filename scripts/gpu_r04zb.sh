@@ -21,3 +21,8 @@ for k in 1 2 3; do
 done
 step c1new 900 python3 bench.py --no-cpu-baseline --config c1 --steps 2 --warmup 1 || exit $?; show c1new
 FDFS_GPU_PROBE_LIB=ab step c1old 900 python3 bench.py --no-cpu-baseline --config c1 --steps 2 --warmup 1 || exit $?; show c1old
+# lane-per-file loads, no transposes (probe FDFS_GPU_HASH_QUAD=0) against the pair form
+for k in 1 2; do
+  FDFS_GPU_PROBE_LIB=1 step pair_$k 300 $B2 || exit $?; show pair_$k
+  FDFS_GPU_PROBE_LIB=1 FDFS_GPU_HASH_QUAD=0 step lane_$k 300 $B2 || exit $?; show lane_$k
+done
