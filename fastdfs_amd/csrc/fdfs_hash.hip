@@ -401,7 +401,7 @@ __global__ __launch_bounds__(TM == 2 || MODE == 5 ? 1024 : kHashBlock) __attribu
         // 8.58-8.60 ms (profiles/r04/pair_loads_ab.txt).  The pair's line
         // addresses are broadcast by DPP quad_perm [k,k,2+k,2+k].
         auto issue_p = [&](u32x4 (&R)[SV], uint32_t stp) {
-            const uint8_t *ln = stp < nsteps ? reinterpret_cast<const uint8_t *>(w + SV * (uint64_t)stp) : safe;
+            const uint8_t *ln = (MODE != 2 && stp < nsteps) ? reinterpret_cast<const uint8_t *>(w + SV * (uint64_t)stp) : safe;
             const uint64_t a = reinterpret_cast<uint64_t>(ln);
             const uint32_t lo = (uint32_t)a, hi = (uint32_t)(a >> 32);
             auto ld = [&](int k, uint32_t lk, uint32_t hk) {
