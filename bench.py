@@ -475,6 +475,10 @@ def main():
                 "algorithmic_bytes_per_launch": nbytes}
         if tsrc:
             roof["traffic_source"] = tsrc
+        if args.config == "c2":
+            roof["note"] = ("below the HBM roof: the hash step is co-bound by VALU issue and the LDS "
+                            "pipe, and the chip holds ~2.0 of its 2.4 GHz under this load (loads or "
+                            "compute alone keep 2.4); DESIGN.md 4.2, profiles/r04/clock_ablation_c2.txt")
         if args.config in ("c1", "c3", "c4") and method != F.SIG_CRC_ONLY:
             # lane-per-file batches whose largest file's dependent chain (MD5
             # / ELFHash) outlasts the HBM stream: the roof is that chain (c4
