@@ -9,7 +9,9 @@ step's signatures across all ranks (bucket -> RCCL all-to-all -> group ->
 all-to-all back).  Weak scaling: every rank owns its own batch.  The same
 line carries "dedup_100m": config 5's 100M-signature dedup split over the
 run's ranks (strong scaling), so the 1/2/4/8-GPU runs of the default bench
-give the dedup scaling curve too.
+give the dedup scaling curve too, and "large_file": config 4 (8 x 1 GiB per
+GPU, CRC32 only, the segmented crc_seg_kernel) -- the north star's
+large-file corpus -- with its own roofline and CPU baseline.
 
 Other workloads: --config c3 (MD5 method, 1-4 MiB files), c4 (1 GiB files,
 CRC-only segmented path), c5 (dedup only, 100M signatures, strong scaling).
@@ -17,7 +19,8 @@ CRC-only segmented path), c5 (dedup only, 100M signatures, strong scaling).
 Prints ONE JSON line on rank 0 (contract in the task statement), with a
 "roofline" object for the dominant kernel (its duration measured by HIP
 events recorded inside libfdfs_gpu on the launch stream) and a
-"cpu_baseline" object (the C oracle of the reference loops on host cores).
+"cpu_baseline" object (the C oracle of the reference loops on host cores,
+over a bounded sample: at most 4 GiB copied to the host, repeated to ~10 s).
 """
 from __future__ import annotations
 
@@ -153,39 +156,71 @@ def host_threads(args) -> int:
     return max(1, min(n, int(q))) if q else n
 
 
+HOST_SAMPLE_CAP = 4 << 30  # bytes copied to the host for a CPU baseline sample
+
+
+def host_sample(data, offs_np, sizes_np, budget, threads):
+    """The first files of the batch as a host buffer of about `budget` bytes:
+    at least min(n, threads) files (one per thread), each file cut to its
+    first `cap` bytes when whole files would not fit the budget (1 GiB files:
+    the per-byte loop rate does not depend on where a file is cut).  Returns
+    (host bytes, offsets, sizes, k files, cap or None)."""
+    n = len(sizes_np)
+    m = max(1, min(n, threads))
+    cap = max(64 << 10, int(budget // m))
+    cut = sizes_np[:max(m, 1)].max() > cap
+    sz = np.minimum(sizes_np, cap) if cut else sizes_np
+    cum = np.cumsum(sz)
+    k = int(min(n, max(m, np.searchsorted(cum, budget) + 1)))
+    sz = np.asarray(sz[:k], dtype=np.int64)
+    if not cut:
+        end = int(offs_np[k - 1] + sizes_np[k - 1])
+        return data[:end].cpu().numpy(), offs_np[:k], sz, k, None
+    parts = [data[int(o):int(o) + int(s)] for o, s in zip(offs_np[:k], sz)]
+    host = torch.cat(parts).cpu().numpy()
+    offs = np.zeros(k, np.int64)
+    offs[1:] = np.cumsum(sz)[:-1]
+    return host, offs, sz, k, cap
+
+
 def cpu_baseline(data, offs_np, sizes_np, method, variant, seconds, threads):
     """The C oracle (restated reference loops, 256 KiB chunks as dio_write_file
-    gets them) on a bounded prefix of the same batch, `threads` host threads,
-    one file per thread at a time."""
+    gets them) on a bounded sample of the same batch, `threads` host threads,
+    one file per thread at a time.  At most HOST_SAMPLE_CAP
+    bytes are copied to the host; a sample shorter than ~`seconds` of work is
+    hashed again (`passes`), so the timing covers ~`seconds` either way."""
     from oracle import oracle as O
     O.lib()
 
-    def run(k):
-        end = int(offs_np[k - 1] + sizes_np[k - 1])
-        host = data[:end].cpu().numpy()
+    def run(smp, reps):
+        host, offs, sz = smp[0], smp[1], smp[2]
         t0 = time.perf_counter()
-        O.dio_batch(host, offs_np[:k], sizes_np[:k], method, variant, 256 * 1024, threads)
-        return time.perf_counter() - t0, int(sizes_np[:k].sum())
+        for _ in range(reps):
+            O.dio_batch(host, offs, sz, method, variant, 256 * 1024, threads)
+        return time.perf_counter() - t0, int(sz.sum()) * reps
 
     n = len(sizes_np)
-    k = min(n, max(threads * 4, 64))
-    dt, nb = run(k)
-    while dt < 0.5 and k < n:  # probe until the timing is meaningful
-        k = min(n, k * 4)
-        dt, nb = run(k)
-    rate = nb / dt
-    # size the measured sample to ~`seconds` of CPU work
-    want = rate * seconds
-    cum = np.cumsum(sizes_np)
-    k2 = int(min(n, max(k, np.searchsorted(cum, want) + 1)))
-    if k2 > k:
-        dt, nb = run(k2)
-        k = k2
-    return {"value": round(nb / dt / 1e9, 4), "unit": "GB/s", "cores": threads, "kind": "port",
-            "host_cpus": len(os.sched_getaffinity(0)), "cgroup_cpus": cgroup_cpus(),
-            "sample": f"first {k} files of the rank-0 batch ({nb / 1e9:.2f} GB), "
-                      f"oracle/fdfs_oracle.c orc_dio_batch, 256 KiB chunks, {threads} threads, "
-                      f"{dt:.1f} s", "cpu_model": cpu_model()}
+    budget = 64 << 20
+    while True:  # probe until the timing is meaningful
+        smp = host_sample(data, offs_np, sizes_np, budget, threads)
+        dt, nb = run(smp, 1)
+        whole = smp[3] == n and smp[4] is None
+        if dt >= 0.5 or whole or budget >= HOST_SAMPLE_CAP:
+            break
+        budget = min(HOST_SAMPLE_CAP, budget * 4)
+    want = nb / dt * seconds  # bytes of ~`seconds` of CPU work
+    if want > nb and not whole and budget < HOST_SAMPLE_CAP:
+        smp = host_sample(data, offs_np, sizes_np, min(want, HOST_SAMPLE_CAP), threads)
+    reps = max(1, int(round(want / max(int(smp[2].sum()), 1))))
+    dt, nb = run(smp, reps)
+    k, cap = smp[3], smp[4]
+    busy = min(threads, k)
+    what = f"first {k} files of the rank-0 batch" + (f", each cut to its first {cap >> 20} MiB" if cap else "")
+    return {"value": round(nb / dt / 1e9, 4), "unit": "GB/s", "cores": busy, "kind": "port",
+            "threads": threads, "host_cpus": len(os.sched_getaffinity(0)), "cgroup_cpus": cgroup_cpus(),
+            "sample": f"{what} ({int(smp[2].sum()) / 1e9:.2f} GB host copy) x {reps} pass(es), "
+                      f"oracle/fdfs_oracle.c orc_dio_batch, 256 KiB chunks, {threads} threads "
+                      f"({busy} with a file), {dt:.1f} s", "cpu_model": cpu_model()}
 
 
 # The reference's own dedup decision costs at least one synchronous FastDHT
@@ -256,15 +291,17 @@ def load_traffic(config: str, kernel: str):
     return None, None
 
 
-SQ_KERNEL = {"c2": "sig_hash_kernel<true, 0, 0", "c3": "md5_pair_kernel<true"}  # name prefixes
+# name prefixes of the dominant kernels in the pmc_sq files (round 5 dropped
+# the probe-mode template parameters: sig_hash_kernel<true, false>)
+SQ_KERNEL = {"c2": ("sig_hash_kernel<true, false>", "sig_hash_kernel<true, 0, 0"), "c3": ("md5_pair_kernel<true",)}
 
 
 def load_valu(config: str, avg_ms: float):
     """VALU issue of the dominant kernel: SQ_INSTS_VALU per launch from the
-    newest committed rocprofv3 --pmc pass (profiles/r04, else r03, r02,
+    newest committed rocprofv3 --pmc pass (profiles/r05, else r04, r03, r02,
     r01, pmc_sq_<config>.txt; the count does not depend on timing) over the
     live kernel time, in int32 lane-ops/s against VALU_PEAK_TOPS."""
-    for rnd in ("r04", "r03", "r02", "r01"):
+    for rnd in ("r05", "r04", "r03", "r02", "r01"):
         path = os.path.join(ROOT, "profiles", rnd, f"pmc_sq_{config}.txt")
         try:
             for line in open(path):
@@ -309,7 +346,7 @@ def dedup_strong(ctx, sig, gidx, world, steps, warmup):
 
 
 METHODS = {"crc": F.SIG_CRC_ONLY, "hash": F.SIG_HASH, "md5": F.SIG_MD5}
-KERNEL_OF = {F.SIG_CRC_ONLY: (_lib.KERNEL_CRC_SEG, "crc_seg_kernel<SAR,2>"),
+KERNEL_OF = {F.SIG_CRC_ONLY: (_lib.KERNEL_CRC_SEG, "crc_seg_kernel<SAR>"),
              F.SIG_HASH: (_lib.KERNEL_SIG_LANE, "sig_hash_kernel<SAR>"),
              F.SIG_MD5: (_lib.KERNEL_SIG_LANE, "md5_pair_kernel<SAR>")}
 
@@ -339,6 +376,112 @@ def chain_floor_ms(ctx, data, offs_t, sizes_t, sizes, method, kernel, alone=Fals
     ms, cnt = ctx.read_timing(kernel)
     ctx.set_timing(False)
     return ms / max(cnt, 1), int(sizes[k])
+
+
+def c4_sizes(n):
+    return np.full(n, 1 << 30, dtype=np.int64)
+
+
+def c4_workload(n):
+    return f"config 4: {n} x 1 GiB files/GPU, segmented CRC32 (64 KiB) + GF(2) combine"
+
+
+def batch_line(args, ctx, world, rank, dev, config, sizes, method, workload, steps, warmup, threads,
+               variant, traffic_ok):
+    """One signature workload (configs 1-4): a batch per rank resident in
+    HBM, `steps` timed steps of fdfs_gpu_sig_batch (+ the global dedup of the
+    step's signatures when the method makes them); the dominant kernel's
+    mean duration from the library's HIP events on its launch stream; the
+    CPU baseline on rank 0 at N = 1.  The batch is freed on return."""
+    n = len(sizes)
+    kernel, kname = KERNEL_OF[method]
+    workload += {F.SIG_CRC_ONLY: ", CRC32 only (check_file_duplicate=0)",
+                 F.SIG_HASH: ", CRC32 + HASH_CODES4 signature + bulk dedup per step",
+                 F.SIG_MD5: ", CRC32 + MD5 signature + bulk dedup per step"}[method]
+    if config == "c4" and method == F.SIG_CRC_ONLY:
+        workload = workload.split(", CRC32 only")[0] + ", CRC32 only (check_file_duplicate=0, the default)"
+    data, offs_t, sizes_t = C.device_batch(sizes, seed=2 + 1000 * rank, device=dev, align=args.align)
+    nbytes = int(sizes.sum())
+    gidx = (torch.arange(n, device=dev, dtype=torch.int64) + rank * n)
+    ctx.reserve(n, n)
+
+    def step():
+        crc, sig, _ = ctx.sig_batch(data, offs_t, sizes_t, method=method, check_bounds=False)
+        if sig is not None:
+            dedup_step(ctx, sig, gidx, world)
+
+    for _ in range(warmup):
+        step()
+    torch.cuda.synchronize()
+    ctx.set_timing(True)
+    ctx.read_timing(kernel)
+    dt = timed(step, steps, 0, world)
+    kms, launches = ctx.read_timing(kernel)
+    ctx.set_timing(False)
+    total_bytes = sum_over_ranks(float(nbytes), world) * steps
+    out = {"value": round(total_bytes / dt / 1e9, 3), "unit": "GB/s",
+           "ms_per_step": round(dt / steps * 1e3, 3), "scaling": "weak",
+           "files_per_s": round(sum_over_ranks(float(n), world) * steps / dt, 1)}
+    avg_ms = kms / max(launches, 1)
+    per_launch = float(nbytes)  # each file byte read once; 28 B/file of outputs on top
+    achieved = per_launch / (avg_ms * 1e-3) / 1e9
+    traffic, tsrc = load_traffic(config, kname) if traffic_ok else (None, None)
+    roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
+            "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
+            "traffic": traffic, "kernel": kname,
+            "kernel_ms_avg": round(avg_ms, 4), "launches": launches,
+            "algorithmic_bytes_per_launch": nbytes}
+    if tsrc:
+        roof["traffic_source"] = tsrc
+    if config == "c2" and method == F.SIG_HASH:
+        roof["note"] = ("below the HBM roof: the hash step is co-bound by VALU issue and the LDS "
+                        "pipe, and the chip holds ~2.0 of its 2.4 GHz under this load (loads or "
+                        "compute alone keep 2.4); DESIGN.md 4.2, profiles/r04/clock_ablation_c2.txt")
+    if config in ("c1", "c3", "c4") and method != F.SIG_CRC_ONLY:
+        # lane-per-file batches whose largest file's dependent chain (MD5
+        # / ELFHash) outlasts the HBM stream: the roof is that chain (c4
+        # with --method hash / md5: 1 GiB files, one lane each)
+        fms, fbytes = chain_floor_ms(ctx, data, offs_t, sizes_t, sizes, method, kernel)
+        roof.update({"bound": "md5_chain" if method == F.SIG_MD5 else "elf_chain",
+                     "peak": round(per_launch / (fms * 1e-3) / 1e9, 1),
+                     "frac": round(fms / avg_ms, 4), "hbm_frac": round(achieved / HBM_PEAK_GBS, 4),
+                     "chain_floor_ms": round(fms, 3), "chain_floor_file_bytes": fbytes,
+                     "note": "peak = batch bytes over the time the same kernel takes for the "
+                             "largest file on the path it takes in the batch (one lane's serial "
+                             "chain; the other files of that timing batch are empty)"})
+        if method == F.SIG_MD5 and config != "c4":
+            ams, _ = chain_floor_ms(ctx, data, offs_t, sizes_t, sizes, method, kernel, alone=True)
+            roof["md5_alone_floor_ms"] = round(ams, 3)
+            roof["md5_alone_note"] = ("the largest file as a one-file batch: its CRC moves to the "
+                                      "segmented kernel and the lane runs MD5 alone")
+    out["roofline"] = roof
+    valu = load_valu(config, avg_ms) if not args.method else None
+    if valu:
+        out["valu"] = valu
+    if method != F.SIG_CRC_ONLY:
+        # dedup-only throughput of the same signatures (files/s, all ranks)
+        _, sig, _ = ctx.sig_batch(data, offs_t, sizes_t, method=method, check_bounds=False)
+        ddt = timed(lambda: dedup_step(ctx, sig, gidx, world), steps, 1, world)
+        out["dedup_files_per_s"] = round(sum_over_ranks(float(n), world) * steps / ddt, 1)
+        del sig
+    out["config"] = {"workload": workload, "files_per_gpu": n, "bytes_per_gpu": nbytes,
+                     "method": {0: "crc_only", 1: "hash", 2: "md5"}[method],
+                     "crc_variant": "unsigned" if variant else "signed", "align": args.align,
+                     "parallelism": f"dp{world} (files sharded, dedup all-to-all)"}
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        offs_np = C.layout(sizes, args.align)[0]
+        cb = cpu_baseline(data, offs_np, sizes, method, variant, args.cpu_seconds, threads)
+        one = cpu_baseline(data, offs_np, sizes, method, variant, args.cpu_seconds / 2, 1)
+        cb["single_thread"] = {k: one[k] for k in ("value", "unit", "sample")}
+        # the GPU line over the CPU line, so a reader sees at once where the
+        # host's cores would win (ratio < 1)
+        cb["gpu_over_cpu"] = round(out["value"] / cb["value"], 2) if cb["value"] else None
+        out["cpu_baseline"] = cb
+    else:
+        out["cpu_baseline"] = None
+    del data, offs_t, sizes_t, gidx
+    torch.cuda.empty_cache()
+    return out
 
 
 def rccl_exchange_check(ctx, world, rank, dev):
@@ -415,12 +558,10 @@ def main():
                    (10 << 20, 50), (100 << 20, 10)]
             sizes = np.concatenate([np.full(c, sz, np.int64) for sz, c in mix])
             sizes = sizes[np.random.default_rng(1 + 1000 * rank).permutation(sizes.size)]
-            n = sizes.size
             method = F.SIG_HASH
             workload = "config 1: test_upload DEBUG mix (gen_files sizes 5K..100M, 65,560 files)"
         elif args.config == "c2":
-            n = args.files or 1_000_000
-            sizes = C.small_files_sizes(n, seed=1 + 1000 * rank)
+            sizes = C.small_files_sizes(args.files or 1_000_000, seed=1 + 1000 * rank)
             method = F.SIG_HASH
             workload = "config 2: 1M files/GPU of U[4,64] KiB"
         elif args.config == "c3":
@@ -429,87 +570,14 @@ def main():
             method = F.SIG_MD5
             workload = f"config 3: {n} files/GPU of U[1,4] MiB"
         else:
-            n = args.files or 8
-            sizes = np.full(n, 1 << 30, dtype=np.int64)
+            sizes = c4_sizes(args.files or 8)
             method = F.SIG_CRC_ONLY
-            workload = f"config 4: {n} x 1 GiB files/GPU, segmented CRC32 (64 KiB) + GF(2) combine"
+            workload = c4_workload(len(sizes))
         if args.method:
             method = METHODS[args.method]
-        kernel, kname = KERNEL_OF[method]
-        workload += {F.SIG_CRC_ONLY: ", CRC32 only (check_file_duplicate=0)",
-                     F.SIG_HASH: ", CRC32 + HASH_CODES4 signature + bulk dedup per step",
-                     F.SIG_MD5: ", CRC32 + MD5 signature + bulk dedup per step"}[method]
-        if args.config == "c4":
-            workload = workload.split(", CRC32 only")[0]
-        data, offs_t, sizes_t = C.device_batch(sizes, seed=2 + 1000 * rank, device=dev, align=args.align)
-        nbytes = int(sizes.sum())
-        gidx = (torch.arange(n, device=dev, dtype=torch.int64) + rank * n)
-        ctx.reserve(n, n)
-
-        def step():
-            crc, sig, _ = ctx.sig_batch(data, offs_t, sizes_t, method=method, check_bounds=False)
-            if sig is not None:
-                dedup_step(ctx, sig, gidx, world)
-
-        for _ in range(args.warmup):
-            step()
-        torch.cuda.synchronize()
-        ctx.set_timing(True)
-        ctx.read_timing(kernel)
-        dt = timed(step, args.steps, 0, world)
-        kms, launches = ctx.read_timing(kernel)
-        ctx.set_timing(False)
-        total_bytes = sum_over_ranks(float(nbytes), world) * args.steps
-        res.update({"value": round(total_bytes / dt / 1e9, 3), "unit": "GB/s",
-                    "ms_per_step": round(dt / args.steps * 1e3, 3), "scaling": "weak",
-                    "files_per_s": round(sum_over_ranks(float(n), world) * args.steps / dt, 1)})
-        avg_ms = kms / max(launches, 1)
-        per_launch = float(nbytes)  # each file byte read once; 28 B/file of outputs on top
-        achieved = per_launch / (avg_ms * 1e-3) / 1e9
-        traffic, tsrc = load_traffic(args.config, kname) if (args.align == 16 and not args.method) \
-            else (None, None)
-        roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
-                "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
-                "traffic": traffic, "kernel": kname,
-                "kernel_ms_avg": round(avg_ms, 4), "launches": launches,
-                "algorithmic_bytes_per_launch": nbytes}
-        if tsrc:
-            roof["traffic_source"] = tsrc
-        if args.config == "c2":
-            roof["note"] = ("below the HBM roof: the hash step is co-bound by VALU issue and the LDS "
-                            "pipe, and the chip holds ~2.0 of its 2.4 GHz under this load (loads or "
-                            "compute alone keep 2.4); DESIGN.md 4.2, profiles/r04/clock_ablation_c2.txt")
-        if args.config in ("c1", "c3", "c4") and method != F.SIG_CRC_ONLY:
-            # lane-per-file batches whose largest file's dependent chain (MD5
-            # / ELFHash) outlasts the HBM stream: the roof is that chain (c4
-            # with --method hash / md5: 1 GiB files, one lane each)
-            fms, fbytes = chain_floor_ms(ctx, data, offs_t, sizes_t, sizes, method, kernel)
-            roof.update({"bound": "md5_chain" if method == F.SIG_MD5 else "elf_chain",
-                         "peak": round(per_launch / (fms * 1e-3) / 1e9, 1),
-                         "frac": round(fms / avg_ms, 4), "hbm_frac": round(achieved / HBM_PEAK_GBS, 4),
-                         "chain_floor_ms": round(fms, 3), "chain_floor_file_bytes": fbytes,
-                         "note": "peak = batch bytes over the time the same kernel takes for the "
-                                 "largest file on the path it takes in the batch (one lane's serial "
-                                 "chain; the other files of that timing batch are empty)"})
-            if method == F.SIG_MD5 and args.config != "c4":
-                ams, _ = chain_floor_ms(ctx, data, offs_t, sizes_t, sizes, method, kernel, alone=True)
-                roof["md5_alone_floor_ms"] = round(ams, 3)
-                roof["md5_alone_note"] = ("the largest file as a one-file batch: its CRC moves to the "
-                                          "segmented kernel and the lane runs MD5 alone")
-        res["roofline"] = roof
-        valu = load_valu(args.config, avg_ms) if not args.method else None
-        if valu:
-            res["valu"] = valu
-        if method != F.SIG_CRC_ONLY:
-            # dedup-only throughput of the same signatures (files/s, all ranks)
-            _, sig, _ = ctx.sig_batch(data, offs_t, sizes_t, method=method, check_bounds=False)
-            ddt = timed(lambda: dedup_step(ctx, sig, gidx, world), args.steps, 1, world)
-            res["dedup_files_per_s"] = round(sum_over_ranks(float(n), world) * args.steps / ddt, 1)
-        cfg = {"workload": workload, "files_per_gpu": n, "bytes_per_gpu": nbytes,
-               "method": {0: "crc_only", 1: "hash", 2: "md5"}[method],
-               "crc_variant": "unsigned" if variant else "signed", "align": args.align,
-               "parallelism": f"dp{world} (files sharded, dedup all-to-all)"}
-        res["config"] = cfg
+        res.update(batch_line(args, ctx, world, rank, dev, args.config, sizes, method, workload,
+                              args.steps, args.warmup, threads, variant,
+                              traffic_ok=args.align == 16 and not args.method))
         if args.config == "c2" and not args.files and not args.method and args.align == 16:
             # config 5's 100M-record dedup, strong-scaled over the ranks of
             # this run: the driver's 1/2/4/8-GPU runs of the default bench
@@ -526,14 +594,15 @@ def main():
                 res["dedup_100m"]["xgmi_bytes_per_step"] = round(peer)
                 res["dedup_100m"]["xgmi_gbs"] = round(peer / (ddt / st5) / 1e9, 1)
             del sig5, gidx5
-        if rank == 0 and world == 1 and not args.no_cpu_baseline:
-            offs_np = C.layout(sizes, args.align)[0]
-            res["cpu_baseline"] = cpu_baseline(data, offs_np, sizes, method, variant,
-                                               args.cpu_seconds, threads)
-            one = cpu_baseline(data, offs_np, sizes, method, variant, args.cpu_seconds / 2, 1)
-            res["cpu_baseline"]["single_thread"] = {k: one[k] for k in ("value", "unit", "sample")}
-        else:
-            res["cpu_baseline"] = None
+            torch.cuda.empty_cache()
+            # the north star's large-file corpus (config 4: 8 x 1 GiB per
+            # GPU, CRC32 only -- the upload path's default with
+            # check_file_duplicate=0 -- crc_seg_kernel), weak-scaled like the
+            # main line, with its own roofline and CPU baseline
+            lf = batch_line(args, ctx, world, rank, dev, "c4", c4_sizes(8), F.SIG_CRC_ONLY,
+                            c4_workload(8), min(args.steps, 10), 2, threads, variant, traffic_ok=True)
+            res["large_file"] = {k: lf[k] for k in ("value", "unit", "ms_per_step", "scaling", "files_per_s",
+                                                    "roofline", "cpu_baseline", "config")}
     else:  # c5: dedup only, strong scaling over a fixed 100M-signature set
         total = args.files or 100_000_000
         sig, gidx = C.c5_signatures(total, world, rank, dev)

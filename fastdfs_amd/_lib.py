@@ -19,6 +19,11 @@ if os.environ.get("FDFS_GPU_PROBE_LIB") == "1":
 elif os.environ.get("FDFS_GPU_PROBE_LIB") == "ab":  # `make ab`: the previous form of a kernel, for A/B runs
     LIB_PATH = os.path.join(_HERE, "lib", "ab", "libfdfs_gpu.so")
 HEADER_PATH = os.path.join(os.path.dirname(_HERE), "include", "fdfs_gpu.h")
+# The test-hooks build (`make test-hooks`, part of `make all`): the same
+# objects with fdfs_api.cpp compiled with FDFS_TEST_HOOKS, which adds
+# fdfs_gpu_inject_error (fastdfs_amd/csrc/fdfs_test_hooks.h).  The shipped
+# library does not export it; only the error-path tests load this one.
+TEST_HOOKS_LIB_PATH = os.path.join(_HERE, "lib", "test", "libfdfs_gpu.so")
 
 SIG_CRC_ONLY = 0
 SIG_HASH = 1
@@ -48,7 +53,6 @@ EXPORTS = (
     "fdfs_gpu_sig_batch_host",
     "fdfs_gpu_scrub",
     "fdfs_gpu_last_error",
-    "fdfs_gpu_inject_error",
     "fdfs_gpu_state_init",
     "fdfs_gpu_update_batch",
     "fdfs_gpu_final_batch",
@@ -101,13 +105,32 @@ _lib = None
 def load() -> ctypes.CDLL:
     """Load libfdfs_gpu.so; raises if it has not been built."""
     global _lib
-    if _lib is not None:
-        return _lib
-    if not os.path.exists(LIB_PATH):
+    if _lib is None:
+        _lib = _bind(LIB_PATH)
+    return _lib
+
+
+_hooks = None
+
+
+def load_test_hooks() -> ctypes.CDLL:
+    """The test-hooks build of the library (a second copy of every entry
+    point plus fdfs_gpu_inject_error), for the error-path tests only."""
+    global _hooks
+    if _hooks is None:
+        L = _bind(TEST_HOOKS_LIB_PATH)
+        L.fdfs_gpu_inject_error.restype = ctypes.c_int
+        L.fdfs_gpu_inject_error.argtypes = [ctypes.c_void_p, ctypes.c_void_p]
+        _hooks = L
+    return _hooks
+
+
+def _bind(path: str) -> ctypes.CDLL:
+    if not os.path.exists(path):
         raise RuntimeError(
-            f"libfdfs_gpu.so not found at {LIB_PATH}: build it with "
+            f"{os.path.basename(path)} not found at {path}: build it with "
             "`python -c 'import __graft_entry__ as g; g.build()'` (no CPU fallback exists)")
-    L = ctypes.CDLL(LIB_PATH)
+    L = ctypes.CDLL(path)
     vp, u64, u32, i32 = ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint32, ctypes.c_int
     L.fdfs_gpu_abi_version.restype = i32
     L.fdfs_gpu_abi_version.argtypes = []
@@ -154,8 +177,6 @@ def load() -> ctypes.CDLL:
     L.fdfs_gpu_scrub.argtypes = [vp, ctypes.POINTER(FdfsGpuBatch), vp, vp, vp, vp, vp]
     L.fdfs_gpu_last_error.restype = ctypes.c_char_p
     L.fdfs_gpu_last_error.argtypes = [vp]
-    L.fdfs_gpu_inject_error.restype = i32
-    L.fdfs_gpu_inject_error.argtypes = [vp, vp]
     L.fdfs_gpu_state_init.restype = i32
     L.fdfs_gpu_state_init.argtypes = [vp, vp, u32, vp]
     L.fdfs_gpu_update_batch.restype = i32
@@ -190,5 +211,4 @@ def load() -> ctypes.CDLL:
     L.fdfs_gpu_index_stats.argtypes = [vp, ctypes.POINTER(u64), ctypes.POINTER(u64), ctypes.POINTER(u64)]
     L.fdfs_gpu_index_slots.restype = i32
     L.fdfs_gpu_index_slots.argtypes = [vp, ctypes.POINTER(u64)]
-    _lib = L
     return L

@@ -87,8 +87,10 @@ class Context:
     state libfastcommon declares; True selects logical shifts (zlib CRC).
     """
 
-    def __init__(self, device: int | None = None, unsigned_hash: bool = False):
-        self._L = _lib.load()
+    def __init__(self, device: int | None = None, unsigned_hash: bool = False, test_hooks: bool = False):
+        # test_hooks: the context lives in the test-hooks build of the
+        # library (fdfs_gpu_inject_error), for the error-path tests only
+        self._L = _lib.load_test_hooks() if test_hooks else _lib.load()
         if device is None:
             device = torch.cuda.current_device()
         self.device = int(device)
@@ -127,8 +129,9 @@ class Context:
         return ms.value, cnt.value
 
     def inject_error(self, stream=None):
-        """Test hook (fdfs_gpu_inject_error): queue a lane-path error on
-        `stream`; a later call of this context fails with EIO once."""
+        """Test hook (fdfs_gpu_inject_error, contexts opened with
+        test_hooks=True): queue a lane-path error on `stream`; a later call
+        of this context fails with EIO once."""
         self._rc(self._L.fdfs_gpu_inject_error(self._h, _stream_handle(stream)), "fdfs_gpu_inject_error")
 
     def reserve(self, max_files: int, max_records: int = 0):

@@ -25,10 +25,7 @@ struct fdfs_gpu_ctx {
     uint32_t lat_files = 0;  // lane batches up to one wave per SIMD (BigCrcWs::lat_files)
     uint32_t ncu = 0;        // the device's CU count, read once at open (BigCrcWs::ncu)
     uint64_t lane_err_seen = 0;  // lane-path error count already reported (lane_err_check)
-    // the segmented passes' stream when they run beside the lane kernel
-    // (BigCrcWs::side) and its fork / join events
-    hipStream_t side = nullptr;
-    hipEvent_t fork = nullptr, join = nullptr;
+    uint32_t lane_err_next = 0;  // the next launch's slot of the error-count ring (lane_err_note)
     void *ws = nullptr;
     size_t ws_bytes = 0;
     char err[256] = {0};
@@ -126,37 +123,6 @@ fdfs::BigCrcWs carve_big(const fdfs_gpu_ctx *ctx, Carve &cv, uint32_t n)
     big.big_min = cv.take<uint64_t>(1);
     big.lat_files = ctx->lat_files;
     big.ncu = ctx->ncu;
-#ifdef FDFS_PROBES
-    // measurement build only: FDFS_GPU_LAT_FILES overrides (0 = always kBigCrcMin)
-    static long lf = -2;
-    if (lf == -2) {
-        const char *ev = getenv("FDFS_GPU_LAT_FILES");
-        lf = ev ? atol(ev) : -1;
-    }
-    if (lf >= 0)
-        big.lat_files = (uint32_t)lf;
-    // FDFS_GPU_MD5_T_BIN: MD5 batches above lat_files offload the CRC of the
-    // files in size bins >= this one; FDFS_GPU_SIDE=1: beside the lane kernel
-    // (2: enqueued after it, on a lowest-priority stream; 3: items of the
-    // pair kernel's queue)
-    static long mb = -2, sd = -2;
-    if (mb == -2) {
-        const char *ev = getenv("FDFS_GPU_MD5_T_BIN");
-        mb = ev ? atol(ev) : 0;
-        const char *es = getenv("FDFS_GPU_SIDE");
-        sd = es ? atol(es) : 0;
-    }
-    big.md5_bin = (uint32_t)mb;
-    if (sd == 3 || sd == 4) {  // 3: the CRC segments as md5_pair_kernel queue items; 4: of the tail chunks
-        big.md5_inline = true;
-        big.md5_tail = sd == 4;
-    } else if (sd >= 1) {  // 2: enqueued after the lane kernel
-        big.side = ctx->side;
-        big.fork = ctx->fork;
-        big.join = ctx->join;
-        big.side_late = sd == 2;
-    }
-#endif
     return big;
 }
 
@@ -166,8 +132,9 @@ size_t dedup_ws_bytes(uint64_t n) { return fdfs::dedup_ws_bytes(n) + align_up(8 
 // words), then kAnnTail words {owner-side room, workspace room, errno}.
 constexpr int kAnnTail = 3;
 constexpr size_t kAnnMax = 64 + kAnnTail;                   // words of one announcement
-constexpr size_t kAnnDevWords = kAnnMax + 64 * kAnnMax + 8;  // own, all ranks', agreement flag
-constexpr size_t kAnnHostWords = 64 * kAnnTail + 64 * kAnnMax + 8;  // tails, all ranks', flag
+constexpr size_t kErrRing = 64;  // lane_err_note's per-launch slots
+constexpr size_t kAnnDevWords = kAnnMax + 64 * kAnnMax + 8 + kErrRing;  // own, all ranks', agreement flag, ring
+constexpr size_t kAnnHostWords = 64 * kAnnTail + 64 * kAnnMax + 8 + kErrRing;  // tails, all ranks', flag, ring
 
 bool capturing(hipStream_t st)
 {
@@ -201,27 +168,37 @@ struct WsScope {
 
 // The lane path's device error word (fdfs::kLaneErrWord, zeroed with the
 // histogram at every launch) feeds a per-context error COUNT: after each lane
-// launch a one-thread kernel adds 1 to a device counter when the launch's
-// word is set, and the counter is copied to a pinned host word.  The count
-// only grows, so a later launch's copy can never erase an earlier launch's
-// error (a copy of the per-launch word itself could: two calls queued back
-// to back, the second's 0 landing after the first's 1).  The context's next
-// call whose check sees a count above the last one it reported fails with
-// EIO.  Device word: dann[kAnnErrCount]; host copy: hann[kHannErrCount].
+// launch a one-thread kernel adds 1 to a device counter (a device-scope
+// atomic: a context may be called on several streams) when the launch's word
+// is set, and writes the new count to the launch's own slot of a ring, which
+// is copied to the same slot of a pinned host ring.  The count only grows and
+// every launch has its own slot, so no copy can erase another launch's count
+// (one shared host word could go back: two calls on two streams, the older
+// count's copy landing after the newer one).  The context's next call whose
+// check sees a count (the ring's maximum) above the last one it reported
+// fails with EIO.  Device: dann[kAnnErrCount] and the ring at
+// dann[kAnnErrRing]; host ring: hann[kHannErrRing].
 constexpr size_t kAnnErrCount = kAnnMax + 64 * kAnnMax + 6;
-constexpr size_t kHannErrCount = 64 * kAnnTail + 64 * kAnnMax + 2;
+constexpr size_t kAnnErrRing = kAnnMax + 64 * kAnnMax + 8;
+constexpr size_t kHannErrRing = 64 * kAnnTail + 64 * kAnnMax + 8;
 
 hipError_t lane_err_note(fdfs_gpu_ctx *ctx, const uint32_t *hist, hipStream_t st)
 {
-    hipError_t e = fdfs::launch_lane_err_count(hist ? hist + fdfs::kLaneErrWord : nullptr, ctx->dann + kAnnErrCount, st);
+    const uint32_t k = ctx->lane_err_next++ % kErrRing;  // under the context's mutex
+    hipError_t e = fdfs::launch_lane_err_count(hist ? hist + fdfs::kLaneErrWord : nullptr, ctx->dann + kAnnErrCount,
+                                               ctx->dann + kAnnErrRing + k, st);
     if (e == hipSuccess)
-        e = hipMemcpyAsync(ctx->hann + kHannErrCount, ctx->dann + kAnnErrCount, 8, hipMemcpyDeviceToHost, st);
+        e = hipMemcpyAsync(ctx->hann + kHannErrRing + k, ctx->dann + kAnnErrRing + k, 8, hipMemcpyDeviceToHost, st);
     return e;
 }
 
 int lane_err_check(fdfs_gpu_ctx *ctx)
 {
-    const uint64_t v = __atomic_load_n(ctx->hann + kHannErrCount, __ATOMIC_ACQUIRE);
+    uint64_t v = 0;
+    for (size_t k = 0; k < kErrRing; k++) {
+        const uint64_t x = __atomic_load_n(ctx->hann + kHannErrRing + k, __ATOMIC_ACQUIRE);
+        v = x > v ? x : v;
+    }
     if (v <= ctx->lane_err_seen)
         return 0;
     ctx->lane_err_seen = v;
@@ -357,17 +334,6 @@ int fdfs_gpu_open(int device, unsigned flags, fdfs_gpu_ctx **out)
             h->Dc[p][x] = h->t.D[p][x ^ 0xFF];
     fdfs::build_poly_mfma_tables(h->pm);
     hipError_t e = hipEventCreateWithFlags(&ctx->ws_ev, hipEventDisableTiming);
-#ifdef FDFS_PROBES  // the side-stream offload measurement (FDFS_GPU_SIDE, carve_big)
-    int prio_lo = 0, prio_hi = 0;  // the side stream at the lowest priority
-    if (e == hipSuccess)
-        e = hipDeviceGetStreamPriorityRange(&prio_lo, &prio_hi);
-    if (e == hipSuccess)
-        e = hipStreamCreateWithPriority(&ctx->side, hipStreamNonBlocking, prio_lo);
-    if (e == hipSuccess)
-        e = hipEventCreateWithFlags(&ctx->fork, hipEventDisableTiming);
-    if (e == hipSuccess)
-        e = hipEventCreateWithFlags(&ctx->join, hipEventDisableTiming);
-#endif
     if (e == hipSuccess)
         e = hipMalloc(&ctx->d_tabs, sizeof(fdfs::DevTables));
     if (e == hipSuccess)
@@ -376,8 +342,16 @@ int fdfs_gpu_open(int device, unsigned flags, fdfs_gpu_ctx **out)
         e = hipMalloc(reinterpret_cast<void **>(&ctx->dann), 8 * kAnnDevWords);
     if (e == hipSuccess)
         e = hipHostMalloc(reinterpret_cast<void **>(&ctx->hann), 8 * kAnnHostWords, 0);
-    if (e == hipSuccess)
-        e = hipMemset(ctx->dann, 0, 8 * kAnnDevWords);
+    if (e == hipSuccess) {  // zeroed on a private stream: waits for nothing else on the device
+        hipStream_t zs = nullptr;
+        e = hipStreamCreateWithFlags(&zs, hipStreamNonBlocking);
+        if (e == hipSuccess)
+            e = hipMemsetAsync(ctx->dann, 0, 8 * kAnnDevWords, zs);
+        if (e == hipSuccess)
+            e = hipStreamSynchronize(zs);
+        if (zs)
+            (void)hipStreamDestroy(zs);
+    }
     if (e == hipSuccess)
         std::memset(ctx->hann, 0, 8 * kAnnHostWords);
     delete h;
@@ -390,12 +364,6 @@ int fdfs_gpu_open(int device, unsigned flags, fdfs_gpu_ctx **out)
             (void)hipHostFree(ctx->hann);
         if (ctx->ws_ev)
             (void)hipEventDestroy(ctx->ws_ev);
-        if (ctx->side)
-            (void)hipStreamDestroy(ctx->side);
-        if (ctx->fork)
-            (void)hipEventDestroy(ctx->fork);
-        if (ctx->join)
-            (void)hipEventDestroy(ctx->join);
         delete ctx;
         return EIO;
     }
@@ -406,10 +374,6 @@ int fdfs_gpu_open(int device, unsigned flags, fdfs_gpu_ctx **out)
     ctx->seg_grid = (unsigned)(ncu * fdfs::crc_seg_blocks_per_cu());
     ctx->lat_files = (uint32_t)ncu * 4 * 64;
     ctx->ncu = (uint32_t)ncu;
-    if ((e = hipDeviceSynchronize()) != hipSuccess) {  // the zeroed words above
-        fdfs_gpu_close(ctx);
-        return EIO;
-    }
     *out = ctx;
     return 0;
 }
@@ -440,12 +404,6 @@ int fdfs_gpu_close(fdfs_gpu_ctx *ctx)
         (void)hipFree(ctx->d_tabs);
     if (ctx->ws_ev)
         (void)hipEventDestroy(ctx->ws_ev);
-    if (ctx->side)
-        (void)hipStreamDestroy(ctx->side);
-    if (ctx->fork)
-        (void)hipEventDestroy(ctx->fork);
-    if (ctx->join)
-        (void)hipEventDestroy(ctx->join);
     delete ctx;
     return 0;
 }
@@ -462,6 +420,9 @@ int fdfs_gpu_reserve(fdfs_gpu_ctx *ctx, uint64_t max_files, uint64_t max_records
 
 const char *fdfs_gpu_last_error(fdfs_gpu_ctx *ctx) { return ctx ? ctx->err : "null context"; }
 
+#ifdef FDFS_TEST_HOOKS  // the test build only (make test-hooks): not in the shipped library
+#include "fdfs_test_hooks.h"
+
 int fdfs_gpu_inject_error(fdfs_gpu_ctx *ctx, void *stream)
 {
     if (!ctx)
@@ -473,6 +434,7 @@ int fdfs_gpu_inject_error(fdfs_gpu_ctx *ctx, void *stream)
     const hipError_t e = lane_err_note(ctx, nullptr, reinterpret_cast<hipStream_t>(stream));
     return e == hipSuccess ? 0 : fail(ctx, e, "inject_error");
 }
+#endif
 
 int fdfs_gpu_set_timing(fdfs_gpu_ctx *ctx, int enable)
 {

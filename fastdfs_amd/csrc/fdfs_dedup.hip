@@ -285,7 +285,6 @@ struct DpOut {
 // K1: keys, the singleton answer (rep = own gidx, ref = 1) of every record,
 // and the tile's entries sorted by digit (top d1 bits; unstable: order inside
 // a partition does not matter) written back as one contiguous run.
-template <bool DEF>
 __global__ __launch_bounds__(kDpTileThreads) void dp_tile_kernel(
     const uint8_t *__restrict__ sig, uint32_t stride, const uint64_t *__restrict__ gidx,
     uint32_t gstride, uint64_t n, int d1, uint64_t tiles, uint64_t *__restrict__ ent1,
@@ -312,10 +311,9 @@ __global__ __launch_bounds__(kDpTileThreads) void dp_tile_kernel(
             load_sig(sig + r * stride, a, b, c);
             key[it] = (uint32_t)sig_hash(a, b, c);
             // every record starts as its own class; dp_group overwrites the
-            // records of classes with more than one member (!DEF: dp_split
-            // writes these instead)
-            if constexpr (DEF)
-                out.store(r, gstride ? gidx[r * gstride] : r, 1u, true);
+            // records of classes with more than one member (writing these
+            // from dp_split instead measured neutral)
+            out.store(r, gstride ? gidx[r * gstride] : r, 1u, true);
         }
     }
 #pragma unroll
@@ -411,26 +409,13 @@ __device__ __forceinline__ uint32_t dp_sw(uint32_t i) { return i ^ (((i >> 4) & 
 
 // NB: digit bins (1 << d2 <= NB); 1024 bins keep the LDS at 72 KB, two
 // workgroups per CU.
-// DEF: the singleton answers of records [g * kDpChunk, (g + 1) * kDpChunk)
-// are written here (coalesced, beside the chunk's gather) instead of by
-// dp_tile; every chunk index below ceil(n / kDpChunk) is a real chunk (the
-// buckets' chunk counts sum to at least that).
-template <int NB, bool DEF>
+template <int NB>
 __global__ __launch_bounds__(kDpSplitThreads) void dp_split_kernel(
     const uint64_t *__restrict__ ent1, int d1, int d2, uint64_t tiles, const uint64_t *__restrict__ off1,
     const uint32_t *__restrict__ loc1, const uint32_t *__restrict__ cb, const uint32_t *__restrict__ chunk_ta,
     const uint4 *__restrict__ chunk_hd, uint64_t *__restrict__ ent2, uint16_t *__restrict__ cdo,
     DpOut out, const uint64_t *__restrict__ gidx, uint32_t gstride, uint64_t n)
 {
-    if constexpr (DEF) {
-        const uint64_t r0 = (uint64_t)blockIdx.x * kDpChunk;
-#pragma unroll
-        for (int q = 0; q < kDpSplitPer; q++) {
-            const uint64_t r = r0 + (uint64_t)q * kDpSplitThreads + threadIdx.x;
-            if (r < n)
-                out.store(r, gstride ? gidx[r * gstride] : r, 1u, true);
-        }
-    }
     constexpr int NT = kDpSplitThreads;
     constexpr int PER = NB / NT;
     static_assert(NB % NT == 0, "bins per thread");
@@ -732,10 +717,7 @@ __device__ __forceinline__ uint32_t dp_cn(const uint32_t *cn, uint32_t l)
 // The LDS grouping of one partition whose key halves and records (kh, rc)
 // are in registers, entry k of this thread at local index threadIdx.x + k *
 // 512.  Ends with a barrier.
-// probe: measurement build only (make probes), FDFS_GPU_DEDUP_PROBE bit 0 =
-// no confirmation reads (every equal key taken as equal), bit 1 = no final
-// stores; results are wrong under either
-template <int PROBE, int GM>
+template <int GM>
 __device__ __forceinline__ void dp_group_lds(DpLds<GM> &L, const DpArgs &A, const uint32_t (&kh)[kDpEpt],
                                              const uint32_t (&rc)[kDpEpt], uint32_t cnt)
 {
@@ -782,31 +764,29 @@ __device__ __forceinline__ void dp_group_lds(DpLds<GM> &L, const DpArgs &A, cons
         const uint32_t r = L.rec[l];
         uint32_t o = L.rec[own];
         uint64_t gl = r, go = o;
-        if constexpr (!(PROBE & 1)) {
-            uint64_t ra, rb, rcc, oa, ob, oc;
-            load_sig(A.sig + (uint64_t)r * A.stride, ra, rb, rcc);
-            load_sig(A.sig + (uint64_t)o * A.stride, oa, ob, oc);
-            if constexpr (GM != GM_INDEX) {
-                gl = gidx_of(A.out, A.sig, A.stride, GM, r);
-                go = gidx_of(A.out, A.sig, A.stride, GM, o);
+        uint64_t ra, rb, rcc, oa, ob, oc;
+        load_sig(A.sig + (uint64_t)r * A.stride, ra, rb, rcc);
+        load_sig(A.sig + (uint64_t)o * A.stride, oa, ob, oc);
+        if constexpr (GM != GM_INDEX) {
+            gl = gidx_of(A.out, A.sig, A.stride, GM, r);
+            go = gidx_of(A.out, A.sig, A.stride, GM, o);
+        }
+        if (!(ra == oa && rb == ob && rcc == oc)) {
+            // a key-bit collision with a different signature (rare):
+            // walk on from the slot it met -- the first slot with its
+            // key bits along its probe sequence, found again because
+            // every slot is set once -- confirming each equal key
+            const uint32_t key = (uint32_t)sig_hash(ra, rb, rcc), kb = key & kDpKeyMask;
+            uint32_t slot = dp_lprobe(L.word, kb, l, dp_home(key, kDpSlots), own);
+            for (;;) {
+                slot = dp_lprobe(L.word, kb, l, dp_next(slot, kDpSlots), own);
+                if (own == l)
+                    break;  // claimed a slot of its own
+                o = L.rec[own];
+                if (sig_equal(A.sig, A.stride, r, o))
+                    break;
             }
-            if (!(ra == oa && rb == ob && rcc == oc)) {
-                // a key-bit collision with a different signature (rare):
-                // walk on from the slot it met -- the first slot with its
-                // key bits along its probe sequence, found again because
-                // every slot is set once -- confirming each equal key
-                const uint32_t key = (uint32_t)sig_hash(ra, rb, rcc), kb = key & kDpKeyMask;
-                uint32_t slot = dp_lprobe(L.word, kb, l, dp_home(key, kDpSlots), own);
-                for (;;) {
-                    slot = dp_lprobe(L.word, kb, l, dp_next(slot, kDpSlots), own);
-                    if (own == l)
-                        break;  // claimed a slot of its own
-                    o = L.rec[own];
-                    if (sig_equal(A.sig, A.stride, r, o))
-                        break;
-                }
-                go = GM == GM_INDEX ? (uint64_t)o : gidx_of(A.out, A.sig, A.stride, GM, o);
-            }
+            go = GM == GM_INDEX ? (uint64_t)o : gidx_of(A.out, A.sig, A.stride, GM, o);
         }
         if (own != l) {
             atomicAdd(&L.cn[own >> 1], 1u << (16 * (own & 1)));
@@ -816,30 +796,28 @@ __device__ __forceinline__ void dp_group_lds(DpLds<GM> &L, const DpArgs &A, cons
     }
     __syncthreads();
     // (3) answers of the records of multi-member classes
-    if constexpr (!(PROBE & 2)) {
 #pragma unroll
-        for (int k = 0; k < kDpEpt; k++) {
-            const uint32_t l = threadIdx.x + k * NT;
-            if ((claim >> k) & 1u) {
-                const uint32_t c = dp_cn(L.cn, l);
-                if (c > 1) {
-                    const uint64_t m = L.mn[l];
-                    // the class's first record keeps dp_tile's rep = r
-                    A.out.store(rc[k], m, c, GM != GM_INDEX || m != rc[k]);
-                }
+    for (int k = 0; k < kDpEpt; k++) {
+        const uint32_t l = threadIdx.x + k * NT;
+        if ((claim >> k) & 1u) {
+            const uint32_t c = dp_cn(L.cn, l);
+            if (c > 1) {
+                const uint64_t m = L.mn[l];
+                // the class's first record keeps dp_tile's rep = r
+                A.out.store(rc[k], m, c, GM != GM_INDEX || m != rc[k]);
             }
         }
-        for (uint32_t j = threadIdx.x; j < nj; j += NT) {
-            const uint32_t e = L.jl[j];
-            const uint32_t l = e & 0xFFFFu, own = e >> 16;
-            const uint32_t c = dp_cn(L.cn, own);
-            if (c > 1) {
-                const uint32_t r = L.rec[l];
-                const uint64_t m = L.mn[own];
-                // with no gidx a listed entry may be its class's first record
-                // too (the claimer is whichever entry probed first)
-                A.out.store(r, m, c, GM != GM_INDEX || m != r);
-            }
+    }
+    for (uint32_t j = threadIdx.x; j < nj; j += NT) {
+        const uint32_t e = L.jl[j];
+        const uint32_t l = e & 0xFFFFu, own = e >> 16;
+        const uint32_t c = dp_cn(L.cn, own);
+        if (c > 1) {
+            const uint32_t r = L.rec[l];
+            const uint64_t m = L.mn[own];
+            // with no gidx a listed entry may be its class's first record
+            // too (the claimer is whichever entry probed first)
+            A.out.store(r, m, c, GM != GM_INDEX || m != r);
         }
     }
     __syncthreads();
@@ -891,7 +869,7 @@ __device__ __forceinline__ void dp_group_slow(DpLds<GM> &L, const DpArgs &A, con
             __syncthreads();
             l0 = l1;
         }
-        dp_group_lds<0, GM>(L, A, kh, rc, cnt);
+        dp_group_lds<GM>(L, A, kh, rc, cnt);
         return;
     }
     const uint64_t vs = R.bs + below;
@@ -959,7 +937,7 @@ __device__ __forceinline__ void dp_runs_of(uint32_t q, int d2, uint64_t tiles, c
     R.bsize = off1[(uint64_t)(b + 1) * tiles] - R.bs;
 }
 
-template <int PROBE, int GM>
+template <int GM>
 __global__ __launch_bounds__(kDpGroupThreads) __attribute__((amdgpu_waves_per_eu(GM == GM_INDEX ? 8 : 6))) void dp_group_kernel(
     const uint64_t *__restrict__ ent2, int d2, uint64_t tiles, const uint64_t *__restrict__ off1,
     const uint32_t *__restrict__ cb, const uint16_t *__restrict__ cdo, const uint8_t *__restrict__ sig,
@@ -992,7 +970,7 @@ __global__ __launch_bounds__(kDpGroupThreads) __attribute__((amdgpu_waves_per_eu
     }
     __syncthreads();  // run table reads done before the table init
     const DpArgs A{ent2, sig, stride, GM, nullptr, nullptr, nullptr, nullptr, out};
-    dp_group_lds<PROBE, GM>(L, A, kh, rc, cnt);
+    dp_group_lds<GM>(L, A, kh, rc, cnt);
 }
 
 // The listed partitions (slow[0] of them), a few persistent workgroups.
@@ -1068,70 +1046,33 @@ hipError_t launch_dedup_group(const uint8_t *sig, uint32_t sig_stride, const uin
     hipError_t e;
     if (ev0)
         (void)hipEventRecord(ev0, st);
-#ifdef FDFS_PROBES
-    // measurement build only: FDFS_GPU_DEDUP_DEF=1 -> the singleton answers
-    // are written by dp_split instead of dp_tile
-    static int defs = -1;
-    if (defs < 0) {
-        const char *ev = getenv("FDFS_GPU_DEDUP_DEF");
-        defs = ev ? atoi(ev) : 0;
-    }
-    const bool split_def = defs == 1;
-    if (split_def)
-        dp_tile_kernel<false><<<(unsigned)pl.tiles, kDpTileThreads, 0, st>>>(sig, sig_stride, gidx, gidx_stride, n,
-                                                                             pl.d1, pl.tiles, ent1, out, cnt1, loc1);
-    else
-#endif
-        dp_tile_kernel<true><<<(unsigned)pl.tiles, kDpTileThreads, 0, st>>>(sig, sig_stride, gidx, gidx_stride, n,
-                                                                            pl.d1, pl.tiles, ent1, out, cnt1, loc1);
+    dp_tile_kernel<<<(unsigned)pl.tiles, kDpTileThreads, 0, st>>>(sig, sig_stride, gidx, gidx_stride, n, pl.d1,
+                                                                  pl.tiles, ent1, out, cnt1, loc1);
     if ((e = launch_exclusive_scan(cnt1, ncnt, off1, bsum, st)) != hipSuccess)
         return e;
     dp_chunks_kernel<<<1, 256, 0, st>>>(off1, pl.d1, pl.tiles, cb, slow);
     dp_chunk_ta_kernel<<<grid_for(ncnt, 256), 256, 0, st>>>(off1, pl.tiles, ncnt, cb, chunk_ta, chunk_hd);
-#define DP_SPLIT(NB, D)                                                                                  \
-    dp_split_kernel<NB, D><<<(unsigned)pl.chunks, kDpSplitThreads, 0, st>>>(                             \
+#define DP_SPLIT(NB)                                                                                     \
+    dp_split_kernel<NB><<<(unsigned)pl.chunks, kDpSplitThreads, 0, st>>>(                                \
         ent1, pl.d1, pl.d2, pl.tiles, off1, loc1, cb, chunk_ta, chunk_hd, ent2, cdo, out, gidx, gidx_stride, n)
-#ifdef FDFS_PROBES
     if (pl.d2 <= 10)
-        split_def ? DP_SPLIT(1024, true) : DP_SPLIT(1024, false);
+        DP_SPLIT(1024);
     else
-        split_def ? DP_SPLIT(1 << kDpMaxD2, true) : DP_SPLIT(1 << kDpMaxD2, false);
-#else  // dp_tile writes the singleton answers (the DEF form measured neutral)
-    if (pl.d2 <= 10)
-        DP_SPLIT(1024, false);
-    else
-        DP_SPLIT(1 << kDpMaxD2, false);
-#endif
+        DP_SPLIT(1 << kDpMaxD2);
 #undef DP_SPLIT
     const int gmode = !gidx_stride ? GM_INDEX
                       : (gidx == reinterpret_cast<const uint64_t *>(sig + 24) && 8 * gidx_stride == sig_stride)
                           ? GM_ROW
                           : GM_REP;
-#define DP_GROUP(P, G)                                                                                       \
-    dp_group_kernel<P, G><<<(unsigned)pl.nparts(), kDpGroupThreads, 0, st>>>(ent2, pl.d2, pl.tiles, off1, cb, cdo, \
-                                                                           sig, sig_stride, out, slow)
-#ifdef FDFS_PROBES
-    // measurement build only (make probes): FDFS_GPU_DEDUP_PROBE bit 0 = no
-    // confirmation reads, bit 1 = no final stores (wrong results)
-    static int probe = -1;
-    if (probe < 0) {
-        const char *ev = getenv("FDFS_GPU_DEDUP_PROBE");
-        probe = ev ? atoi(ev) : 0;
-    }
-    if (probe == 1 && gmode == GM_INDEX)
-        DP_GROUP(1, GM_INDEX);
-    else if (probe == 2 && gmode == GM_INDEX)
-        DP_GROUP(2, GM_INDEX);
-    else if (probe == 3 && gmode == GM_INDEX)
-        DP_GROUP(3, GM_INDEX);
-    else
-#endif
+#define DP_GROUP(G)                                                                                       \
+    dp_group_kernel<G><<<(unsigned)pl.nparts(), kDpGroupThreads, 0, st>>>(ent2, pl.d2, pl.tiles, off1, cb, cdo, sig, \
+                                                                        sig_stride, out, slow)
     if (gmode == GM_ROW)
-        DP_GROUP(0, GM_ROW);
+        DP_GROUP(GM_ROW);
     else if (gmode == GM_REP)
-        DP_GROUP(0, GM_REP);
+        DP_GROUP(GM_REP);
     else
-        DP_GROUP(0, GM_INDEX);
+        DP_GROUP(GM_INDEX);
 #undef DP_GROUP
     if (gmode == GM_ROW)
         dp_group_slow_kernel<GM_ROW><<<256, kDpGroupThreads, 0, st>>>(ent2, pl.d2, pl.tiles, off1, cb, cdo, sig,

@@ -27,7 +27,7 @@ uint64_t scan_workspace_elems(uint64_t n);
 // sequence is captured in a hipGraph; see zero_u32_kernel).
 hipError_t launch_zero_u32(void *p, uint64_t ndwords, hipStream_t st);
 // count += 1 if *word != 0 (word == nullptr: unconditionally), one thread.
-hipError_t launch_lane_err_count(const uint32_t *word, uint64_t *count, hipStream_t st);
+hipError_t launch_lane_err_count(const uint32_t *word, uint64_t *count, uint64_t *slot, hipStream_t st);
 hipError_t launch_exclusive_scan(const uint64_t *in, uint64_t n, uint64_t *out, uint64_t *bsum,
                                  hipStream_t st);
 // Lane paths: files of at least a threshold T get their CRC (and for HASH
@@ -46,31 +46,6 @@ struct BigCrcWs {  // device arrays of n entries (seg_first n + 1)
     uint64_t *big_min;   // [1]: the T big_plan_kernel chose (read by the lane kernel)
     uint32_t lat_files;  // host: batches up to this many files choose T adaptively (0: never)
     uint32_t ncu = 0;    // host: the context device's CU count (fdfs_gpu_open), sizes persistent grids
-    uint32_t md5_bin = 0;  // MD5 batches above lat_files: T = the lower bound of this size bin (0: no offload)
-    // side != nullptr: the segmented kernels run on `side`, concurrently with
-    // the lane kernel (fork after big_plan_kernel, join before the patch)
-    hipStream_t side = nullptr;
-    hipEvent_t fork = nullptr, join = nullptr;
-    bool side_late = false;  // the segmented kernels enqueued after the lane kernel (host order)
-    // MD5 batches above lat_files: the offloaded files' CRC segments are items
-    // of md5_pair_kernel's own queue after its MD5 chunks (no crc_seg launch)
-    bool md5_inline = false;
-    // with md5_inline: offload the CRC of the tail chunks (those after the
-    // pair kernel's first G = its grid) instead of the files >= T
-    bool md5_tail = false;
-};
-// The CRC segment items md5_pair_kernel takes once its MD5 chunks are gone
-// (nbig == nullptr: none): the 64 KiB segments of big_plan_kernel's list
-// (the files >= T, whose loader lanes skipped their CRC), each XORed into
-// crc[i] advanced to its file's end (crc zeroed by big_plan_kernel).
-struct PairSegs {
-    const uint32_t *nbig = nullptr;
-    const uint64_t *offs = nullptr, *sizes = nullptr, *seg_first = nullptr;
-    uint32_t *crc = nullptr;
-    // the loader lanes of chunks >= crc_chunks skip the CRC too (tail
-    // offload: the chunks taken after the first G, whose files big_plan's
-    // tail form lists)
-    uint32_t crc_chunks = ~0u;
 };
 hipError_t launch_poly_seg(const uint8_t *base, const uint64_t *boffs, const uint64_t *bsizes,
                            const uint64_t *seg_first, const uint32_t *nbig, uint32_t *bpoly,
@@ -93,7 +68,7 @@ hipError_t launch_md5_stage(bool sar, const uint8_t *base, const uint64_t *offs,
                             const uint64_t *sizes, uint32_t n, const uint32_t *order,
                             const DevTables *tabs, const uint64_t *big_min, uint32_t *queue, uint32_t *crc_out,
                             uint8_t *sig_out, int32_t *codes_out, fdfs_gpu_file_state *states,
-                            const uint32_t *sidx, unsigned ncu, const PairSegs *segs, hipStream_t st);
+                            const uint32_t *sidx, unsigned ncu, hipStream_t st);
 hipError_t launch_sig_hash(bool sar, const uint8_t *base, const uint64_t *offs,
                            const uint64_t *sizes, uint32_t n, const uint32_t *order,
                            const DevTables *tabs, const uint64_t *big_min, uint32_t *crc_out, uint8_t *sig_out,
@@ -154,7 +129,6 @@ hipError_t launch_crc_fold(const CrcParts &blk, uint32_t nranks, const uint64_t 
 uint32_t sidx_table_size(uint32_t n);
 hipError_t launch_sidx_check(const uint32_t *sidx, uint32_t n, uint32_t *table, uint32_t *flag, hipStream_t st);
 int crc_seg_blocks_per_cu();
-int crc_table_mode();
 
 // formats, FastDHT routing, scrub (fdfs_format.hip)
 hipError_t launch_file_ids(bool sar, uint32_t server_id, const uint32_t *crc32, const int64_t *size,

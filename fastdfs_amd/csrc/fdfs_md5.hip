@@ -9,8 +9,6 @@
 #include "fdfs_md5.hpp"
 #include "fdfs_segcrc.hpp"
 
-#include <cstdlib>
-
 namespace fdfs {
 
 __device__ __forceinline__ void store_sig(uint8_t *sig, uint64_t L, uint32_t w2, uint32_t w3,
@@ -328,8 +326,8 @@ __global__ __launch_bounds__(64 * kMd5Waves) void md5_stage_kernel(
 // loads stays in flight across it (__syncthreads would wait for them).
 // Four workgroups per CU (35.8 KB of LDS each), the same 64 MD5 lanes per
 // SIMD as the fused form's one wave per SIMD.
-// Issue priority from a wave-uniform count of remaining 128-byte rounds
-// (production; probe PM 6 leaves it out): the waves with the most work left
+// Issue priority from a wave-uniform count of remaining 128-byte rounds:
+// the waves with the most work left
 // issue first on their SIMDs -- longest-remaining-first, the LPT rule applied
 // to the SIMD's issue arbiter -- against the hardware's oldest-wave-first
 // default, which favours the workgroups dispatched first whatever they have
@@ -357,96 +355,12 @@ __device__ __forceinline__ void pair_barrier()
     asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
 }
 
-#ifdef FDFS_PROBES
-// PM 5 (probe build): per workgroup {start, end} wall clock (s_memrealtime,
-// 100 MHz), chunks taken, 128-byte rounds run, HW_ID and XCC_ID, read back
-// by fdfs_gpu_probe_pairs (scripts/pair_timeline.py): where the batch's time
-// ends, pair by pair.
-constexpr int kPairProbeMax = 8192;
-__device__ uint64_t g_pair_probe[kPairProbeMax * 8];  // [wg][8]: 4 words above, then first chunk, its end, rounds
-#endif
-
-// CRC segment items (PairSegs): after the MD5 chunks the workgroup's waves
-// take 64 KiB segments of the offloaded files from the same queue, one per
-// wave at a time -- queue index nw + s is segment s -- so the CRC of the
-// largest files (whose loader lanes skipped it) is computed by the pairs
-// whose chunks ended first, while the largest MD5 chains still run, instead
-// of beside those chains on their SIMDs.  Each segment's
-// zero-init CRC (crc_segment, the wave's 64 lanes over 1 KiB each) is
-// advanced to its file's end and XORed into segs.crc[i] (CRC32_ex is linear
-// over GF(2); big_patch_kernel writes the files' crc_out).  Called by both
-// waves right after the chunk fetch that found no MD5 chunk (that fetch's
-// barriers end every use of sD / sbuf); `first` = that fetch's item, taken by
-// the MD5 wave.  The segmented kernel's tables replace the pair's: the
-// complemented slice tables for SAR (crc_seg_kernel's domain) and ADV4032 in
-// the staging buffer; the reduction tables are read from global memory.
 template <bool SAR>
-__device__ __forceinline__ void pair_crc_items(const PairSegs &segs, const uint8_t *base, const DevTables *tabs,
-                                               uint32_t *queue, uint32_t nw, uint32_t first, bool loader,
-                                               uint32_t *sD, const uint32_t *sT, uint32_t *sA)
-{
-    const uint32_t nb = *segs.nbig;
-    const uint64_t total = segs.seg_first[nb];
-    if (total == 0)
-        return;  // workgroup-uniform
-    if (SAR)
-        lds_fill(sD, &tabs->Dc[0][0], 16 * 256);
-    lds_fill(sA, &tabs->t.ADV4032[0][0], 4 * 256);
-    __syncthreads();
-    const int lane = threadIdx.x & 63;
-    const Rep8Lane R8 = rep8_lane(lane);  // unused by the TM 0 tables
-    const uint32_t K16 = tabs->t.K16;
-    const uint32_t *sR = &tabs->t.ADVRED[0][0][0];
-    uint64_t s = first;
-    if (loader) {  // the MD5 wave keeps the workgroup's item, the loader fetches its own
-        uint32_t got = 0;
-        if (lane == 0)
-            got = atomicAdd(queue, 1u);
-        s = (uint64_t)__shfl(got, 0) - nw;
-    }
-    while (s < total) {
-        uint32_t lo = 0, hi = nb;  // last i with seg_first[i] <= s
-        while (hi - lo > 1) {
-            const uint32_t mid = (lo + hi) >> 1;
-            if (segs.seg_first[mid] <= s)
-                lo = mid;
-            else
-                hi = mid;
-        }
-        const uint32_t i = lo;
-        const uint64_t k = s - segs.seg_first[i];
-        const uint64_t L = segs.sizes[i];
-        const uint64_t lo_b = k * kSegBytes;
-        const uint64_t hi_b = (L < lo_b + kSegBytes) ? L : lo_b + kSegBytes;
-        const uint32_t v = crc_segment<SAR, 0>(sD, sT, sA, sR, R8, K16, base + segs.offs[i] + lo_b, hi_b - lo_b,
-                                               k == 0, lane);
-        const uint32_t adv = advance_any(tabs, v, L - hi_b, lane);
-        if (lane == 0)
-            atomicXor(&segs.crc[i], adv ^ (k == 0 ? crc_final_const<SAR>(L) : 0u));
-        uint32_t got = 0;
-        if (lane == 0)
-            got = atomicAdd(queue, 1u);
-        s = (uint64_t)__shfl(got, 0) - nw;
-    }
-}
-
-// PM: probe mode, a template parameter so that the production
-// instantiation (PM 0) carries no probe branch; PM != 0 is instantiated only
-// in the probe build (make probes): 1 = MD5 wave at s_setprio 2, 2 = no CRC
-// arithmetic, 3 = no MD5 arithmetic (wrong results), 4 = both waves at
-// s_setprio 2 while their chunk is among the largest quarter (the chunks
-// that end the batch), 0 after; 5 = per-workgroup timeline; 6 = no issue
-// priority (round 3's production form); 7 = young chunks first; 8 = static
-// boustrophedon chunk pairing (chunk w, then 2G - 1 - w); 9 / 10 = the
-// priority in 512 KiB / 2 MiB units; 11 = re-evaluated every 64 rounds.  PM 0
-// (production) sets the longest-remaining-first priority (prio_by_remaining).
-template <bool SAR, int PM>
 __global__ __launch_bounds__(128) void md5_pair_kernel(
     const uint8_t *__restrict__ base, const uint64_t *__restrict__ offs,
     const uint64_t *__restrict__ sizes, const uint32_t *__restrict__ order, uint32_t n,
     const DevTables *__restrict__ tabs, const uint64_t *__restrict__ big_min_p, uint32_t *__restrict__ queue,
-    uint32_t *__restrict__ crc_out, uint8_t *__restrict__ sig_out, int32_t *__restrict__ codes_out,
-    PairSegs segs)
+    uint32_t *__restrict__ crc_out, uint8_t *__restrict__ sig_out, int32_t *__restrict__ codes_out)
 {
     constexpr int CH = kMd5Chunk;
     constexpr int PIECES = CH / 16;
@@ -465,73 +379,19 @@ __global__ __launch_bounds__(128) void md5_pair_kernel(
     typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
     // wave-uniform role (an SGPR, so both roles' barriers are scalar branches)
     const bool loader = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6) != 0;
-    if constexpr (PM == 1) {
-        if (!loader)
-            __builtin_amdgcn_s_setprio(2);
-    }
     const int lane = threadIdx.x & 63;
     const uint32_t nw = (n + 63) / 64;
     const uint8_t *safe = reinterpret_cast<const uint8_t *>(tabs);
     const uint32_t K16 = tabs->t.K16;
     const uint64_t big_min = big_min_p ? *big_min_p : ~0ull;
-#ifdef FDFS_PROBES
-    uint64_t pr_t0 = 0, pr_chunks = 0, pr_rounds = 0;
-    if constexpr (PM == 5)
-        pr_t0 = wall_clock64();
-#endif
-    uint32_t first_item = 0;  // the queue index past the MD5 chunks that ended the loop
-    uint32_t kch = 0;         // chunks this workgroup has taken
     for (;;) {
-        if (threadIdx.x == 64) {
-            if constexpr (PM == 8) {
-                // static boustrophedon pairing: workgroup w takes chunk w,
-                // then chunk 2G - 1 - w (the largest first chunks get no
-                // second one, the smallest get the largest of the rest), then
-                // the queue from 2G (batches of more than 2G chunks)
-                const uint32_t G = gridDim.x, c2 = 2 * G - 1 - blockIdx.x;
-                s_chunk = kch == 0 ? blockIdx.x : (kch == 1 && c2 < nw) ? c2 : 2 * G + atomicAdd(queue, 1u);
-            } else {
-                s_chunk = atomicAdd(queue, 1u);
-            }
-        }
-        kch++;
+        if (threadIdx.x == 64)
+            s_chunk = atomicAdd(queue, 1u);
         __syncthreads();
         const uint32_t chunk = __builtin_amdgcn_readfirstlane(s_chunk);
         __syncthreads();  // s_chunk read by both waves before the next chunk's write
-        if (chunk >= nw) {
-#ifdef FDFS_PROBES
-            if constexpr (PM == 5) {
-                if (threadIdx.x == 0 && blockIdx.x < kPairProbeMax) {
-                    const uint32_t hw = __builtin_amdgcn_s_getreg((4) | (0 << 6) | (31 << 11));
-                    const uint32_t xcc = __builtin_amdgcn_s_getreg((20) | (0 << 6) | (31 << 11));
-                    uint64_t *o = g_pair_probe + 8ull * blockIdx.x;
-                    o[0] = pr_t0;
-                    o[1] = wall_clock64();
-                    o[2] = pr_chunks | (pr_rounds << 20);
-                    o[3] = (uint64_t)hw | ((uint64_t)xcc << 32);
-                }
-            }
-#endif
-            first_item = chunk - nw;
+        if (chunk >= nw)
             break;
-        }
-        if constexpr (PM == 4) {
-            if (chunk < nw / 4)
-                __builtin_amdgcn_s_setprio(2);
-            else
-                __builtin_amdgcn_s_setprio(0);
-        }
-        if constexpr (PM == 7) {  // the last-dispatched first chunks and every later chunk first
-            const uint32_t q = chunk < gridDim.x ? chunk * 4 / gridDim.x : 3;
-            if (q >= 3)
-                __builtin_amdgcn_s_setprio(3);
-            else if (q == 2)
-                __builtin_amdgcn_s_setprio(2);
-            else if (q == 1)
-                __builtin_amdgcn_s_setprio(1);
-            else
-                __builtin_amdgcn_s_setprio(0);
-        }
         const uint32_t i = chunk * 64 + lane;
         bool valid = i < n;
         uint32_t f = valid ? order[i] : 0;
@@ -550,41 +410,8 @@ __global__ __launch_bounds__(128) void md5_pair_kernel(
         }
         const uint64_t rounds = (mx + BPR - 1) / BPR;
         const uint8_t *tp = p + (nblk << 6);
-        uint64_t after = 0;  // PM 8: rounds of the chunk this workgroup takes next (its priority counts them)
-        if constexpr (PM == 8) {
-            const uint32_t c2 = 2 * gridDim.x - 1 - blockIdx.x;
-            if (kch == 1 && c2 < nw) {
-                const uint32_t i2 = c2 * 64 + lane;
-                const uint32_t f2 = i2 < n ? order[i2] : n;
-                uint64_t m2 = f2 < n ? (sizes[f2] >> 6) : 0;
-#pragma unroll
-                for (int o = 32; o; o >>= 1) {
-                    const uint64_t y = __shfl_xor(m2, o);
-                    m2 = y > m2 ? y : m2;
-                }
-                after = (m2 + BPR - 1) / BPR;
-            }
-        }
-#ifdef FDFS_PROBES
-        if constexpr (PM == 5) {
-            if (threadIdx.x == 0 && blockIdx.x < kPairProbeMax) {
-                uint64_t *o = g_pair_probe + 8ull * blockIdx.x;
-                if (pr_chunks == 1)
-                    o[5] = wall_clock64();  // the first chunk ended (this is the second)
-                if (pr_chunks == 0) {
-                    o[4] = chunk;
-                    o[6] = rounds;
-                } else if (pr_chunks == 1) {
-                    o[7] = chunk;
-                }
-            }
-        }
-        pr_chunks += 1;
-        pr_rounds += rounds;
-#endif
         if (loader) {
-            // else the CRC comes from crc_seg_kernel or the CRC segment items
-            const bool small = L < big_min && chunk < segs.crc_chunks && PM != 2;
+            const bool small = L < big_min;  // else the CRC comes from crc_seg_kernel
             const int piece = lane % PIECES, fsub = lane / PIECES;
             const uint8_t *lp[NLD];
             uint64_t lim[NLD];
@@ -624,19 +451,8 @@ __global__ __launch_bounds__(128) void md5_pair_kernel(
             };
             issue(RA, 0);
             for (uint64_t r = 0; r < rounds; r += 2) {
-                if constexpr (PM == 0 || PM == 8) {
-                    if ((r & 255) == 0)
-                        prio_by_remaining(rounds - r + after);
-                } else if constexpr (PM == 9) {  // 512 KiB units
-                    if ((r & 255) == 0)
-                        prio_by_remaining<12>(rounds - r);
-                } else if constexpr (PM == 10) {  // 2 MiB units
-                    if ((r & 255) == 0)
-                        prio_by_remaining<14>(rounds - r);
-                } else if constexpr (PM == 11) {  // re-evaluated every 64 rounds
-                    if ((r & 63) == 0)
-                        prio_by_remaining(rounds - r);
-                }
+                if ((r & 255) == 0)
+                    prio_by_remaining(rounds - r);
                 issue(RB, r + 1);
                 stage(RA, sbuf[0]);
                 pair_barrier();
@@ -662,19 +478,8 @@ __global__ __launch_bounds__(128) void md5_pair_kernel(
             uint32_t st[4] = {0x67452301u, 0xefcdab89u, 0x98badcfeu, 0x10325476u};  // my_md5_init
             const uint8_t *mine = &sbuf[0][0] + lane * STRIDE;
             for (uint64_t r = 0; r < rounds; r++) {
-                if constexpr (PM == 0 || PM == 8) {
-                    if ((r & 255) == 0)
-                        prio_by_remaining(rounds - r + after);
-                } else if constexpr (PM == 9) {  // 512 KiB units
-                    if ((r & 255) == 0)
-                        prio_by_remaining<12>(rounds - r);
-                } else if constexpr (PM == 10) {  // 2 MiB units
-                    if ((r & 255) == 0)
-                        prio_by_remaining<14>(rounds - r);
-                } else if constexpr (PM == 11) {  // re-evaluated every 64 rounds
-                    if ((r & 63) == 0)
-                        prio_by_remaining(rounds - r);
-                }
+                if ((r & 255) == 0)
+                    prio_by_remaining(rounds - r);
                 pair_barrier();
                 const uint4 *q = reinterpret_cast<const uint4 *>(mine + (r & 1) * (64 * STRIDE));
                 // block b + 1's words are read from LDS (for every lane,
@@ -688,7 +493,7 @@ __global__ __launch_bounds__(128) void md5_pair_kernel(
                         for (int k = 0; k < 4; k++)
                             nxt[k] = q[4 * (b + 1) + k];
                     }
-                    if (r * BPR + b < nblk && PM != 3) {
+                    if (r * BPR + b < nblk) {
                         const uint32_t m[16] = {cur[0].x, cur[0].y, cur[0].z, cur[0].w, cur[1].x, cur[1].y,
                                                 cur[1].z, cur[1].w, cur[2].x, cur[2].y, cur[2].z, cur[2].w,
                                                 cur[3].x, cur[3].y, cur[3].z, cur[3].w};
@@ -711,90 +516,35 @@ __global__ __launch_bounds__(128) void md5_pair_kernel(
             }
         }
     }
-#ifdef FDFS_PROBES  // measured, not kept: BigCrcWs::md5_inline is set by the probe build only
-    if (segs.nbig)
-        pair_crc_items<SAR>(segs, base, tabs, queue, nw, first_item, loader, sD, sT,
-                            reinterpret_cast<uint32_t *>(&sbuf[0][0]));
-#else
-    (void)first_item;
-#endif
 }
 
 hipError_t launch_md5_stage(bool sar, const uint8_t *base, const uint64_t *offs,
                             const uint64_t *sizes, uint32_t n, const uint32_t *order,
                             const DevTables *tabs, const uint64_t *big_min, uint32_t *queue, uint32_t *crc_out,
                             uint8_t *sig_out, int32_t *codes_out, fdfs_gpu_file_state *states,
-                            const uint32_t *sidx, unsigned ncu, const PairSegs *segs, hipStream_t st)
+                            const uint32_t *sidx, unsigned ncu, hipStream_t st)
 {
     if (ncu == 0)
         return hipErrorInvalidValue;
-#ifdef FDFS_PROBES
-    static int mode = -1;
-    if (mode < 0) {  // A/B (make probes): FDFS_GPU_MD5_QUEUE=0 -> one chunk per wave, all resident
-        const char *ev = getenv("FDFS_GPU_MD5_QUEUE");
-        mode = ev ? atoi(ev) : 1;
-    }
-#else
-    constexpr int mode = 1;
-#endif
     constexpr unsigned kBlk = 64 * kMd5Waves;
     const uint32_t nw = (n + 63) / 64;
-#ifdef FDFS_PROBES
-    static int pair = -1;
-    if (pair < 0) {  // A/B (make probes): FDFS_GPU_MD5_PAIR=0 -> the fused kernel, 2.. -> md5_pair_kernel PM 1..
-        const char *ev = getenv("FDFS_GPU_MD5_PAIR");
-        pair = ev ? atoi(ev) : 1;
-    }
-#else
-    constexpr int pair = 1;
-#endif
-    if (pair != 0 && mode != 0 && queue && !states) {  // queue zeroed by the caller
+    if (queue && !states) {  // one-shot batches: the wave pairs (queue zeroed by the caller)
         const unsigned g = 4u * ncu;
         const unsigned grid2 = g < nw ? g : nw;
-        const PairSegs ps = segs ? *segs : PairSegs{};
-#define PAIR_LAUNCH(PM)                                                                                       \
-    (sar ? md5_pair_kernel<true, PM><<<grid2, 128, 0, st>>>(base, offs, sizes, order, n, tabs, big_min, queue, \
-                                                           crc_out, sig_out, codes_out, ps)                  \
-         : md5_pair_kernel<false, PM><<<grid2, 128, 0, st>>>(base, offs, sizes, order, n, tabs, big_min, queue, \
-                                                            crc_out, sig_out, codes_out, ps))
-#ifdef FDFS_PROBES
-        if (pair == 2)
-            PAIR_LAUNCH(1);
-        else if (pair == 3)
-            PAIR_LAUNCH(2);
-        else if (pair == 4)
-            PAIR_LAUNCH(3);
-        else if (pair == 5)
-            PAIR_LAUNCH(4);
-        else if (pair == 6)
-            PAIR_LAUNCH(5);
-        else if (pair == 7)
-            PAIR_LAUNCH(6);
-        else if (pair == 8)
-            PAIR_LAUNCH(7);
-        else if (pair == 9)
-            PAIR_LAUNCH(8);
-        else if (pair == 10)
-            PAIR_LAUNCH(9);
-        else if (pair == 11)
-            PAIR_LAUNCH(10);
-        else if (pair == 12)
-            PAIR_LAUNCH(11);
+        if (sar)
+            md5_pair_kernel<true><<<grid2, 128, 0, st>>>(base, offs, sizes, order, n, tabs, big_min, queue, crc_out,
+                                                         sig_out, codes_out);
         else
-#endif
-            PAIR_LAUNCH(0);
-#undef PAIR_LAUNCH
+            md5_pair_kernel<false><<<grid2, 128, 0, st>>>(base, offs, sizes, order, n, tabs, big_min, queue, crc_out,
+                                                          sig_out, codes_out);
         return hipGetLastError();
     }
     unsigned grid = (n + kBlk - 1) / kBlk;
-    uint32_t *q = nullptr;
-    if (mode && queue) {  // queue zeroed by the caller (launch_sig_lane's workspace memset)
-        q = queue;
+    if (queue)  // queue zeroed by the caller (launch_sig_lane's workspace memset)
         grid = ncu < (nw + kMd5Waves - 1) / kMd5Waves ? ncu : (nw + kMd5Waves - 1) / kMd5Waves;
-    }
     const uint32_t w1 = ncu * kMd5Waves;
-#define MD5_LAUNCH(S, T)                                                                              \
-    md5_stage_kernel<S, T><<<grid, kBlk, 0, st>>>(base, offs, sizes, order, n, tabs, big_min, w1, q, \
+#define MD5_LAUNCH(S, T)                                                                                  \
+    md5_stage_kernel<S, T><<<grid, kBlk, 0, st>>>(base, offs, sizes, order, n, tabs, big_min, w1, queue, \
                                                   crc_out, sig_out, codes_out, states, sidx)
     if (states)
         sar ? MD5_LAUNCH(true, true) : MD5_LAUNCH(false, true);
@@ -806,12 +556,3 @@ hipError_t launch_md5_stage(bool sar, const uint8_t *base, const uint64_t *offs,
 
 }  // namespace fdfs
 
-#ifdef FDFS_PROBES
-extern "C" int fdfs_gpu_probe_pairs(uint64_t *host, size_t words)
-{
-    if (words > 8ull * fdfs::kPairProbeMax)
-        words = 8ull * fdfs::kPairProbeMax;
-    return hipMemcpyFromSymbol(host, HIP_SYMBOL(fdfs::g_pair_probe), 8 * words, 0, hipMemcpyDeviceToHost) ==
-                   hipSuccess ? 0 : 5;
-}
-#endif

@@ -1,6 +1,5 @@
-// Segment-parallel CRC32_ex building blocks (device side), shared by
-// crc_seg_kernel (fdfs_sig.hip) and the CRC segment items md5_pair_kernel
-// takes after its MD5 chunks (fdfs_md5.hip).  Reference loop:
+// Segment-parallel CRC32_ex building blocks (device side) of crc_seg_kernel
+// (fdfs_sig.hip).  Reference loop:
 // storage/storage_dio.c:465-467 (CRC32_ex over each chunk).
 #pragma once
 #include "fdfs_device.hpp"
@@ -44,48 +43,15 @@ __device__ __forceinline__ uint4 seg_fix_vector(uint4 w, int64_t off, int64_t a0
 // 4 KiB block grid is aligned to the segment's last full vector, so the only
 // partial vector is the first (leading neutral bytes do not change a
 // zero-init state).  See DESIGN.md "K2 segmented CRC" for the algebra.
-// Table modes of the segmented kernel: 0 = 8-bit slice-by-16 (16 KiB, bank
-// conflicts; A/B reference), 2 = rotated replicated slice-by-8 (64 KiB,
-// conflict-free; K is then K8).
-template <bool SAR, int TM>
-__device__ __forceinline__ uint32_t chain16x(const uint32_t *sD, uint32_t lb, const Rep8Lane &R,
-                                             uint32_t c, uint4 w, uint32_t K)
-{
-    if constexpr (TM == 2)
-        return chain16r<SAR>(sD, R, c, w, K);
-    else
-        return chain16<SAR>(sD, c, w, K);
-}
-
-// QL: quad-cooperative loads -- in instruction q lane 4m + j reads vector
-// 16m + 4q + j of the block, so one instruction reads 16 contiguous 64-byte
-// pieces instead of 64 scattered 16-byte ones (half the lines per
-// instruction), and a 4 x 4 transpose per dword position within the lane
-// quad (quad_transpose, 8 VALU per 4 vectors) gives every lane its own
-// contiguous 64 bytes again -- the load pattern sig_hash_kernel uses.
-// NT (probe): the block loads as non-temporal loads.
-template <bool NT>
-__device__ __forceinline__ uint4 seg_load(const uint4 *p)
-{
-    if constexpr (NT) {
-        typedef uint32_t v4 __attribute__((ext_vector_type(4)));
-        const v4 r = __builtin_nontemporal_load(reinterpret_cast<const v4 *>(p));
-        return make_uint4(r.x, r.y, r.z, r.w);
-    } else {
-        return *p;
-    }
-}
-
-// PF (probe): 2 = two blocks in flight (the next two blocks' loads issued
-// before the first block is folded) instead of one.
-template <bool SAR, int TM, bool QL = false, bool NT = false, int PF = 1>
+// The tables are the rotated, replicated slice-by-8 form (64 KiB,
+// conflict-free; fdfs_device.hpp chain16r), with K = K8.
+template <bool SAR>
 __device__ __forceinline__ uint32_t crc_segment(const uint32_t *sD, const uint32_t *sT,
                                                 const uint32_t *sA, const uint32_t *sR,
-                                                const Rep8Lane &R8, uint32_t K16,
+                                                const Rep8Lane &R8, uint32_t K8,
                                                 const uint8_t *Ap, uint64_t len, bool first_seg,
                                                 int lane)
 {
-    const uint32_t lb = (uint32_t)(lane & 31) * 4u;
     const int64_t a0 = (int64_t)((uintptr_t)Ap & 15u);  // segment start within its vector
     const uint4 *v = reinterpret_cast<const uint4 *>(Ap - a0);
     const int64_t e_off = a0 + (int64_t)len;
@@ -96,21 +62,9 @@ __device__ __forceinline__ uint32_t crc_segment(const uint32_t *sD, const uint32
         const int64_t J = (nvec + 255) >> 8;
         const uint4 neutral = SAR ? make_uint4(~0u, ~0u, ~0u, ~0u) : make_uint4(0, 0, 0, 0);
         uint32_t acc = 0;
-        // QL: the vector lane `lane` loads as piece q (its quad's
-        // cooperative pattern); else its own vector q
-        const int qm = lane & ~3, qj = lane & 3;
-        auto lidx = [&](int64_t blk0, int q) -> int64_t {
-            return QL ? blk0 + 4 * qm + 4 * q + qj : blk0 + 4 * lane + q;
-        };
-        auto untangle = [&](uint4 (&w)[4]) {
-            if constexpr (QL) {
-                quad_transpose(w[0].x, w[1].x, w[2].x, w[3].x);
-                quad_transpose(w[0].y, w[1].y, w[2].y, w[3].y);
-                quad_transpose(w[0].z, w[1].z, w[2].z, w[3].z);
-                quad_transpose(w[0].w, w[1].w, w[2].w, w[3].w);
-            }
-        };
-        uint4 nx[4], nx2[4];
+        // lane `lane` folds vectors 4 lane .. 4 lane + 3 of each 4 KiB block
+        auto lidx = [&](int64_t blk0, int q) -> int64_t { return blk0 + 4 * lane + q; };
+        uint4 nx[4];
         {  // first (partial) block: vectors before index 0 are neutral
             const int64_t b0 = nvec - 256 * J;
             const int64_t vb = b0 + 4 * lane;
@@ -118,20 +72,8 @@ __device__ __forceinline__ uint32_t crc_segment(const uint32_t *sD, const uint32
 #pragma unroll
             for (int q = 0; q < 4; q++) {
                 const int64_t li = lidx(b0, q);
-                w[q] = seg_load<NT>(&v[li < 0 ? 0 : li]);
+                w[q] = v[li < 0 ? 0 : li];
             }
-            if (PF == 2 && J > 1) {  // blocks 1 and 2 in flight while block 0 is folded
-                // (block 0 may start before the segment: only blocks >= 1 are
-                // loaded here, the second clamped to the last block)
-                const int64_t j2 = J > 2 ? 2 : 1;
-#pragma unroll
-                for (int q = 0; q < 4; q++)
-                    nx[q] = seg_load<NT>(&v[lidx(nvec - 256 * (J - 1), q)]);
-#pragma unroll
-                for (int q = 0; q < 4; q++)
-                    nx2[q] = seg_load<NT>(&v[lidx(nvec - 256 * (J - j2), q)]);
-            }
-            untangle(w);
 #pragma unroll
             for (int q = 0; q < 4; q++) {
                 const int64_t vi = vb + q;
@@ -142,40 +84,32 @@ __device__ __forceinline__ uint32_t crc_segment(const uint32_t *sD, const uint32
             }
 #pragma unroll
             for (int q = 0; q < 4; q++)
-                acc = chain16x<SAR, TM>(sD, lb, R8, acc, w[q], K16);
+                acc = chain16r<SAR>(sD, R8, acc, w[q], K8);
         }
         // blocks 1..J-1: the next block's 64 B per lane is loaded while this
         // one is folded (index clamped on the last block: no branch)
-        if (PF == 1 && J > 1) {
+        if (J > 1) {
 #pragma unroll
             for (int q = 0; q < 4; q++)
-                nx[q] = seg_load<NT>(&v[lidx(nvec - 256 * (J - 1), q)]);
+                nx[q] = v[lidx(nvec - 256 * (J - 1), q)];
         }
         for (int64_t jb = 1; jb < J; jb++) {
             uint4 w[4];
 #pragma unroll
             for (int q = 0; q < 4; q++)
                 w[q] = nx[q];
-            if constexpr (PF == 2) {
-                const int64_t jn = (jb + 2 < J) ? jb + 2 : J - 1;
-#pragma unroll
-                for (int q = 0; q < 4; q++) {
-                    nx[q] = nx2[q];
-                    nx2[q] = seg_load<NT>(&v[lidx(nvec - 256 * (J - jn), q)]);
-                }
-            } else {
+            {
                 const int64_t jn = (jb + 1 < J) ? jb + 1 : jb;
 #pragma unroll
                 for (int q = 0; q < 4; q++)
-                    nx[q] = seg_load<NT>(&v[lidx(nvec - 256 * (J - jn), q)]);
+                    nx[q] = v[lidx(nvec - 256 * (J - jn), q)];
             }
-            untangle(w);
             acc = apply4(sA, acc);  // advance 4032 B to this lane's next piece
             if (jb == 1 && nvec - 256 * (J - 1) == 1 && lane == 0)
                 w[0] = seg_fix_vector<SAR>(w[0], 16, a0, xor4);  // vector 1 opens block 1
 #pragma unroll
             for (int q = 0; q < 4; q++)
-                acc = chain16x<SAR, TM>(sD, lb, R8, acc, w[q], K16);
+                acc = chain16r<SAR>(sD, R8, acc, w[q], K8);
         }
         // wave reduction: lane group values relative to the group's end
 #pragma unroll

@@ -1,9 +1,9 @@
 // libfdfs_gpu: segmented CRC32 kernel, planning kernels and launchers (gfx950).
 //
-//  * crc_seg_kernel<SAR, TM>: CRC32 only (the default upload path and the
+//  * crc_seg_kernel<SAR>: CRC32 only (the default upload path and the
 //    CRC of the MD5 method), one WAVE per 64 KiB segment of a file,
 //    coalesced 4 KiB strides, conflict-free rotated slice-by-8 tables in LDS
-//    (TM 2; TM 0 = plain slice-by-16 for A/B), a 6-level GF(2) combine across
+//    (the byte-table slice-by-16 form measured slower), a 6-level GF(2) combine across
 //    the wave, and a GF(2) matrix-power advance to combine segments of large
 //    files.
 //  * planning kernels: size-bin counting sort (lane-per-file paths), per-file
@@ -18,14 +18,12 @@
 #include "fdfs_kernels.hpp"
 #include "fdfs_segcrc.hpp"
 
-#include <cstdlib>
-
 namespace fdfs {
 
 // ------------------------------------------------------- segmented CRC path
 // (device helpers in fdfs_segcrc.hpp)
 
-template <bool SAR, int TM, bool QL = false, bool NT = false, int PF = 1>
+template <bool SAR>
 __global__ __launch_bounds__(kSegBlock) void crc_seg_kernel(
     const uint8_t *__restrict__ base, const uint64_t *__restrict__ offs,
     const uint64_t *__restrict__ sizes, const uint64_t *__restrict__ seg_first, uint32_t n_host,
@@ -38,25 +36,19 @@ __global__ __launch_bounds__(kSegBlock) void crc_seg_kernel(
         if ((total * w0) / nw == (total * (w0 + (blockDim.x >> 6))) / nw)
             return;
     }
-    // TM 2 (64 KiB conflict-free tables): the reduction tables stay in
-    // global memory (24 lookups per segment).  TM 0: everything in LDS.
-    constexpr int kD = TM == 2 ? kRep8Dwords : 16 * 256;
-    constexpr int kR = TM ? 0 : 6 * 4 * 256;
-    __shared__ uint32_t smem[kD + 256 + 2 * 4 * 256 + kR];
+    // the 64 KiB conflict-free tables in LDS; the reduction tables stay in
+    // global memory (24 lookups per segment)
+    constexpr int kD = kRep8Dwords;
+    __shared__ uint32_t smem[kD + 256 + 2 * 4 * 256];
     uint32_t *sD = smem, *sT = smem + kD, *sA = sT + 256, *sS = sA + 1024;
-    const uint32_t *sR = TM ? &tabs->t.ADVRED[0][0][0] : sS + 1024;
+    const uint32_t *sR = &tabs->t.ADVRED[0][0][0];
     lds_fill(sS, &tabs->t.ADVSEG[0][0], 4 * 256);
-    if constexpr (TM == 2)
-        lds_fill_rep8(sD, SAR ? &tabs->Dc[0][0] : &tabs->t.D[0][0]);
-    else
-        lds_fill(sD, SAR ? &tabs->Dc[0][0] : &tabs->t.D[0][0], 16 * 256);
+    lds_fill_rep8(sD, SAR ? &tabs->Dc[0][0] : &tabs->t.D[0][0]);
     lds_fill(sT, tabs->t.T, 256);
     lds_fill(sA, &tabs->t.ADV4032[0][0], 4 * 256);
-    if constexpr (!TM)
-        lds_fill(sS + 1024, &tabs->t.ADVRED[0][0][0], 6 * 4 * 256);
     __syncthreads();
 
-    const uint32_t K16 = TM == 2 ? tabs->t.K8 : tabs->t.K16;
+    const uint32_t K8 = tabs->t.K8;
     const Rep8Lane R8 = rep8_lane(threadIdx.x & 63);
     const int lane = threadIdx.x & 63;
     const uint64_t wpb = blockDim.x >> 6;
@@ -109,7 +101,7 @@ __global__ __launch_bounds__(kSegBlock) void crc_seg_kernel(
         const uint8_t *fp = base + offs[f];
         const uint64_t lo_b = k * kSegBytes;
         const uint64_t hi_b = (L < lo_b + kSegBytes) ? L : lo_b + kSegBytes;
-        const uint32_t v = crc_segment<SAR, TM, QL, NT, PF>(sD, sT, sA, sR, R8, K16, fp + lo_b, hi_b - lo_b, k == 0, lane);
+        const uint32_t v = crc_segment<SAR>(sD, sT, sA, sR, R8, K8, fp + lo_b, hi_b - lo_b, k == 0, lane);
         if (run_f == f) {
             const uint64_t len = hi_b - lo_b;
             const uint32_t adv = (len == kSegBytes) ? apply4(sS, run_state)
@@ -428,7 +420,7 @@ __device__ __forceinline__ uint64_t bin_lo(int b)
 __global__ __launch_bounds__(1024) void big_plan_kernel(
     const uint32_t *__restrict__ hist, const uint32_t *__restrict__ order,
     const uint64_t *__restrict__ offs, const uint64_t *__restrict__ sizes, uint32_t n, int method,
-    uint32_t lat_files, uint32_t md5_bin, uint32_t *__restrict__ nbig_out, uint64_t *__restrict__ big_min,
+    uint32_t lat_files, uint32_t *__restrict__ nbig_out, uint64_t *__restrict__ big_min,
     uint64_t *__restrict__ boffs, uint64_t *__restrict__ bsizes,
     uint64_t *__restrict__ seg_first, uint32_t *__restrict__ bcrc, uint32_t *__restrict__ bpoly,
     uint32_t *__restrict__ err)
@@ -443,7 +435,7 @@ __global__ __launch_bounds__(1024) void big_plan_kernel(
     const int mi = method == 2 ? 1 : 0;
     if (n > lat_files) {
         if (threadIdx.x == 0)
-            b0_s = mi ? (md5_bin ? md5_bin : (uint32_t)kSizeBins) : size_bin(kBigCrcMin);
+            b0_s = mi ? (uint32_t)kSizeBins : size_bin(kBigCrcMin);  // MD5: no offload
     } else {
         // thread t: bins 2t, 2t + 1, both of exponent t >> 4
         const int t = threadIdx.x;
@@ -580,65 +572,6 @@ __global__ __launch_bounds__(1024) void big_plan_kernel(
         seg_first[nbig] = carry;
 }
 
-#ifdef FDFS_PROBES
-// Tail form of the list (probe, BigCrcWs::md5_tail): the files at order
-// positions [p0, n) -- the MD5 chunks taken after the pair kernel's first
-// G -- listed like big_plan_kernel lists the files >= T: compacted offsets
-// and sizes, the exclusive scan of their 64 KiB segment counts, zeroed CRC
-// slots; *nbig_out = n - p0 (one block).
-__global__ __launch_bounds__(1024) void tail_plan_kernel(
-    const uint32_t *__restrict__ order, const uint64_t *__restrict__ offs, const uint64_t *__restrict__ sizes,
-    uint32_t n, uint32_t p0, uint32_t *__restrict__ nbig_out, uint64_t *__restrict__ big_min,
-    uint64_t *__restrict__ boffs, uint64_t *__restrict__ bsizes, uint64_t *__restrict__ seg_first,
-    uint32_t *__restrict__ bcrc, uint32_t *__restrict__ err)
-{
-    __shared__ uint64_t wsum64[16];
-    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-    const uint32_t m = n > p0 ? n - p0 : 0;
-    if (threadIdx.x == 0) {
-        *nbig_out = m;
-        *big_min = ~0ull;  // no size threshold
-    }
-    uint64_t carry = 0;
-    for (uint32_t i0 = 0; i0 < m; i0 += blockDim.x) {
-        const uint32_t i = i0 + threadIdx.x;
-        uint64_t ns = 0;
-        if (i < m) {
-            const uint32_t f = order[p0 + i];
-            const bool ok = f < n;
-            if (!ok)
-                atomicOr(err, 1u);
-            const uint64_t L = ok ? sizes[f] : 0;
-            boffs[i] = ok ? offs[f] : 0;
-            bsizes[i] = L;
-            bcrc[i] = 0;
-            ns = (L + kSegBytes - 1) / kSegBytes;
-        }
-        uint64_t x = ns;
-#pragma unroll
-        for (int o = 1; o < 64; o <<= 1) {
-            const uint64_t y = __shfl_up(x, o);
-            if (lane >= o)
-                x += y;
-        }
-        if (lane == 63)
-            wsum64[wid] = x;
-        __syncthreads();
-        uint64_t before = carry;
-        for (int k = 0; k < wid; k++)
-            before += wsum64[k];
-        if (i < m)
-            seg_first[i] = before + x - ns;
-        uint64_t tot = 0;
-        for (int k = 0; k < (int)(blockDim.x >> 6); k++)
-            tot += wsum64[k];
-        carry += tot;
-        __syncthreads();
-    }
-    if (threadIdx.x == 0)
-        seg_first[m] = carry;
-}
-#endif
 
 // After the lane kernel: the big files' segmented CRC, simple_hash and
 // Time33 into crc_out, their signature fields and codes[0], [2], [3].
@@ -717,18 +650,6 @@ hipError_t launch_zero_u32(void *p, uint64_t ndwords, hipStream_t st)
 {
     if (ndwords == 0)
         return hipSuccess;
-#ifdef FDFS_PROBES
-    // measurement build only: FDFS_GPU_MEMSET=1 restores round 2's
-    // hipMemsetAsync zeroing (scripts/graph_memset_probe.py dumps the
-    // captured graph it makes)
-    static int ms = -1;
-    if (ms < 0) {
-        const char *ev = getenv("FDFS_GPU_MEMSET");
-        ms = (ev && ev[0] == '1') ? 1 : 0;
-    }
-    if (ms)
-        return hipMemsetAsync(p, 0, 4 * ndwords, st);
-#endif
     uint64_t g = (ndwords + 255) / 256;
     zero_u32_kernel<<<(unsigned)(g < 4096 ? g : 4096), 256, 0, st>>>(static_cast<uint32_t *>(p), ndwords);
     return hipGetLastError();
@@ -736,17 +657,22 @@ hipError_t launch_zero_u32(void *p, uint64_t ndwords, hipStream_t st)
 
 // The context's lane-path error count (fdfs_api.cpp lane_err_note): +1 when
 // this launch's error word is set (word == nullptr: a fault injected by
-// fdfs_gpu_inject_error).  One thread; stream-ordered like every call of a
-// context, so the plain add needs no atomic.
-__global__ void lane_err_count_kernel(const uint32_t *__restrict__ word, uint64_t *__restrict__ count)
+// fdfs_gpu_inject_error).  A context may be called on several streams, so
+// two of these can run at once: the add is a device-scope atomic, and the
+// new count goes to the launch's own host slot (fdfs_api.cpp lane_err_note).
+__global__ void lane_err_count_kernel(const uint32_t *__restrict__ word, unsigned long long *__restrict__ count,
+                                      unsigned long long *__restrict__ slot)
 {
-    if (threadIdx.x == 0 && (!word || *word))
-        *count += 1;
+    if (threadIdx.x == 0) {
+        const unsigned long long inc = (!word || *word) ? 1ull : 0ull;
+        *slot = atomicAdd(count, inc) + inc;
+    }
 }
 
-hipError_t launch_lane_err_count(const uint32_t *word, uint64_t *count, hipStream_t st)
+hipError_t launch_lane_err_count(const uint32_t *word, uint64_t *count, uint64_t *slot, hipStream_t st)
 {
-    lane_err_count_kernel<<<1, 64, 0, st>>>(word, count);
+    lane_err_count_kernel<<<1, 64, 0, st>>>(word, reinterpret_cast<unsigned long long *>(count),
+                                            reinterpret_cast<unsigned long long *>(slot));
     return hipGetLastError();
 }
 
@@ -824,93 +750,44 @@ hipError_t launch_sig_lane(bool sar, int method, const uint8_t *base, const uint
         return e;
     uint32_t *cursor = hist + kSizeBins;
     const unsigned hb = (n + 1023) / 1024, sb = (n + 1024 * kBinItems - 1) / (1024 * kBinItems);
-    // bmask: the bins' low mantissa bits cleared (probe FDFS_GPU_BIN_SHIFT:
-    // 2^s sub-octave bins merged, so a wave's 64 files come from a narrower
-    // index range of the batch; the production bins are 1/32 octave)
-    uint32_t bmask = ~0u;
-#ifdef FDFS_PROBES
-    static int bsh = -1;
-    if (bsh < 0) {
-        const char *ev = getenv("FDFS_GPU_BIN_SHIFT");
-        bsh = ev ? atoi(ev) : 0;
-    }
-    bmask = ~((1u << (bsh & 7)) - 1u);
-#endif
+    // bmask: the bins' low mantissa bits cleared (all kept: 1/32-octave
+    // bins; merging 2^s of them measured slower)
+    const uint32_t bmask = ~0u;
     bin_hist_kernel<<<hb < 128 ? hb : 128, 1024, 0, st>>>(sizes, n, hist, bmask);
     bin_scan_kernel<<<1, 1024, 0, st>>>(hist, cursor);
     uint32_t *err = hist + kLaneErrWord;
     bin_scatter_kernel<<<sb, 1024, 0, st>>>(sizes, n, cursor, order, err, bmask);
     const bool offload = big != nullptr;
-    // MD5 one-shot batches above lat_files with md5_inline: the offloaded
-    // CRC segments are md5_pair_kernel's own queue items (no segmented launch)
-    const bool inline_segs = offload && method == 2 && !states && big->md5_inline && n > big->lat_files;
-    PairSegs ps;
-    uint32_t tail_p0 = 0;  // md5_tail: the order position of the first offloaded file
-    if (inline_segs) {
-        ps.nbig = big->nbig;
-        ps.offs = big->offs;
-        ps.sizes = big->sizes;
-        ps.seg_first = big->seg_first;
-        ps.crc = big->crc;
-        if (big->md5_tail) {
-            const uint32_t nw = (n + 63) / 64, G = 4 * big->ncu < nw ? 4 * big->ncu : nw;
-            ps.crc_chunks = G;
-            tail_p0 = 64 * G < n ? 64 * G : n;
-        }
-    }
-    // the segmented passes over the files >= T (CRC; HASH: simple_hash,
-    // Time33 too): before the lane kernel on `st`, or on big->side beside it
-    // (forked after big_plan_kernel; side_late: enqueued after the lane
-    // kernel, so the lane kernel's workgroups are dispatched first)
-    auto seg_passes = [&](hipStream_t ss) -> hipError_t {
-        hipError_t e2 = crc_seg_run(sar, base, big->offs, big->sizes, big->seg_first, n, big->nbig, tabs, big->crc,
-                                    seg_grid, ss);
-        if (e2 == hipSuccess && method == 1)
-            e2 = launch_poly_seg(base, big->offs, big->sizes, big->seg_first, big->nbig, big->poly, seg_grid, ss);
-        if (e2 == hipSuccess && big->side)
-            e2 = hipEventRecord(big->join, big->side);
-        return e2;
-    };
     if (offload) {
-#ifdef FDFS_PROBES
-        if (inline_segs && big->md5_tail)
-            tail_plan_kernel<<<1, 1024, 0, st>>>(order, offs, sizes, n, tail_p0, big->nbig, big->big_min, big->offs,
-                                                 big->sizes, big->seg_first, big->crc, err);
-        else
-#endif
-        big_plan_kernel<<<1, 1024, 0, st>>>(hist, order, offs, sizes, n, method, big->lat_files, big->md5_bin,
-                                            big->nbig, big->big_min, big->offs, big->sizes, big->seg_first,
-                                            big->crc, big->poly, err);
-        if (big->side && !inline_segs) {  // fork: the segmented passes beside the lane kernel
-            if ((e = hipEventRecord(big->fork, st)) != hipSuccess ||
-                (e = hipStreamWaitEvent(big->side, big->fork, 0)) != hipSuccess)
-                return e;
-        }
-        if (!inline_segs && !(big->side && big->side_late) &&
-            (e = seg_passes(big->side ? big->side : st)) != hipSuccess)
+        // the segmented passes over the files >= T (CRC; HASH: simple_hash,
+        // Time33 too), before the lane kernel (beside it on a second stream
+        // measured no faster: the two compete for HBM)
+        big_plan_kernel<<<1, 1024, 0, st>>>(hist, order, offs, sizes, n, method, big->lat_files, big->nbig,
+                                            big->big_min, big->offs, big->sizes, big->seg_first, big->crc, big->poly,
+                                            err);
+        if ((e = crc_seg_run(sar, base, big->offs, big->sizes, big->seg_first, n, big->nbig, tabs, big->crc,
+                             seg_grid, st)) != hipSuccess)
+            return e;
+        if (method == 1 && (e = launch_poly_seg(base, big->offs, big->sizes, big->seg_first, big->nbig, big->poly,
+                                                seg_grid, st)) != hipSuccess)
             return e;
     }
     const uint64_t *bmin = offload ? big->big_min : nullptr;
     if (ev0)
         (void)hipEventRecord(ev0, st);
     e = (method == 2) ? launch_md5_stage(sar, base, offs, sizes, n, order, tabs, bmin, hist + 2 * kSizeBins,
-                                         crc_out, sig_out, codes_out, states, sidx, big ? big->ncu : 0,
-                                         inline_segs ? &ps : nullptr, st)
+                                         crc_out, sig_out, codes_out, states, sidx, big ? big->ncu : 0, st)
                       : launch_sig_hash(sar, base, offs, sizes, n, order, tabs, bmin, crc_out, sig_out,
                                         codes_out, states, sidx, st);
     if (e != hipSuccess)
         return e;
     if (ev1)
         (void)hipEventRecord(ev1, st);
-    if (offload && !inline_segs && big->side && big->side_late && (e = seg_passes(big->side)) != hipSuccess)
-        return e;
-    if (offload && !inline_segs && big->side && (e = hipStreamWaitEvent(st, big->join, 0)) != hipSuccess)
-        return e;
     if (offload && states)
         big_patch_state_kernel<<<256, 256, 0, st>>>(big->nbig, order, n, big->crc, big->poly, sizes, sidx,
                                                     method == 2, states, tabs);
     else if (offload)
-        big_patch_kernel<<<256, 256, 0, st>>>(big->nbig, order + tail_p0, n, big->crc, big->poly, method == 2,
+        big_patch_kernel<<<256, 256, 0, st>>>(big->nbig, order, n, big->crc, big->poly, method == 2,
                                               crc_out, sig_out, codes_out);
     return hipGetLastError();
 }
@@ -919,62 +796,10 @@ static hipError_t crc_seg_run(bool sar, const uint8_t *base, const uint64_t *off
                               const uint64_t *seg_first, uint32_t n, const uint32_t *n_dev,
                               const DevTables *tabs, uint32_t *crc_out, unsigned grid, hipStream_t st)
 {
-    const int tm = crc_table_mode();
-#ifdef FDFS_PROBES
-    static int ql = -1;  // FDFS_GPU_SEG_QUAD=1: quad-cooperative segment loads
-    if (ql < 0) {
-        const char *ev = getenv("FDFS_GPU_SEG_QUAD");
-        ql = ev ? atoi(ev) : 0;
-    }
-    if (ql && tm == 2) {
-        if (sar)
-            crc_seg_kernel<true, 2, true><<<grid, kSegBlock, 0, st>>>(base, offs, sizes, seg_first, n, n_dev, tabs,
-                                                                     crc_out);
-        else
-            crc_seg_kernel<false, 2, true><<<grid, kSegBlock, 0, st>>>(base, offs, sizes, seg_first, n, n_dev, tabs,
-                                                                      crc_out);
-        return hipGetLastError();
-    }
-    static int nt = -1;  // FDFS_GPU_SEG_NT=1: non-temporal block loads
-    if (nt < 0) {
-        const char *ev = getenv("FDFS_GPU_SEG_NT");
-        nt = ev ? atoi(ev) : 0;
-    }
-    static int pf = -1;  // FDFS_GPU_SEG_PF=2: two blocks in flight per wave
-    if (pf < 0) {
-        const char *ev = getenv("FDFS_GPU_SEG_PF");
-        pf = ev ? atoi(ev) : 1;
-    }
-    if (pf == 2 && tm == 2) {
-        if (sar)
-            crc_seg_kernel<true, 2, false, false, 2><<<grid, kSegBlock, 0, st>>>(base, offs, sizes, seg_first, n,
-                                                                                n_dev, tabs, crc_out);
-        else
-            crc_seg_kernel<false, 2, false, false, 2><<<grid, kSegBlock, 0, st>>>(base, offs, sizes, seg_first, n,
-                                                                                 n_dev, tabs, crc_out);
-        return hipGetLastError();
-    }
-    if (nt && tm == 2) {
-        if (sar)
-            crc_seg_kernel<true, 2, false, true><<<grid, kSegBlock, 0, st>>>(base, offs, sizes, seg_first, n, n_dev,
-                                                                            tabs, crc_out);
-        else
-            crc_seg_kernel<false, 2, false, true><<<grid, kSegBlock, 0, st>>>(base, offs, sizes, seg_first, n, n_dev,
-                                                                             tabs, crc_out);
-        return hipGetLastError();
-    }
-#endif
-#define SEG_LAUNCH(S, T) \
-    crc_seg_kernel<S, T><<<grid, kSegBlock, 0, st>>>(base, offs, sizes, seg_first, n, n_dev, tabs, crc_out)
-    if (sar && tm == 2)
-        SEG_LAUNCH(true, 2);
-    else if (sar)
-        SEG_LAUNCH(true, 0);
-    else if (tm == 2)
-        SEG_LAUNCH(false, 2);
+    if (sar)
+        crc_seg_kernel<true><<<grid, kSegBlock, 0, st>>>(base, offs, sizes, seg_first, n, n_dev, tabs, crc_out);
     else
-        SEG_LAUNCH(false, 0);
-#undef SEG_LAUNCH
+        crc_seg_kernel<false><<<grid, kSegBlock, 0, st>>>(base, offs, sizes, seg_first, n, n_dev, tabs, crc_out);
     return hipGetLastError();
 }
 
@@ -1000,29 +825,10 @@ hipError_t launch_crc_seg(bool sar, const uint8_t *base, const uint64_t *offs, c
     return hipGetLastError();
 }
 
-// Table form of the segmented CRC kernel: rotated slice-by-8 (default) or
-// plain slice-by-16 (A/B measurement only).
-int crc_table_mode()
-{
-#ifdef FDFS_PROBES
-    static int v = -1;
-    if (v < 0) {  // A/B (make probes): FDFS_GPU_CRC_TABLES=byte -> slice-by-16 with bank conflicts
-        const char *e = getenv("FDFS_GPU_CRC_TABLES");
-        v = (e && e[0] == 'b') ? 0 : 2;
-    }
-    return v;
-#else
-    return 2;
-#endif
-}
-
 int crc_seg_blocks_per_cu()
 {
     int nb = 0;
-    const int tm = crc_table_mode();
-    hipError_t e = tm == 2 ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, crc_seg_kernel<true, 2>, kSegBlock, 0)
-                           : hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, crc_seg_kernel<true, 0>, kSegBlock, 0);
-    if (e != hipSuccess)
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, crc_seg_kernel<true>, kSegBlock, 0) != hipSuccess)
         return 1;
     return nb > 0 ? nb : 1;
 }

@@ -491,14 +491,6 @@ int fdfs_gpu_scrub(fdfs_gpu_ctx *ctx, const fdfs_gpu_batch *batch, const uint32_
 /* Last HIP error string of this context (for logging), never NULL. */
 const char *fdfs_gpu_last_error(fdfs_gpu_ctx *ctx);
 
-/* Fault injection for tests of the error path: queues on `stream` what a
- * signature launch whose size binning went wrong leaves behind (the lane
- * path's error count raised by one), so that a later call of the context --
- * the first whose entry check sees it, whatever calls were queued in between
- * on any stream -- returns EIO once.  The lane path's errors are counted,
- * not overwritten, so a later launch never hides an earlier one. */
-int fdfs_gpu_inject_error(fdfs_gpu_ctx *ctx, void *stream);
-
 #ifdef __cplusplus
 }
 #endif

@@ -30,15 +30,12 @@ step stats_c5 600 rocprofv3 --kernel-trace --stats -d $O/stats_c5 -o run --outpu
 step stats_c1 900 rocprofv3 --kernel-trace --stats -d $O/stats_c1 -o run --output-format csv -- $B --config c1 --steps 2 --warmup 1 || exit $?
 find $O -name "*kernel_trace.csv" -size +8M -delete  # keep the small traces (steady-state means)
 fi
-if [ "${PART:-all}" != 1 ]; then  # PART=2: PMC passes and probes
+if [ "${PART:-all}" != 1 ]; then  # PART=2: PMC passes
 for c in c2 c3 c4 c5; do
   step fetch_$c 300 rocprofv3 --pmc FETCH_SIZE -d $O/fetch_$c -o run --output-format csv -- $B --config $c --steps 1 --warmup 1 || exit $?
   step write_$c 300 rocprofv3 --pmc WRITE_SIZE -d $O/write_$c -o run --output-format csv -- $B --config $c --steps 1 --warmup 1 || exit $?
 done
 step sq_c3 600 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_MFMA GRBM_GUI_ACTIVE -d $O/sq_c3 -o run --output-format csv -- $B --config c3 --steps 1 --warmup 1 || exit $?
 step sq_c2 300 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_MFMA GRBM_GUI_ACTIVE -d $O/sq_c2 -o run --output-format csv -- $B --steps 1 --warmup 1 || exit $?
-for m in 1 2; do
-  FDFS_GPU_PROBE_LIB=1 FDFS_GPU_HASH_MODE=$m step probe_c2_mode$m 300 $B || exit $?
-done
 fi
 echo done

@@ -13,9 +13,9 @@ import sys
 sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
 from pmc_summary import load  # noqa: E402
 
-BENCH_KERNEL = {"c2": ("sig_hash_kernel<true, 0, 0, false", "sig_hash_kernel<SAR>"),
+BENCH_KERNEL = {"c2": ("sig_hash_kernel<true, false>", "sig_hash_kernel<SAR>"),
                 "c3": ("md5_pair_kernel<true", "md5_pair_kernel<SAR>"),
-                "c4": ("crc_seg_kernel<true, 2", "crc_seg_kernel<SAR,2>")}
+                "c4": ("crc_seg_kernel<true>", "crc_seg_kernel<SAR>")}
 
 
 BENCH_C5_KERNEL = "dedup_group (dp_tile + scan + chunks + dp_split + dp_group)"
@@ -121,16 +121,6 @@ def main(src, dst):
             for k, v in sq.items():
                 if "fdfs::" in k:
                     out.write(f"{short(k)} {json.dumps(v)}\n")
-    if not any(os.path.exists(os.path.join(src, f"probe_c2_mode{m}.log")) for m in (1, 2)):
-        return
-    with open(os.path.join(dst, "probes_c2.txt"), "w") as out:
-        for m in (1, 2):
-            log = os.path.join(src, f"probe_c2_mode{m}.log")
-            if os.path.exists(log):
-                d = json.loads(open(log).read().strip().split("\n")[-1])
-                out.write(f"FDFS_GPU_HASH_MODE={m} ({'loads only' if m == 1 else 'compute only'}): "
-                          f"kernel {d['roofline']['kernel_ms_avg']} ms\n")
-
 
 if __name__ == "__main__":
     main(sys.argv[1], sys.argv[2])

@@ -473,7 +473,7 @@ def test_lane_error_is_sticky(oracle):
     error), the ones after it succeed, and their results are exact."""
     import errno
     import fastdfs_amd as F
-    ctx = F.Context(0)
+    ctx = F.Context(0, test_hooks=True)  # the shipped library has no fault injection
     dev = torch.device("cuda", 0)
     s = torch.cuda.Stream(dev)
     rng = np.random.default_rng(5)
