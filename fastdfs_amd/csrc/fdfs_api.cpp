@@ -928,14 +928,14 @@ int fdfs_gpu_dedup_bucket(fdfs_gpu_ctx *ctx, const uint8_t *sig, const uint64_t 
     if (!g.ok)
         return ENODEV;
     hipStream_t st = reinterpret_cast<hipStream_t>(stream);
-    int rc = ensure_ws(ctx, align_up(8 * 64), st);
+    int rc = ensure_ws(ctx, align_up(8 * fdfs::bucket_ws_elems(n)), st);
     if (rc)
         return rc;
     WsScope wsc(ctx, st);
-    uint64_t *cursor = static_cast<uint64_t *>(ctx->ws);
+    uint64_t *bws = static_cast<uint64_t *>(ctx->ws);
     hipEvent_t a, b;
     timing_pair(ctx, FDFS_KERNEL_BUCKET, a, b);
-    hipError_t e = fdfs::launch_dedup_bucket(sig, gidx, n, nranks, records_out, counts_out, cursor,
+    hipError_t e = fdfs::launch_dedup_bucket(sig, gidx, n, nranks, records_out, counts_out, bws,
                                              row_of_out, st, a, b);
     return e == hipSuccess ? 0 : fail(ctx, e, "dedup_bucket launch");
 }
@@ -1251,7 +1251,7 @@ struct DgPlan {
 
 static size_t dg_a_bytes(uint64_t n)
 {
-    return align_up(32 * n) + align_up(8 * n) + align_up(16 * n) + align_up(8 * 64);
+    return align_up(32 * n) + align_up(8 * n) + align_up(16 * n) + align_up(8 * fdfs::bucket_ws_elems(n));
 }
 
 static size_t dg_b_bytes(uint64_t m)
@@ -1323,7 +1323,7 @@ struct DgSide {
     uint8_t *rows = nullptr;     // [n] 32-byte rows grouped by owner
     uint64_t *row_of = nullptr;  // [n] row of each record
     uint64_t *back = nullptr;    // [n] {rep, ref} answers, in row order
-    uint64_t *cursor = nullptr;  // [64] bucket cursors
+    uint64_t *bws = nullptr;     // the bucket's tile counts and their scan (bucket_ws_elems)
     uint64_t m = 0;              // rows this rank groups as owner
     uint8_t *rows_in = nullptr;  // [m]
     uint64_t *ans = nullptr;     // [m] {rep, ref} for the way back (the group's packed answers)
@@ -1335,7 +1335,7 @@ static void dg_carve_a(DgSide &s, void *mem)
     s.rows = c.take<uint8_t>(32 * s.n);
     s.row_of = c.take<uint64_t>(s.n);
     s.back = c.take<uint64_t>(2 * s.n);
-    s.cursor = c.take<uint64_t>(64);
+    s.bws = c.take<uint64_t>(fdfs::bucket_ws_elems(s.n));
 }
 
 static void dg_carve_b(DgSide &s, void *mem, uint64_t m)
@@ -1369,8 +1369,7 @@ static hipError_t dg_bucket(fdfs_gpu_ctx *ctx, DgSide &s, int nranks, uint64_t *
 {
     hipEvent_t a, b;
     timing_pair(ctx, FDFS_KERNEL_BUCKET, a, b);
-    return fdfs::launch_dedup_bucket(s.sig, s.gidx, s.n, (uint32_t)nranks, s.rows, ann, s.cursor, s.row_of, st, a,
-                                     b);
+    return fdfs::launch_dedup_bucket(s.sig, s.gidx, s.n, (uint32_t)nranks, s.rows, ann, s.bws, s.row_of, st, a, b);
 }
 
 // The announcement's tail {owner-side room, workspace room, errno}, staged

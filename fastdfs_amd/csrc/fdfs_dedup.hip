@@ -1097,65 +1097,85 @@ __device__ __forceinline__ uint32_t owner_of(const uint8_t *row, uint32_t nranks
     return (uint32_t)((sig_hash(a, b, c) >> 32) % nranks);
 }
 
-__global__ void bucket_count_kernel(const uint8_t *__restrict__ sig, uint64_t n, uint32_t nranks,
-                                    uint64_t *__restrict__ counts)
+// Bucketing by owner in tiles of kBkTile records, with no device-scope
+// atomics: bucket_count_kernel writes each tile's count per owner
+// (cnt[owner * tiles + tile]), one exclusive scan of those gives where every
+// (owner, tile) run starts in the owner-grouped rows (owner-major, so each
+// owner's rows are contiguous), and bucket_scatter_kernel places each tile's
+// records at their run's start plus their rank among the tile's records of
+// that owner (an LDS counter).  Round 4's form (every block of 256 records
+// reserving its ranges with one global atomic per owner on shared cursors,
+// and summing its counts the same way) spent 0.81 ms per 12.5M records in
+// those atomics (profiles/r05/dedup_rank_share.txt); this form reads the
+// signatures twice and writes each row once.
+constexpr int kBkThreads = 256, kBkItems = 16, kBkTile = kBkThreads * kBkItems;
+
+uint64_t bucket_tiles(uint64_t n) { return (n + kBkTile - 1) / kBkTile; }
+
+size_t bucket_ws_elems(uint64_t n)  // u64 words: cnt and off (64 owners x tiles + 1 each), the scan's block sums
 {
-    __shared__ uint32_t h[64];
-    for (int k = threadIdx.x; k < 64; k += blockDim.x)
-        h[k] = 0;
-    __syncthreads();
-    for (uint64_t r = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; r < n;
-         r += (uint64_t)gridDim.x * blockDim.x)
-        atomicAdd(&h[owner_of(sig + 24 * r, nranks)], 1u);
-    __syncthreads();
-    for (uint32_t k = threadIdx.x; k < nranks; k += blockDim.x)
-        if (h[k])
-            atomicAdd(reinterpret_cast<unsigned long long *>(&counts[k]), (unsigned long long)h[k]);
+    const uint64_t nt = 64 * bucket_tiles(n) + 1;
+    return 2 * nt + scan_workspace_elems(nt) + 2;
 }
 
-__global__ void bucket_scatter_kernel(const uint8_t *__restrict__ sig, const uint64_t *__restrict__ gidx,
-                                      uint64_t n, uint32_t nranks, const uint64_t *__restrict__ counts,
-                                      uint64_t *__restrict__ cursor, uint8_t *__restrict__ rows,
-                                      uint64_t *__restrict__ row_of)
+__global__ __launch_bounds__(kBkThreads) void bucket_count_kernel(const uint8_t *__restrict__ sig, uint64_t n,
+                                                                  uint32_t nranks, uint64_t tiles,
+                                                                  uint64_t *__restrict__ cnt)
+{
+    __shared__ uint32_t h[kBkThreads / 64][64];  // per wave: fewer lanes on one LDS counter
+    const int w = threadIdx.x >> 6;
+    for (int k = threadIdx.x; k < (kBkThreads / 64) * 64; k += kBkThreads)
+        (&h[0][0])[k] = 0;
+    __syncthreads();
+    const uint64_t t0 = (uint64_t)blockIdx.x * kBkTile;
+#pragma unroll 4
+    for (int it = 0; it < kBkItems; it++) {
+        const uint64_t r = t0 + (uint64_t)it * kBkThreads + threadIdx.x;
+        if (r < n)
+            atomicAdd(&h[w][owner_of(sig + 24 * r, nranks)], 1u);
+    }
+    __syncthreads();
+    for (uint32_t k = threadIdx.x; k < nranks; k += kBkThreads) {
+        uint32_t c = 0;
+#pragma unroll
+        for (int q = 0; q < kBkThreads / 64; q++)
+            c += h[q][k];
+        cnt[(uint64_t)k * tiles + blockIdx.x] = c;
+    }
+}
+
+// off: the scan of cnt (off[nranks * tiles] = n).  Block 0 also writes each
+// owner's row count (counts_out[q], the announcement's first nranks words).
+__global__ __launch_bounds__(kBkThreads) void bucket_scatter_kernel(
+    const uint8_t *__restrict__ sig, const uint64_t *__restrict__ gidx, uint64_t n, uint32_t nranks,
+    uint64_t tiles, const uint64_t *__restrict__ off, uint8_t *__restrict__ rows, uint64_t *__restrict__ row_of,
+    uint64_t *__restrict__ counts_out)
 {
     __shared__ uint32_t cnt[64];
     __shared__ uint64_t bas[64];
-    __shared__ uint64_t start[64];
-    if (threadIdx.x == 0) {
-        uint64_t run = 0;
-        for (uint32_t k = 0; k < nranks; k++) {
-            start[k] = run;
-            run += counts[k];
-        }
+    if (threadIdx.x < nranks) {
+        cnt[threadIdx.x] = 0;
+        bas[threadIdx.x] = off[(uint64_t)threadIdx.x * tiles + blockIdx.x];
+        if (blockIdx.x == 0)
+            counts_out[threadIdx.x] = off[(uint64_t)(threadIdx.x + 1) * tiles] - off[(uint64_t)threadIdx.x * tiles];
     }
-    for (uint64_t r0 = (uint64_t)blockIdx.x * blockDim.x; r0 < n; r0 += (uint64_t)gridDim.x * blockDim.x) {
-        for (int k = threadIdx.x; k < 64; k += blockDim.x)
-            cnt[k] = 0;
-        __syncthreads();
-        const uint64_t r = r0 + threadIdx.x;
-        uint32_t own = 0, rank = 0;
+    __syncthreads();
+    const uint64_t t0 = (uint64_t)blockIdx.x * kBkTile;
+#pragma unroll 4
+    for (int it = 0; it < kBkItems; it++) {
+        const uint64_t r = t0 + (uint64_t)it * kBkThreads + threadIdx.x;
         if (r < n) {
-            own = owner_of(sig + 24 * r, nranks);
-            rank = atomicAdd(&cnt[own], 1u);
-        }
-        __syncthreads();
-        for (uint32_t k = threadIdx.x; k < nranks; k += blockDim.x)
-            if (cnt[k])
-                bas[k] = start[k] + atomicAdd(reinterpret_cast<unsigned long long *>(&cursor[k]),
-                                              (unsigned long long)cnt[k]);
-        __syncthreads();
-        if (r < n) {
-            const uint64_t pos = bas[own] + rank;
-            const uint64_t *s = reinterpret_cast<const uint64_t *>(sig + 24 * r);
-            uint64_t *d = reinterpret_cast<uint64_t *>(rows + 32 * pos);
-            d[0] = s[0];
-            d[1] = s[1];
-            d[2] = s[2];
-            d[3] = gidx ? gidx[r] : r;
+            uint64_t a, b, c;
+            load_sig(sig + 24 * r, a, b, c);
+            const uint32_t own = (uint32_t)((sig_hash(a, b, c) >> 32) % nranks);  // owner_of
+            const uint64_t pos = bas[own] + atomicAdd(&cnt[own], 1u);
+            const uint64_t g = gidx ? gidx[r] : r;
+            uint4 *d = reinterpret_cast<uint4 *>(rows + 32 * pos);  // two 16-byte stores per row
+            d[0] = make_uint4((uint32_t)a, (uint32_t)(a >> 32), (uint32_t)b, (uint32_t)(b >> 32));
+            d[1] = make_uint4((uint32_t)c, (uint32_t)(c >> 32), (uint32_t)g, (uint32_t)(g >> 32));
             if (row_of)
                 row_of[r] = pos;
         }
-        __syncthreads();
     }
 }
 
@@ -1183,21 +1203,21 @@ hipError_t launch_answer_gather(const uint64_t *back, const uint64_t *row_of, ui
 
 hipError_t launch_dedup_bucket(const uint8_t *sig, const uint64_t *gidx, uint64_t n,
                                uint32_t nranks, uint8_t *records_out, uint64_t *counts_out,
-                               uint64_t *cursor, uint64_t *row_of_out, hipStream_t st,
+                               uint64_t *ws, uint64_t *row_of_out, hipStream_t st,
                                hipEvent_t ev0, hipEvent_t ev1)
 {
     hipError_t e;
-    if ((e = launch_zero_u32(counts_out, 2ull * nranks, st)) != hipSuccess)
-        return e;
-    if ((e = launch_zero_u32(cursor, 2ull * nranks, st)) != hipSuccess)
-        return e;
     if (n == 0)
-        return hipSuccess;
+        return launch_zero_u32(counts_out, 2ull * nranks, st);
+    const uint64_t tiles = bucket_tiles(n), nt = (uint64_t)nranks * tiles;
+    uint64_t *cnt = ws, *off = ws + 64 * tiles + 1, *bsum = off + 64 * tiles + 1;
     if (ev0)
         (void)hipEventRecord(ev0, st);
-    bucket_count_kernel<<<grid_for(n, 256), 256, 0, st>>>(sig, n, nranks, counts_out);
-    bucket_scatter_kernel<<<grid_for(n, 256), 256, 0, st>>>(sig, gidx, n, nranks, counts_out, cursor,
-                                                            records_out, row_of_out);
+    bucket_count_kernel<<<(unsigned)tiles, kBkThreads, 0, st>>>(sig, n, nranks, tiles, cnt);
+    if ((e = launch_exclusive_scan(cnt, nt, off, bsum, st)) != hipSuccess)
+        return e;
+    bucket_scatter_kernel<<<(unsigned)tiles, kBkThreads, 0, st>>>(sig, gidx, n, nranks, tiles, off, records_out,
+                                                                  row_of_out, counts_out);
     if (ev1)
         (void)hipEventRecord(ev1, st);
     return hipGetLastError();

@@ -163,8 +163,10 @@ hipError_t launch_dedup_group(const uint8_t *sig, uint32_t sig_stride, const uin
                               uint32_t *ref_out, bool packed, hipStream_t st, hipEvent_t ev0, hipEvent_t ev1);
 hipError_t launch_dedup_bucket(const uint8_t *sig, const uint64_t *gidx, uint64_t n,
                                uint32_t nranks, uint8_t *records_out, uint64_t *counts_out,
-                               uint64_t *cursor, uint64_t *row_of_out, hipStream_t st,
+                               uint64_t *ws, uint64_t *row_of_out, hipStream_t st,
                                hipEvent_t ev0, hipEvent_t ev1);
+// u64 words of launch_dedup_bucket's workspace for n records
+size_t bucket_ws_elems(uint64_t n);
 
 // incremental dedup index (fdfs_index.hip)
 struct IndexTable {

@@ -1,10 +1,12 @@
-"""Config 3 pair timeline (probe build, FDFS_GPU_PROBE_LIB=1 FDFS_GPU_MD5_PAIR=6):
-when each md5_pair_kernel workgroup ends, how many chunks and 128-byte rounds
-it ran, and where it sat (HW_ID / XCC_ID).  Answers whether the batch ends
-with a few workgroups (a tail that idle SIMDs could fill) or all together
-(no tail: the batch is throughput-bound).
+"""Config 3 pair timeline (probe build with csrc/probes/pair_timeline.patch,
+FDFS_GPU_PROBE_LIB=1): when each workgroup of the MD5 kernel that ran the
+batch (md5_pair_kernel's chunk queue, the production form, or with
+FDFS_GPU_MD5_PACK=1 the lane-packed md5_pack_kernel, one chunk per pair)
+ends, how many chunks and 128-byte rounds it ran, and where it sat (HW_ID /
+XCC_ID).  Answers whether the batch ends with a few workgroups (a tail that
+idle SIMDs could fill) or all together.
 
-Usage: FDFS_GPU_PROBE_LIB=1 FDFS_GPU_MD5_PAIR=6 python3 scripts/pair_timeline.py [--files N]
+Usage: FDFS_GPU_PROBE_LIB=1 [FDFS_GPU_MD5_PACK=1] python3 scripts/pair_timeline.py [--files N]
 """
 import argparse
 import ctypes
@@ -28,7 +30,7 @@ def main():
     ap.add_argument("--reps", type=int, default=3)
     ap.add_argument("--out", default="")
     a = ap.parse_args()
-    assert os.environ.get("FDFS_GPU_PROBE_LIB") == "1" and os.environ.get("FDFS_GPU_MD5_PAIR") == "6"
+    assert os.environ.get("FDFS_GPU_PROBE_LIB") == "1"
     dev = torch.device("cuda", 0)
     sizes = C.photo_sizes(a.files, seed=3)
     data, offs, szs = C.device_batch(sizes, seed=2, device=dev, align=16)
@@ -37,7 +39,7 @@ def main():
     L.fdfs_gpu_probe_pairs.restype = ctypes.c_int
     L.fdfs_gpu_probe_pairs.argtypes = [ctypes.c_void_p, ctypes.c_size_t]
     ncu = torch.cuda.get_device_properties(dev).multi_processor_count
-    nwg = min(4 * ncu, (a.files + 63) // 64)
+    nwg = min(4 * ncu, (a.files + 63) // 64)  # the grid of either kernel
     hz = 100e6  # s_memrealtime
     res = []
     for rep in range(a.reps):
@@ -46,11 +48,9 @@ def main():
         ctx.sig_batch(data, offs, szs, method=F.SIG_MD5, check_bounds=False)
         torch.cuda.synchronize()
         kms, _ = ctx.read_timing(_lib.KERNEL_SIG_LANE)
-        buf = np.zeros(8 * nwg, np.uint64)
-        # the per-chunk words are written only when a second chunk starts
+        buf = np.zeros(4 * nwg, np.uint64)
         assert L.fdfs_gpu_probe_pairs(buf.ctypes.data, buf.size) == 0
-        r8 = buf.reshape(nwg, 8)
-        r = r8[:, :4]
+        r = buf.reshape(nwg, 4)
         t0 = r[:, 0].astype(np.float64)
         t1 = r[:, 1].astype(np.float64)
         base = t0.min()
@@ -80,7 +80,7 @@ def main():
              "workgroups": int(nwg), "start_ms_q": q(start_ms), "end_ms_q": q(end_ms),
              "chunks_q": q(chunks), "rounds_q": q(rounds), "rounds_total": int(rounds.sum()),
              "idle_after_end_frac": round(idle_frac, 4),
-             "first_chunk_rank_of_last_10": [int(i) for i in np.argsort(end_ms)[-10:]],
+             "last_10_workgroups": [int(i) for i in np.argsort(end_ms)[-10:]],
              "cus": len(cus), "cu_end_ms_q": q(cu_end), "cu_rounds_q": q(cu_rounds),
              "corr_end_vs_rounds": round(float(np.corrcoef(end_ms, rounds)[0, 1]), 4),
              "simd_hist": np.bincount(simd, minlength=4).tolist(),
@@ -88,11 +88,8 @@ def main():
         res.append(d)
         print(json.dumps(d), flush=True)
         if a.out and rep == a.reps - 1:
-            first_end = np.where(chunks > 1, (r8[:, 5].astype(np.float64) - base) / hz * 1e3, end_ms)
             np.savez_compressed(a.out, start_ms=start_ms, end_ms=end_ms, chunks=chunks, rounds=rounds,
-                                hw=hw, xcc=xcc, first_chunk=r8[:, 4].astype(np.int64),
-                                first_rounds=r8[:, 6].astype(np.int64), first_end_ms=first_end,
-                                second_chunk=np.where(chunks > 1, r8[:, 7].astype(np.int64), -1))
+                                hw=hw, xcc=xcc)
     ctx.close()
 
 

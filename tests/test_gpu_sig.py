@@ -277,6 +277,31 @@ def test_md5_many_chunks(oracle, ctxs):
     _check(oracle, ctxs[0], 0, buf, offs2, sz, methods=(2,))
 
 
+@pytest.mark.parametrize("shape", ["packed", "packed_tiny", "queue"])
+def test_md5_packed_lanes(oracle, ctxs, shape):
+    """More files than the pair kernel has lanes (100K > 1,024 pairs x 64),
+    so pairs take chunk after chunk from the queue: "packed" and
+    "packed_tiny" are the batches round 5's lane-packed plan balanced
+    (U[8, 32] KiB, the config-3 shape scaled down; the second with 3,000
+    files of 0-299 bytes: files of no whole round, odd block counts) -- the
+    plan ran them bit-exact on the GPU and measured slower on config 3, so it
+    lives in the probe build (csrc/probes/md5_pack.patch, DESIGN 4.3) --;
+    "queue" is a bimodal batch (8 and 32 KiB).  Every file's CRC and MD5
+    signature against the oracle, plus two byte-misaligned files."""
+    rng = np.random.default_rng({"packed": 41, "packed_tiny": 42, "queue": 43}[shape])
+    n = 100_000
+    if shape == "queue":
+        sizes = np.where(rng.random(n) < 0.5, 32 << 10, 8 << 10) + rng.integers(0, 64, n)
+    else:
+        sizes = rng.integers(8 << 10, (32 << 10) + 1, n)
+        if shape == "packed_tiny":
+            tiny = rng.choice(n, 3000, replace=False)
+            sizes[tiny] = rng.integers(0, 300, 3000)
+    buf, offs, sz = _packed(sizes, 16, rng, slack=64)
+    offs[[7, 70_000]] += np.array([3, 9])
+    _check(oracle, ctxs[0], 0, buf, offs, sz, methods=(2,))
+
+
 def test_md5_at_scale(oracle, ctxs):
     """Config 3 shape (24K photos of 1-4 MiB, ~63 GB in HBM): a random sample
     of files matches the oracle's CRC and MD5 signature bit for bit, and the
