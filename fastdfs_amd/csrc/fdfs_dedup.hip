@@ -1108,7 +1108,7 @@ __device__ __forceinline__ uint32_t owner_of(const uint8_t *row, uint32_t nranks
 // and summing its counts the same way) spent 0.81 ms per 12.5M records in
 // those atomics (profiles/r05/dedup_rank_share.txt); this form reads the
 // signatures twice and writes each row once.
-constexpr int kBkThreads = 256, kBkItems = 16, kBkTile = kBkThreads * kBkItems;
+constexpr int kBkThreads = 256, kBkItems = 32, kBkTile = kBkThreads * kBkItems;  // 8192: one-block scan up to 16K (owner, tile) counts
 
 uint64_t bucket_tiles(uint64_t n) { return (n + kBkTile - 1) / kBkTile; }
 

@@ -443,8 +443,8 @@ __global__ __launch_bounds__(kHashBlock) __attribute__((amdgpu_waves_per_eu(1)))
 // simple_hash_ex / Time33Hash_ex of the big files (>= T), segment-parallel
 // (INIT_HASH_CODES4 starts both at 0, so a file's hash is the polynomial
 // sum_pos b_pos M^(L-1-pos) mod 2^32 and splits over any cut).  One wave per
-// 64 KiB segment of the big-file list big_plan_kernel made; lane l hashes
-// the segment's l-th KiB (Horner, 16-byte loads when the file is aligned),
+// kSegBytes segment of the big-file list big_plan_kernel made; lane l hashes
+// the segment's l-th 1/64 (Horner, 16-byte loads when the file is aligned),
 // scales it by M^(bytes after it in the file) and the wave's sum is added
 // into the file's slot (mod 2^32 addition commutes).  Multiplicative orders
 // of 31 and 33 mod 2^32 divide 2^30, so exponents are reduced mod 2^30.
@@ -471,8 +471,9 @@ __global__ __launch_bounds__(kPolyBlock) void poly_seg_kernel(
         const uint32_t f = lo;
         const uint64_t L = bsizes[f];
         const uint8_t *fp = base + boffs[f];
-        const uint64_t s0 = (sg - seg_first[f]) * kSegBytes + (uint64_t)lane * 1024;
-        const uint64_t s1 = s0 + 1024 < L ? s0 + 1024 : L;
+        constexpr uint64_t span = kSegBytes / 64;  // bytes per lane
+        const uint64_t s0 = (sg - seg_first[f]) * kSegBytes + (uint64_t)lane * span;
+        const uint64_t s1 = s0 + span < L ? s0 + span : L;
         uint32_t h31 = 0, h33 = 0;
         if (s0 < s1) {
             const uint8_t *q = fp + s0;

@@ -4,12 +4,12 @@
 #include <cstdint>
 
 #include "../../include/fdfs_gpu.h"
+#include "fdfs_tables.hpp"
 
 namespace fdfs {
 
 struct DevTables;
 
-constexpr uint64_t kSegBytes = 64 * 1024;  // CRC segment owned by one wave
 constexpr int kSegBlock = 512;             // threads per crc_seg_kernel workgroup
 constexpr int kSizeBins = 2048;            // size bins of the lane-path counting sort
 constexpr int kLaneWsDwords = 2 * kSizeBins + 64;  // size-bin histogram + cursors + MD5 chunk queue + error word

@@ -131,7 +131,7 @@ __device__ __forceinline__ uint32_t crc_segment(const uint32_t *sD, const uint32
     return state;
 }
 
-static_assert(kSegBytes == 65536, "CrcTables::ADVSEG is built for 64 KiB segments");
+static_assert(kSegBytes % 4096 == 0 && kSegBytes % 64 == 0, "segments are whole 4 KiB blocks and 64 lane spans");
 
 // Advance state v by n zero bytes (v -> M^n v) with the GF(2) matrix powers
 // M^(2^k): lane c (< 32) holds column c, one 5-step XOR reduction per set

@@ -1,7 +1,7 @@
 // libfdfs_gpu: segmented CRC32 kernel, planning kernels and launchers (gfx950).
 //
 //  * crc_seg_kernel<SAR>: CRC32 only (the default upload path and the
-//    CRC of the MD5 method), one WAVE per 64 KiB segment of a file,
+//    CRC of the MD5 method), one WAVE per kSegBytes segment of a file,
 //    coalesced 4 KiB strides, conflict-free rotated slice-by-8 tables in LDS
 //    (the byte-table slice-by-16 form measured slower), a 6-level GF(2) combine across
 //    the wave, and a GF(2) matrix-power advance to combine segments of large
@@ -382,7 +382,7 @@ __global__ __launch_bounds__(kScanBlock) void scan_apply_kernel(const uint64_t *
 // Files of >= T bytes (a power of two, so exactly the size bins from bin(T)
 // up) are the first nbig entries of the size-descending order.  One block
 // picks T, then lists them for crc_seg_kernel / poly_seg_kernel: compacted
-// offsets/sizes, the exclusive scan of their 64 KiB segment counts, zeroed
+// offsets/sizes, the exclusive scan of their segment counts, zeroed
 // CRC and polynomial slots.
 //
 // Choosing T.  A batch of more than lat_files files puts several waves on a

@@ -101,7 +101,7 @@ bool build_crc_tables(CrcTables &t, bool arithmetic_shift)
     byte_tables_of(t, t.ADV4032, 4032);
     for (int l = 0; l < 6; l++)
         byte_tables_of(t, t.ADVRED[l], (uint64_t)64 << l);
-    byte_tables_of(t, t.ADVSEG, 65536);
+    byte_tables_of(t, t.ADVSEG, kSegBytes);
 
     for (int i = 0; i < 32; i++)
         t.MPOW[0][i] = crc_step(t, 1u << i, 0);
@@ -110,7 +110,7 @@ bool build_crc_tables(CrcTables &t, bool arithmetic_shift)
             t.MPOW[k][i] = matvec(t.MPOW[k - 1], matvec(t.MPOW[k - 1], 1u << i));
 
     // Self-check the power matrices against direct stepping.
-    for (uint64_t n : {1ull, 7ull, 64ull, 4032ull, 65536ull + 3})
+    for (uint64_t n : {(uint64_t)1, (uint64_t)7, (uint64_t)64, (uint64_t)4032, (uint64_t)65539, kSegBytes})
         for (uint32_t v : {0x80000000u, 0x12345678u, 0xFFFFFFFFu})
             if (crc_advance(t, v, n) != adv_bytes(t, v, n))
                 return false;

@@ -11,6 +11,10 @@
 
 namespace fdfs {
 
+// CRC segment owned by one wave of crc_seg_kernel (and 64 lanes' spans of
+// poly_seg_kernel); ADVSEG advances by exactly this many bytes.
+constexpr uint64_t kSegBytes = 128 * 1024;
+
 // Zero-input byte step M (advance by one zero byte) is GF(2)-linear in the
 // state for both shift semantics, which is what every table below relies on.
 struct CrcTables {
@@ -20,7 +24,7 @@ struct CrcTables {
     uint32_t K8;              // chain8 sign fix: M^8(c) = sum_j D[8+j][byte_j(c)] ^ (c<0 ? K8 : 0)
     uint32_t ADV4032[4][256]; // advance by 4032 zero bytes (wave stride - lane piece)
     uint32_t ADVRED[6][4][256]; // advance by 64<<t bytes, t = 0..5 (wave reduction tree)
-    uint32_t ADVSEG[4][256];  // advance by one 64 KiB segment (kSegBytes)
+    uint32_t ADVSEG[4][256];  // advance by one segment (kSegBytes)
     uint32_t MPOW[48][32];    // columns of M^(2^k), k = 0..47 (arbitrary advance)
     int sar;                  // 1 = arithmetic shift (signed state)
 };
