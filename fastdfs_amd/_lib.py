@@ -18,6 +18,8 @@ if os.environ.get("FDFS_GPU_PROBE_LIB") == "1":
     LIB_PATH = os.path.join(_HERE, "lib", "probes", "libfdfs_gpu.so")
 elif os.environ.get("FDFS_GPU_PROBE_LIB") == "ab":  # `make ab`: the previous form of a kernel, for A/B runs
     LIB_PATH = os.path.join(_HERE, "lib", "ab", "libfdfs_gpu.so")
+elif os.environ.get("FDFS_GPU_PROBE_LIB", "").startswith("var:"):  # `make variant NAME=<x> EXTRA=...`
+    LIB_PATH = os.path.join(_HERE, "lib", "var", os.environ["FDFS_GPU_PROBE_LIB"][4:], "libfdfs_gpu.so")
 HEADER_PATH = os.path.join(os.path.dirname(_HERE), "include", "fdfs_gpu.h")
 # The test-hooks build (`make test-hooks`, part of `make all`): the same
 # objects with fdfs_api.cpp compiled with FDFS_TEST_HOOKS, which adds

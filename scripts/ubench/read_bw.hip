@@ -6,8 +6,9 @@
 //           buffer, each wave reading U blocks ahead (U x 4 loads of 16 B
 //           per lane in flight);
 //   nt    : the same loads non-temporal;
-//   glds  : global_load_lds_dwordx4 into a per-wave LDS ring of R x 4 KiB
-//           (lane-linear), folded from LDS after a counted vmcnt.
+//   glds  : global_load_lds_dwordx4 into a per-wave LDS ring of R slots of
+//           SLOT bytes (lane-linear), folded from LDS after a counted vmcnt
+//           (inline asm, so R - 1 slots stay in flight).
 // hipcc --offload-arch=gfx950 -O3 read_bw.hip -o read_bw && ./read_bw
 #include <hip/hip_runtime.h>
 #include <cstdio>
@@ -49,45 +50,60 @@ __global__ __launch_bounds__(512) void k_reg(const uint4 *__restrict__ v, uint64
     out[(uint64_t)blockIdx.x * blockDim.x + threadIdx.x] = acc;
 }
 
-// glds: each wave streams its range through an R-slot ring of 4 KiB in LDS
-template <int R, int AUX>
-__global__ __launch_bounds__(256) void k_glds(const uint4 *__restrict__ v, uint64_t nblk, uint32_t *out)
+// glds: each wave streams its range through an R-slot ring of SLOT bytes in LDS
+template <int R, int AUX, int SLOT = 4096>
+__global__ __launch_bounds__(1024) void k_glds(const uint4 *__restrict__ v, uint64_t nblk, uint32_t *out)
 {
     extern __shared__ __attribute__((aligned(16))) uint8_t ring[];
+    constexpr int NI = SLOT / 1024;  // glds instructions per slot
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-    uint8_t *my = ring + (size_t)wv * R * 4096;
+    uint8_t *my = ring + (size_t)wv * R * SLOT;
+    const uint64_t nsl = nblk * (4096 / SLOT);
     const uint64_t w = (uint64_t)blockIdx.x * (blockDim.x >> 6) + wv;
     const uint64_t nw = (uint64_t)gridDim.x * (blockDim.x >> 6);
-    const uint64_t b0 = nblk * w / nw, b1 = nblk * (w + 1) / nw;
+    const uint64_t b0 = nsl * w / nw, b1 = nsl * (w + 1) / nw;
     uint32_t acc = 0;
+    // inline asm: with __builtin_amdgcn_global_load_lds hipcc waits for
+    // every outstanding LDS-DMA load before each LDS read (vmcnt(0)), which
+    // leaves one slot in flight whatever R is
     auto issue = [&](uint64_t b, int slot) {
         const uint64_t bb = b < b1 ? b : b1 - 1;
 #pragma unroll
-        for (int q = 0; q < 4; q++)
-            __builtin_amdgcn_global_load_lds(reinterpret_cast<const void *>(v + bb * 256 + q * 64 + lane),
-                                             (__attribute__((address_space(3))) void *)(my + slot * 4096 + q * 1024),
-                                             16, 0, AUX);
+        for (int q = 0; q < NI; q++) {
+            const uint4 *p = v + bb * (SLOT / 16) + q * 64 + lane;
+            const uint32_t dst = (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) void *)(my + slot * SLOT + q * 1024);
+            if (AUX)
+                asm volatile("s_nop 0\n\tglobal_load_lds_dwordx4 %0, off nt" : : "v"(p), "{m0}"(dst) : "memory");
+            else
+                asm volatile("s_nop 0\n\tglobal_load_lds_dwordx4 %0, off" : : "v"(p), "{m0}"(dst) : "memory");
+        }
     };
 #pragma unroll
     for (int s = 0; s < R - 1; s++)
         issue(b0 + s, s);
     int slot = 0;
     for (uint64_t b = b0; b < b1; b++) {
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the slot's last reads are done
         issue(b + R - 1, (slot + R - 1) % R);
-        // the oldest of R blocks in flight has landed once at most (R - 1) * 4 remain
-        if constexpr (R == 2)
+        // the oldest of R slots in flight has landed once (R - 1) * NI remain
+        if constexpr ((R - 1) * NI == 4)
             asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-        else if constexpr (R == 3)
+        else if constexpr ((R - 1) * NI == 8)
             asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
-        else
+        else if constexpr ((R - 1) * NI == 12)
             asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
-        const uint4 *s = reinterpret_cast<const uint4 *>(my + slot * 4096);
+        else if constexpr ((R - 1) * NI == 2)
+            asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+        else if constexpr ((R - 1) * NI == 6)
+            asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+        else
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        const uint4 *s = reinterpret_cast<const uint4 *>(my + slot * SLOT);
 #pragma unroll
-        for (int q = 0; q < 4; q++) {
+        for (int q = 0; q < NI; q++) {
             const uint4 x = s[q * 64 + lane];
             acc ^= x.x ^ x.y ^ x.z ^ x.w;
         }
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         slot = (slot + 1) % R;
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -138,15 +154,24 @@ int main()
             snprintf(nm, sizeof nm, "reg U2 nt T%d blk/CU %d", T, grid / ncu);
             rep(nm, timeit([&] { k_reg<2, true><<<grid, T>>>(v, nblk, out); }));
         }
-    for (int wpc : {4, 8, 16}) {  // waves per CU (256-thread blocks)
-        const int grid = ncu * wpc / 4;
-        snprintf(nm, sizeof nm, "glds R3 default %d waves/CU", wpc);
-        rep(nm, timeit([&] { k_glds<3, 0><<<grid, 256, 4 * 3 * 4096>>>(v, nblk, out); }));
-        snprintf(nm, sizeof nm, "glds R3 nt %d waves/CU", wpc);
-        rep(nm, timeit([&] { k_glds<3, 2><<<grid, 256, 4 * 3 * 4096>>>(v, nblk, out); }));
-        snprintf(nm, sizeof nm, "glds R4 nt %d waves/CU", wpc);
-        rep(nm, timeit([&] { k_glds<4, 2><<<grid, 256, 4 * 4 * 4096>>>(v, nblk, out); }));
-    }
+    // G workgroups per CU sharing W waves (each its ring in dynamic LDS), slots of S
+    auto glds = [&](const char *tag, int waves, int G, int R, int S, int aux, auto kern) {
+        const size_t lds = (size_t)(waves / G) * R * S;
+        snprintf(nm, sizeof nm, "glds %s %2d waves/CU in %d WG R%d x %d B (%zu KB/WG)", tag, waves, G, R, S, lds >> 10);
+        rep(nm, timeit([&] { kern<<<ncu * G, 64 * (waves / G), lds>>>(v, nblk, out); }));
+    };
+    glds("nt", 8, 1, 2, 4096, 2, k_glds<2, 2, 4096>);
+    glds("nt", 8, 1, 3, 4096, 2, k_glds<3, 2, 4096>);
+    glds("nt", 8, 1, 4, 4096, 2, k_glds<4, 2, 4096>);
+    glds("nt", 8, 2, 2, 4096, 2, k_glds<2, 2, 4096>);
+    glds("nt", 8, 2, 3, 4096, 2, k_glds<3, 2, 4096>);
+    glds("nt", 8, 2, 4, 4096, 2, k_glds<4, 2, 4096>);
+    glds("nt", 12, 1, 2, 4096, 2, k_glds<2, 2, 4096>);
+    glds("nt", 12, 1, 3, 4096, 2, k_glds<3, 2, 4096>);
+    glds("nt", 16, 2, 2, 4096, 2, k_glds<2, 2, 4096>);
+    glds("nt", 16, 4, 2, 4096, 2, k_glds<2, 2, 4096>);
+    glds("nt", 4, 1, 4, 4096, 2, k_glds<4, 2, 4096>);
+    glds("def", 8, 1, 3, 4096, 0, k_glds<3, 0, 4096>);
     CK(hipDeviceSynchronize());
     printf("done\n");
     return 0;
