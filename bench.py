@@ -383,7 +383,7 @@ def c4_sizes(n):
 
 
 def c4_workload(n):
-    return f"config 4: {n} x 1 GiB files/GPU, segmented CRC32 (64 KiB) + GF(2) combine"
+    return f"config 4: {n} x 1 GiB files/GPU, segmented CRC32 (128 KiB segments) + GF(2) combine"
 
 
 def batch_line(args, ctx, world, rank, dev, config, sizes, method, workload, steps, warmup, threads,

@@ -8,6 +8,7 @@ import csv
 import glob
 import json
 import os
+import subprocess
 import sys
 
 sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
@@ -45,7 +46,7 @@ def steady(trace, out_path):
 
 def main(src, dst):
     os.makedirs(dst, exist_ok=True)
-    for c in ("c1", "c2", "c3", "c4", "c5"):
+    for c in ("c1", "c2", "c3", "c4", "c5", "c4_hash", "c4_md5"):
         log = os.path.join(src, f"bench_{c}.log")
         if os.path.exists(log):
             line = open(log).read().strip().split("\n")[-1]
@@ -113,9 +114,16 @@ def main(src, dst):
                                  "HBM section), write = WRITE_SIZE x 1024",
                        "files": [f"{rel}/pmc_fetch_{c}.txt", f"{rel}/pmc_write_{c}.txt"]},
                       open(os.path.join(os.path.dirname(dst), f"pmc_{c}.json"), "w"), indent=1)
-    for c in ("c2", "c3"):
+    for c in ("c2", "c3", "c4"):
         if not os.path.isdir(os.path.join(src, f"sq_{c}")):
             continue
+        # clock and SIMD issue occupancy of the dominant kernel, per dispatch
+        pat = {"c2": "sig_hash_kernel", "c3": "md5_pair_kernel", "c4": "crc_seg_kernel"}[c]
+        with open(os.path.join(dst, f"issue_clock_{c}.txt"), "w") as out:
+            out.write(f"# python3 scripts/pmc_clock.py {pat} sq_{c} (one pass)\n")
+            out.write(subprocess.run([sys.executable, os.path.join(os.path.dirname(os.path.abspath(__file__)),
+                                                                   "pmc_clock.py"), pat, os.path.join(src, f"sq_{c}")],
+                                     capture_output=True, text=True, check=True).stdout.replace(src + "/", ""))
         sq = load(os.path.join(src, f"sq_{c}"), "max" if c == "c3" else "mean")  # c3: skip the chain-floor dispatches
         with open(os.path.join(dst, f"pmc_sq_{c}.txt"), "w") as out:
             for k, v in sq.items():

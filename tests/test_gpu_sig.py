@@ -140,7 +140,7 @@ def test_crc_plan_small_boundary(oracle, ctxs, n):
 
 @pytest.mark.parametrize("variant", [0, 1])
 def test_large_file_segmented(oracle, ctxs, variant):
-    """Config 4 shape: large files split into 64 KiB segments + GF(2) combine."""
+    """Config 4 shape: large files split into 128 KiB segments + GF(2) combine."""
     rng = np.random.default_rng(21)
     sizes = np.array([(256 << 20) + 12345, 64 << 20, (3 << 16) + 1, 7 << 20], np.int64)
     buf, offs, sz = _packed(sizes, 1, rng)
