@@ -23,6 +23,8 @@ namespace fdfs {
 // ------------------------------------------------------- segmented CRC path
 // (device helpers in fdfs_segcrc.hpp)
 
+constexpr uint32_t kSegRingBytes = (kSegBlock / 64) * kFoldRingBytes;  // dynamic LDS: the waves' fold rings
+
 template <bool SAR>
 __global__ __launch_bounds__(kSegBlock) void crc_seg_kernel(
     const uint8_t *__restrict__ base, const uint64_t *__restrict__ offs,
@@ -36,28 +38,32 @@ __global__ __launch_bounds__(kSegBlock) void crc_seg_kernel(
         if ((total * w0) / nw == (total * (w0 + (blockDim.x >> 6))) / nw)
             return;
     }
-    // the 64 KiB conflict-free tables in LDS; the reduction tables stay in
-    // global memory (24 lookups per segment)
-    constexpr int kD = kRep8Dwords;
-    __shared__ uint32_t smem[kD + 256 + 2 * 4 * 256];
-    uint32_t *sD = smem, *sT = smem + kD, *sA = sT + 256, *sS = sA + 1024;
+    // the plain slice-by-16 tables (the signed variant's data is complemented
+    // before the fold; only the runs' last vectors use them), the 4032-byte
+    // advance and the byte table in LDS; the reduction tables stay in global
+    // memory (24 lookups per run)
+    __shared__ uint32_t smem[16 * 256 + 4 * 256 + 256];
+    uint32_t *sD = smem, *sA = smem + 16 * 256, *sT = sA + 4 * 256;
     const uint32_t *sR = &tabs->t.ADVRED[0][0][0];
-    lds_fill(sS, &tabs->t.ADVSEG[0][0], 4 * 256);
-    lds_fill_rep8(sD, SAR ? &tabs->Dc[0][0] : &tabs->t.D[0][0]);
-    lds_fill(sT, tabs->t.T, 256);
+    lds_fill(sD, &tabs->t.D[0][0], 16 * 256);
     lds_fill(sA, &tabs->t.ADV4032[0][0], 4 * 256);
+    lds_fill(sT, tabs->t.T, 256);
     __syncthreads();
 
-    const uint32_t K8 = tabs->t.K8;
-    const Rep8Lane R8 = rep8_lane(threadIdx.x & 63);
+    const uint32_t K16 = tabs->t.K16;
     const int lane = threadIdx.x & 63;
     const uint64_t wpb = blockDim.x >> 6;
-    const uint64_t w = (uint64_t)blockIdx.x * wpb + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const uint32_t wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const uint64_t w = (uint64_t)blockIdx.x * wpb + wv;
     const uint64_t nw = (uint64_t)gridDim.x * wpb;
     uint64_t s = (total * w) / nw;
     const uint64_t s_end = (total * (w + 1)) / nw;
     if (s >= s_end)
         return;
+    // this wave's fold ring (kFoldRingBytes of the dynamic LDS)
+    extern __shared__ __attribute__((aligned(16))) uint4 fold_ring[];
+    uint4 *ring = fold_ring + (size_t)wv * kFoldSlots;
+    const uint32_t ring_lds = lds_addr(ring);
     uint32_t lo = 0, hi = n;  // last f with seg_first[f] <= s
     while (hi - lo > 1) {
         const uint32_t mid = (lo + hi) >> 1;
@@ -67,53 +73,30 @@ __global__ __launch_bounds__(kSegBlock) void crc_seg_kernel(
             hi = mid;
     }
     uint32_t f = lo;
-    // The wave's segments are consecutive, so a run of segments of one file
-    // is chained in place (state = ADV_seg(state) ^ crc0(seg), one 4-lookup
-    // advance per segment); only when the run ends is the state advanced to
-    // the file end (GF(2) matrix powers) and merged into crc_out.
-    uint32_t run_f = 0xFFFFFFFFu, run_state = 0;
-    uint64_t run_end = 0;
-    bool run_has_first = false, run_whole = false;
-    for (;; s++) {
-        const bool more = s < s_end;
-        if (more) {
-            while (seg_first[f + 1] <= s)
-                f++;
-        }
-        if (run_f != 0xFFFFFFFFu && (!more || f != run_f)) {  // flush the finished run
-            const uint64_t L = sizes[run_f];
-            const uint32_t cl = run_has_first ? crc_final_const<SAR>(L) : 0u;
-            if (run_whole) {
-                if (lane == 0)
-                    crc_out[run_f] = run_state ^ cl;
-            } else {
-                const uint32_t v = advance_any(tabs, run_state, L - run_end, lane);
-                if (lane == 0)
-                    atomicXor(&crc_out[run_f], v ^ cl);
-            }
-            run_f = 0xFFFFFFFFu;
-        }
-        if (!more)
-            break;
-        const uint64_t k = s - seg_first[f];
-        const uint64_t nseg = seg_first[f + 1] - seg_first[f];
+    // The wave's segments are consecutive: each run of segments of one file
+    // is one contiguous byte range, folded as one stream (crc_run); a run
+    // that is the whole file stores its CRC, any other is advanced to the
+    // file end (GF(2) matrix powers) and merged into crc_out by XOR.
+    while (s < s_end) {
+        while (seg_first[f + 1] <= s)
+            f++;
+        const uint64_t k0 = s - seg_first[f];
+        const uint64_t s_stop = seg_first[f + 1] < s_end ? seg_first[f + 1] : s_end;
         const uint64_t L = sizes[f];
-        const uint8_t *fp = base + offs[f];
-        const uint64_t lo_b = k * kSegBytes;
-        const uint64_t hi_b = (L < lo_b + kSegBytes) ? L : lo_b + kSegBytes;
-        const uint32_t v = crc_segment<SAR>(sD, sT, sA, sR, R8, K8, fp + lo_b, hi_b - lo_b, k == 0, lane);
-        if (run_f == f) {
-            const uint64_t len = hi_b - lo_b;
-            const uint32_t adv = (len == kSegBytes) ? apply4(sS, run_state)
-                                                    : advance_any(tabs, run_state, len, lane);
-            run_state = adv ^ v;
+        const uint64_t lo_b = k0 * kSegBytes;
+        const uint64_t hi_b = (L < (s_stop - seg_first[f]) * kSegBytes) ? L : (s_stop - seg_first[f]) * kSegBytes;
+        const uint32_t v = crc_run<SAR>(sD, sA, sT, sR, K16, base + offs[f] + lo_b, hi_b - lo_b, k0 == 0, ring,
+                                        ring_lds, lane);
+        const uint32_t cl = k0 == 0 ? crc_final_const<SAR>(L) : 0u;
+        if (k0 == 0 && hi_b == L) {
+            if (lane == 0)
+                crc_out[f] = v ^ cl;
         } else {
-            run_f = f;
-            run_state = v;
-            run_has_first = (k == 0);
+            const uint32_t u = advance_any(tabs, v, L - hi_b, lane);
+            if (lane == 0)
+                atomicXor(&crc_out[f], u ^ cl);
         }
-        run_end = hi_b;
-        run_whole = run_has_first && (k + 1 == nseg);
+        s = s_stop;
     }
 }
 
@@ -768,8 +751,10 @@ hipError_t launch_sig_lane(bool sar, int method, const uint8_t *base, const uint
         if ((e = crc_seg_run(sar, base, big->offs, big->sizes, big->seg_first, n, big->nbig, tabs, big->crc,
                              seg_grid, st)) != hipSuccess)
             return e;
+        // poly_seg_kernel: 2 workgroups of 4 waves per CU (its own grid; the
+        // CRC kernel's is one 8-wave workgroup per CU)
         if (method == 1 && (e = launch_poly_seg(base, big->offs, big->sizes, big->seg_first, big->nbig, big->poly,
-                                                seg_grid, st)) != hipSuccess)
+                                                2 * big->ncu, st)) != hipSuccess)
             return e;
     }
     const uint64_t *bmin = offload ? big->big_min : nullptr;
@@ -797,9 +782,9 @@ static hipError_t crc_seg_run(bool sar, const uint8_t *base, const uint64_t *off
                               const DevTables *tabs, uint32_t *crc_out, unsigned grid, hipStream_t st)
 {
     if (sar)
-        crc_seg_kernel<true><<<grid, kSegBlock, 0, st>>>(base, offs, sizes, seg_first, n, n_dev, tabs, crc_out);
+        crc_seg_kernel<true><<<grid, kSegBlock, kSegRingBytes, st>>>(base, offs, sizes, seg_first, n, n_dev, tabs, crc_out);
     else
-        crc_seg_kernel<false><<<grid, kSegBlock, 0, st>>>(base, offs, sizes, seg_first, n, n_dev, tabs, crc_out);
+        crc_seg_kernel<false><<<grid, kSegBlock, kSegRingBytes, st>>>(base, offs, sizes, seg_first, n, n_dev, tabs, crc_out);
     return hipGetLastError();
 }
 
@@ -828,7 +813,7 @@ hipError_t launch_crc_seg(bool sar, const uint8_t *base, const uint64_t *offs, c
 int crc_seg_blocks_per_cu()
 {
     int nb = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, crc_seg_kernel<true>, kSegBlock, 0) != hipSuccess)
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, crc_seg_kernel<true>, kSegBlock, kSegRingBytes) != hipSuccess)
         return 1;
     return nb > 0 ? nb : 1;
 }

@@ -101,7 +101,6 @@ bool build_crc_tables(CrcTables &t, bool arithmetic_shift)
     byte_tables_of(t, t.ADV4032, 4032);
     for (int l = 0; l < 6; l++)
         byte_tables_of(t, t.ADVRED[l], (uint64_t)64 << l);
-    byte_tables_of(t, t.ADVSEG, kSegBytes);
 
     for (int i = 0; i < 32; i++)
         t.MPOW[0][i] = crc_step(t, 1u << i, 0);
@@ -109,6 +108,14 @@ bool build_crc_tables(CrcTables &t, bool arithmetic_shift)
         for (int i = 0; i < 32; i++)
             t.MPOW[k][i] = matvec(t.MPOW[k - 1], matvec(t.MPOW[k - 1], 1u << i));
 
+    // The sparse fold's relation S(A) = 0 on every basis vector.
+    for (int i = 0; i < 32; i++) {
+        uint32_t v = 0;
+        for (int k = 0; k < kFoldTerms; k++)
+            v ^= crc_advance(t, 1u << i, 16ull * (uint64_t)fold_exp(t.sar != 0, k));
+        if (v != 0)
+            return false;
+    }
     // Self-check the power matrices against direct stepping.
     for (uint64_t n : {(uint64_t)1, (uint64_t)7, (uint64_t)64, (uint64_t)4032, (uint64_t)65539, kSegBytes})
         for (uint32_t v : {0x80000000u, 0x12345678u, 0xFFFFFFFFu})

@@ -8,12 +8,33 @@
 // advance and GF(2) power tables; no kernel code changes.
 #pragma once
 #include <cstdint>
+#ifndef __host__
+#define __host__
+#define __device__
+#endif
 
 namespace fdfs {
 
-// CRC segment owned by one wave of crc_seg_kernel (and 64 lanes' spans of
-// poly_seg_kernel); ADVSEG advances by exactly this many bytes.
+// The unit crc_seg_kernel's waves divide the files into (a wave folds its
+// consecutive segments of one file as one run), and poly_seg_kernel's per
+// wave (64 lanes' spans).
 constexpr uint64_t kSegBytes = 128 * 1024;
+
+// The sparse fold of crc_seg_kernel: S(y) = sum_k y^e_k,
+// k = 0..4, with S(A) = 0 for A = the advance by 16 zero bytes of each shift
+// variant (a 5-term multiple of A's minimal polynomial, found by a
+// meet-in-the-middle search over the powers of A, scripts/fold_search.py;
+// build_crc_tables re-verifies it on the 32 basis vectors).  Because
+// A^e_4 = sum_{k<4} A^e_k, the CRC contribution of a 16-byte vector at
+// distance >= e_4 vectors from the end moves to the four vectors
+// e_4 - e_k further on, by XOR alone.  The gaps e_4 - e_3 (203 / 145) are
+// >= 64: a wave folds 64 consecutive vectors at once.
+constexpr int kFoldTerms = 5;
+__host__ __device__ constexpr int fold_exp(bool sar, int k)
+{
+    return sar ? (k == 0 ? 0 : k == 1 ? 332 : k == 2 ? 344 : k == 3 ? 372 : 575)
+               : (k == 0 ? 0 : k == 1 ? 89 : k == 2 ? 117 : k == 3 ? 155 : 300);
+}
 
 // Zero-input byte step M (advance by one zero byte) is GF(2)-linear in the
 // state for both shift semantics, which is what every table below relies on.
@@ -22,9 +43,8 @@ struct CrcTables {
     uint32_t D[16][256];      // slice-by-16: byte x at chunk position p -> state at chunk end
     uint32_t K16;             // chain16 sign fix: M^16(c) = sum_j D[j][byte_j(c)] ^ (c<0 ? K16 : 0)
     uint32_t K8;              // chain8 sign fix: M^8(c) = sum_j D[8+j][byte_j(c)] ^ (c<0 ? K8 : 0)
-    uint32_t ADV4032[4][256]; // advance by 4032 zero bytes (wave stride - lane piece)
+    uint32_t ADV4032[4][256]; // advance by 4032 zero bytes (a 4 KiB block - a lane's 64-byte piece)
     uint32_t ADVRED[6][4][256]; // advance by 64<<t bytes, t = 0..5 (wave reduction tree)
-    uint32_t ADVSEG[4][256];  // advance by one segment (kSegBytes)
     uint32_t MPOW[48][32];    // columns of M^(2^k), k = 0..47 (arbitrary advance)
     int sar;                  // 1 = arithmetic shift (signed state)
 };
