@@ -105,8 +105,8 @@ size_t sig_ws_bytes(uint64_t n)
                   align_up(sizeof(uint32_t)) + 2 * align_up(sizeof(uint64_t) * n) +
                   align_up(sizeof(uint64_t) * (n + 1)) + align_up(sizeof(uint32_t) * n) +
                   align_up(2 * sizeof(uint32_t) * n) + align_up(sizeof(uint64_t));  // + BigCrcWs
-    size_t seg = align_up(sizeof(uint64_t) * n) + align_up(sizeof(uint64_t) * (n + 1)) +
-                 align_up(sizeof(uint64_t) * fdfs::scan_workspace_elems(n));
+    size_t seg = align_up(sizeof(uint64_t) * 2 * n) + align_up(sizeof(uint64_t) * 2 * (n + 1)) +
+                 align_up(sizeof(uint64_t) * 2 * fdfs::scan_workspace_elems(n));  // launch_crc_seg's two lists
     return lane > seg ? lane : seg;  // one path per call
 }
 
@@ -371,7 +371,7 @@ int fdfs_gpu_open(int device, unsigned flags, fdfs_gpu_ctx **out)
     int ncu = 256;
     if (hipGetDeviceProperties(&prop, device) == hipSuccess && prop.multiProcessorCount > 0)
         ncu = prop.multiProcessorCount;
-    ctx->seg_grid = (unsigned)(ncu * fdfs::crc_seg_blocks_per_cu());
+    ctx->seg_grid = (unsigned)ncu;  // the CRC launchers size their grids per kernel
     ctx->lat_files = (uint32_t)ncu * 4 * 64;
     ctx->ncu = (uint32_t)ncu;
     *out = ctx;
@@ -500,9 +500,9 @@ int fdfs_gpu_sig_batch(fdfs_gpu_ctx *ctx, const fdfs_gpu_batch *batch, int metho
     const uint8_t *base = static_cast<const uint8_t *>(batch->base);
     hipError_t e;
     if (method == FDFS_SIG_CRC_ONLY) {
-        uint64_t *nseg = cv.take<uint64_t>(n);
-        uint64_t *first = cv.take<uint64_t>((size_t)n + 1);
-        uint64_t *bsum = cv.take<uint64_t>(fdfs::scan_workspace_elems(n));
+        uint64_t *nseg = cv.take<uint64_t>(2 * (size_t)n);
+        uint64_t *first = cv.take<uint64_t>(2 * ((size_t)n + 1));
+        uint64_t *bsum = cv.take<uint64_t>(2 * fdfs::scan_workspace_elems(n));
         hipEvent_t a, b;
         timing_pair(ctx, FDFS_KERNEL_CRC_SEG, a, b);
         e = fdfs::launch_crc_seg(ctx->sar, base, batch->offset, batch->size, n, nseg, first, bsum,
@@ -594,9 +594,9 @@ static int update_batch(fdfs_gpu_ctx *ctx, const fdfs_gpu_batch *chunks, const u
     if (method == FDFS_SIG_CRC_ONLY) {
         // per-chunk CRC by the segmented kernel, then carried onto the state
         uint32_t *tmp = cv.take<uint32_t>(n);
-        uint64_t *nseg = cv.take<uint64_t>(n);
-        uint64_t *first = cv.take<uint64_t>((size_t)n + 1);
-        uint64_t *bsum = cv.take<uint64_t>(fdfs::scan_workspace_elems(n));
+        uint64_t *nseg = cv.take<uint64_t>(2 * (size_t)n);
+        uint64_t *first = cv.take<uint64_t>(2 * ((size_t)n + 1));
+        uint64_t *bsum = cv.take<uint64_t>(2 * fdfs::scan_workspace_elems(n));
         hipEvent_t a, b;
         timing_pair(ctx, FDFS_KERNEL_CRC_SEG, a, b);
         e = fdfs::launch_crc_seg(ctx->sar, base, chunks->offset, chunks->size, n, nseg, first, bsum,
@@ -1684,9 +1684,9 @@ static hipError_t cg_pieces(fdfs_gpu_ctx *ctx, const fdfs_gpu_batch *pieces, con
         return e;
     Carve cv{static_cast<char *>(ctx->ws)};
     uint32_t *crc = cv.take<uint32_t>(np);
-    uint64_t *nseg = cv.take<uint64_t>(np);
-    uint64_t *first = cv.take<uint64_t>((size_t)np + 1);
-    uint64_t *bsum = cv.take<uint64_t>(fdfs::scan_workspace_elems(np));
+    uint64_t *nseg = cv.take<uint64_t>(2 * (size_t)np);
+    uint64_t *first = cv.take<uint64_t>(2 * ((size_t)np + 1));
+    uint64_t *bsum = cv.take<uint64_t>(2 * fdfs::scan_workspace_elems(np));
     hipEvent_t a, b;
     timing_pair(ctx, FDFS_KERNEL_CRC_SEG, a, b);
     e = fdfs::launch_crc_seg(ctx->sar, static_cast<const uint8_t *>(pieces->base), pieces->offset, pieces->size, np,

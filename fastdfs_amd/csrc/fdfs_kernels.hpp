@@ -10,7 +10,7 @@ namespace fdfs {
 
 struct DevTables;
 
-constexpr int kSegBlock = 512;             // threads per crc_seg_kernel workgroup
+constexpr int kSegBlock = 512;             // threads per crc_seg_kernel / crc_tab_kernel workgroup
 constexpr int kSizeBins = 2048;            // size bins of the lane-path counting sort
 constexpr int kLaneWsDwords = 2 * kSizeBins + 64;  // size-bin histogram + cursors + MD5 chunk queue + error word
 // Lane-path error word (zeroed with the histogram at every launch): bit 0 =
@@ -60,9 +60,14 @@ hipError_t launch_sig_lane(bool sar, int method, const uint8_t *base, const uint
                            uint8_t *sig_out, int32_t *codes_out, fdfs_gpu_file_state *states,
                            const uint32_t *sidx, unsigned seg_grid, hipStream_t st,
                            hipEvent_t ev0, hipEvent_t ev1);
+// The CRC of n files, CRC only: the files below kFoldMinBytes through
+// crc_tab_kernel, the others through crc_seg_kernel (the sparse fold), each
+// over its own segment list.  Workspace: nseg[2 n], seg_first[2 (n + 1)],
+// bsum[2 scan_workspace_elems(n)] (crc_plan_elems).
+constexpr uint64_t kFoldMinBytes = 256 * 1024;
 hipError_t launch_crc_seg(bool sar, const uint8_t *base, const uint64_t *offs, const uint64_t *sizes,
                           uint32_t n, uint64_t *nseg, uint64_t *seg_first, uint64_t *bsum,
-                          const DevTables *tabs, uint32_t *crc_out, unsigned grid, hipStream_t st,
+                          const DevTables *tabs, uint32_t *crc_out, unsigned ncu, hipStream_t st,
                           hipEvent_t ev0, hipEvent_t ev1);
 hipError_t launch_md5_stage(bool sar, const uint8_t *base, const uint64_t *offs,
                             const uint64_t *sizes, uint32_t n, const uint32_t *order,
@@ -128,7 +133,8 @@ hipError_t launch_crc_fold(const CrcParts &blk, uint32_t nranks, const uint64_t 
 // reserved value ~0 (table: sidx_table_size(n) u32 of scratch).
 uint32_t sidx_table_size(uint32_t n);
 hipError_t launch_sidx_check(const uint32_t *sidx, uint32_t n, uint32_t *table, uint32_t *flag, hipStream_t st);
-int crc_seg_blocks_per_cu();
+int crc_seg_blocks_per_cu();  // the fold kernel (crc_seg_kernel)
+int crc_tab_blocks_per_cu();  // the table kernel (crc_tab_kernel)
 
 // formats, FastDHT routing, scrub (fdfs_format.hip)
 hipError_t launch_file_ids(bool sar, uint32_t server_id, const uint32_t *crc32, const int64_t *size,

@@ -38,6 +38,103 @@ __device__ __forceinline__ uint4 seg_fix_vector(uint4 w, int64_t off, int64_t a0
     return make_uint4(d[0], d[1], d[2], d[3]);
 }
 
+
+// ---- the table fold (crc_tab_kernel: files below kFoldMinBytes) ---------
+// Zero-init CRC state of the (masked) bytes [Ap, Ap+len) of one segment,
+// computed by the whole wave.  Vectors are 16-byte aligned in memory and the
+// 4 KiB block grid is aligned to the segment's last full vector, so the only
+// partial vector is the first (leading neutral bytes do not change a
+// zero-init state).  See DESIGN.md "K2 segmented CRC" for the algebra.
+// The tables are the rotated, replicated slice-by-8 form (64 KiB,
+// conflict-free; fdfs_device.hpp chain16r) of Dc for the signed variant (its
+// data is folded raw: Dc absorbs the complement) and of D for the unsigned
+// one, with K = K8.
+template <bool SAR>
+__device__ __forceinline__ uint32_t crc_segment(const uint32_t *sD, const uint32_t *sT,
+                                                const uint32_t *sA, const uint32_t *sR,
+                                                const Rep8Lane &R8, uint32_t K8,
+                                                const uint8_t *Ap, uint64_t len, bool first_seg,
+                                                int lane)
+{
+    const int64_t a0 = (int64_t)((uintptr_t)Ap & 15u);  // segment start within its vector
+    const uint4 *v = reinterpret_cast<const uint4 *>(Ap - a0);
+    const int64_t e_off = a0 + (int64_t)len;
+    const int64_t nvec = e_off >> 4;  // full vectors ending at or before the end
+    const bool xor4 = !SAR && first_seg;
+    uint32_t state = 0;
+    if (nvec > 0) {
+        const int64_t J = (nvec + 255) >> 8;
+        const uint4 neutral = SAR ? make_uint4(~0u, ~0u, ~0u, ~0u) : make_uint4(0, 0, 0, 0);
+        uint32_t acc = 0;
+        // lane `lane` folds vectors 4 lane .. 4 lane + 3 of each 4 KiB block
+        auto lidx = [&](int64_t blk0, int q) -> int64_t { return blk0 + 4 * lane + q; };
+        uint4 nx[4];
+        {  // first (partial) block: vectors before index 0 are neutral
+            const int64_t b0 = nvec - 256 * J;
+            const int64_t vb = b0 + 4 * lane;
+            uint4 w[4];
+#pragma unroll
+            for (int q = 0; q < 4; q++) {
+                const int64_t li = lidx(b0, q);
+                w[q] = v[li < 0 ? 0 : li];
+            }
+#pragma unroll
+            for (int q = 0; q < 4; q++) {
+                const int64_t vi = vb + q;
+                if (vi < 0)
+                    w[q] = neutral;
+                else if (16 * vi < a0 + 4)
+                    w[q] = seg_fix_vector<SAR>(w[q], 16 * vi, a0, xor4);
+            }
+#pragma unroll
+            for (int q = 0; q < 4; q++)
+                acc = chain16r<SAR>(sD, R8, acc, w[q], K8);
+        }
+        // blocks 1..J-1: the next block's 64 B per lane is loaded while this
+        // one is folded (index clamped on the last block: no branch)
+        if (J > 1) {
+#pragma unroll
+            for (int q = 0; q < 4; q++)
+                nx[q] = v[lidx(nvec - 256 * (J - 1), q)];
+        }
+        for (int64_t jb = 1; jb < J; jb++) {
+            uint4 w[4];
+#pragma unroll
+            for (int q = 0; q < 4; q++)
+                w[q] = nx[q];
+            {
+                const int64_t jn = (jb + 1 < J) ? jb + 1 : jb;
+#pragma unroll
+                for (int q = 0; q < 4; q++)
+                    nx[q] = v[lidx(nvec - 256 * (J - jn), q)];
+            }
+            acc = apply4(sA, acc);  // advance 4032 B to this lane's next piece
+            if (jb == 1 && nvec - 256 * (J - 1) == 1 && lane == 0)
+                w[0] = seg_fix_vector<SAR>(w[0], 16, a0, xor4);  // vector 1 opens block 1
+#pragma unroll
+            for (int q = 0; q < 4; q++)
+                acc = chain16r<SAR>(sD, R8, acc, w[q], K8);
+        }
+        // wave reduction: lane group values relative to the group's end
+#pragma unroll
+        for (int lv = 0; lv < 6; lv++) {
+            const uint32_t u = apply4(sR + lv * 1024, acc);
+            const uint32_t o = __shfl_xor(u, 1 << lv);
+            if (lane & (1 << lv))
+                acc ^= o;
+        }
+        state = __shfl(acc, 63);
+    }
+    const int64_t t0 = (16 * nvec > a0) ? 16 * nvec : a0;
+    for (int64_t o = t0; o < e_off; o++) {
+        uint32_t b = Ap[o - a0];
+        if (SAR || (xor4 && o < a0 + 4))
+            b ^= 0xFFu;
+        state = crc_byte<SAR>(sT, state, b);
+    }
+    return state;
+}
+
 // ---- the sparse fold (fdfs_tables.hpp fold_exp) -----------
 // A wave reduces a run of 16-byte vectors x_0..x_{n-1} (the run's bytes in
 // the CRC's domain: complemented for the signed variant, the file's first 4

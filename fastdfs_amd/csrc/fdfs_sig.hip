@@ -100,29 +100,119 @@ __global__ __launch_bounds__(kSegBlock) void crc_seg_kernel(
     }
 }
 
+// crc_tab_kernel<SAR>: the table fold, for files below kFoldMinBytes (the
+// sparse fold's per-run costs -- its remainder, its ring's first steps --
+// would dominate there).  One wave per kSegBytes segment range, each lane
+// 64 B of every 4 KiB block with the rotated, replicated slice-by-8 tables,
+// a 6-level GF(2) combine across the wave; a wave's consecutive segments of
+// one file chain with the one-segment advance (ADVSEG).
+template <bool SAR>
+__global__ __launch_bounds__(kSegBlock) void crc_tab_kernel(
+    const uint8_t *__restrict__ base, const uint64_t *__restrict__ offs,
+    const uint64_t *__restrict__ sizes, const uint64_t *__restrict__ seg_first, uint32_t n_host,
+    const uint32_t *__restrict__ n_dev, const DevTables *__restrict__ tabs, uint32_t *__restrict__ crc_out)
+{
+    const uint32_t n = n_dev ? *n_dev : n_host;  // file count, or written by big_plan_kernel
+    const uint64_t total = seg_first[n];
+    {  // a workgroup none of whose waves has a segment (small batches) skips the table fill
+        const uint64_t nw = (uint64_t)gridDim.x * (blockDim.x >> 6), w0 = (uint64_t)blockIdx.x * (blockDim.x >> 6);
+        if ((total * w0) / nw == (total * (w0 + (blockDim.x >> 6))) / nw)
+            return;
+    }
+    // the 64 KiB conflict-free tables in LDS; the reduction tables stay in
+    // global memory (24 lookups per segment)
+    constexpr int kD = kRep8Dwords;
+    __shared__ uint32_t smem[kD + 256 + 2 * 4 * 256];
+    uint32_t *sD = smem, *sT = smem + kD, *sA = sT + 256, *sS = sA + 1024;
+    const uint32_t *sR = &tabs->t.ADVRED[0][0][0];
+    lds_fill(sS, &tabs->t.ADVSEG[0][0], 4 * 256);
+    lds_fill_rep8(sD, SAR ? &tabs->Dc[0][0] : &tabs->t.D[0][0]);
+    lds_fill(sT, tabs->t.T, 256);
+    lds_fill(sA, &tabs->t.ADV4032[0][0], 4 * 256);
+    __syncthreads();
+
+    const uint32_t K8 = tabs->t.K8;
+    const Rep8Lane R8 = rep8_lane(threadIdx.x & 63);
+    const int lane = threadIdx.x & 63;
+    const uint64_t wpb = blockDim.x >> 6;
+    const uint64_t w = (uint64_t)blockIdx.x * wpb + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const uint64_t nw = (uint64_t)gridDim.x * wpb;
+    uint64_t s = (total * w) / nw;
+    const uint64_t s_end = (total * (w + 1)) / nw;
+    if (s >= s_end)
+        return;
+    uint32_t lo = 0, hi = n;  // last f with seg_first[f] <= s
+    while (hi - lo > 1) {
+        const uint32_t mid = (lo + hi) >> 1;
+        if (seg_first[mid] <= s)
+            lo = mid;
+        else
+            hi = mid;
+    }
+    uint32_t f = lo;
+    // The wave's segments are consecutive, so a run of segments of one file
+    // is chained in place (state = ADV_seg(state) ^ crc0(seg), one 4-lookup
+    // advance per segment); only when the run ends is the state advanced to
+    // the file end (GF(2) matrix powers) and merged into crc_out.
+    uint32_t run_f = 0xFFFFFFFFu, run_state = 0;
+    uint64_t run_end = 0;
+    bool run_has_first = false, run_whole = false;
+    for (;; s++) {
+        const bool more = s < s_end;
+        if (more) {
+            while (seg_first[f + 1] <= s)
+                f++;
+        }
+        if (run_f != 0xFFFFFFFFu && (!more || f != run_f)) {  // flush the finished run
+            const uint64_t L = sizes[run_f];
+            const uint32_t cl = run_has_first ? crc_final_const<SAR>(L) : 0u;
+            if (run_whole) {
+                if (lane == 0)
+                    crc_out[run_f] = run_state ^ cl;
+            } else {
+                const uint32_t v = advance_any(tabs, run_state, L - run_end, lane);
+                if (lane == 0)
+                    atomicXor(&crc_out[run_f], v ^ cl);
+            }
+            run_f = 0xFFFFFFFFu;
+        }
+        if (!more)
+            break;
+        const uint64_t k = s - seg_first[f];
+        const uint64_t nseg = seg_first[f + 1] - seg_first[f];
+        const uint64_t L = sizes[f];
+        const uint8_t *fp = base + offs[f];
+        const uint64_t lo_b = k * kSegBytes;
+        const uint64_t hi_b = (L < lo_b + kSegBytes) ? L : lo_b + kSegBytes;
+        const uint32_t v = crc_segment<SAR>(sD, sT, sA, sR, R8, K8, fp + lo_b, hi_b - lo_b, k == 0, lane);
+        if (run_f == f) {
+            const uint64_t len = hi_b - lo_b;
+            const uint32_t adv = (len == kSegBytes) ? apply4(sS, run_state)
+                                                    : advance_any(tabs, run_state, len, lane);
+            run_state = adv ^ v;
+        } else {
+            run_f = f;
+            run_state = v;
+            run_has_first = (k == 0);
+        }
+        run_end = hi_b;
+        run_whole = run_has_first && (k + 1 == nseg);
+    }
+}
+
 // ---------------------------------------------------------------- planning
 
-// Batches of at most kPlanSmall files: segment counts, their exclusive scan
-// (seg_first[0..n]) and the zeroed CRC slots in one workgroup, instead of
-// plan_nseg_kernel + the three-kernel scan (a small call is launch-bound).
+// Batches of at most kPlanSmall files: segment counts, their exclusive scans
+// (seg_first[0..n] of the table kernel's list, seg_first[n + 1 ..] of the
+// fold kernel's: a file's segments are in one of them) and the zeroed CRC
+// slots in one workgroup, instead of plan_nseg_kernel + two three-kernel
+// scans (a small call is launch-bound).
 constexpr int kPlanSmallItems = 4;
 constexpr uint32_t kPlanSmall = 1024 * kPlanSmallItems;
 
-__global__ __launch_bounds__(1024) void plan_small_kernel(const uint64_t *__restrict__ sizes, uint32_t n,
-                                                          uint64_t *__restrict__ seg_first,
-                                                          uint32_t *__restrict__ crc_out)
+__device__ __forceinline__ uint64_t block_scan_u64(uint64_t x, uint64_t *wsum)  // exclusive, 1024 threads
 {
-    __shared__ uint64_t wsum[16];
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-    const uint32_t i0 = threadIdx.x * kPlanSmallItems;
-    uint64_t v[kPlanSmallItems], x = 0;
-#pragma unroll
-    for (int k = 0; k < kPlanSmallItems; k++) {
-        v[k] = i0 + k < n ? (sizes[i0 + k] + kSegBytes - 1) / kSegBytes : 0;
-        x += v[k];
-        if (i0 + k < n)
-            crc_out[i0 + k] = 0;  // empty files keep CRC 0; multi-segment files accumulate by XOR
-    }
     const uint64_t mine = x;
 #pragma unroll
     for (int o = 1; o < 64; o <<= 1) {
@@ -136,11 +226,37 @@ __global__ __launch_bounds__(1024) void plan_small_kernel(const uint64_t *__rest
     uint64_t run = x - mine;
     for (int k = 0; k < wid; k++)
         run += wsum[k];
+    __syncthreads();
+    return run;
+}
+
+__global__ __launch_bounds__(1024) void plan_small_kernel(const uint64_t *__restrict__ sizes, uint32_t n,
+                                                          uint64_t *__restrict__ seg_first,
+                                                          uint32_t *__restrict__ crc_out)
+{
+    __shared__ uint64_t wsum[16];
+    const uint32_t i0 = threadIdx.x * kPlanSmallItems;
+    uint64_t vt[kPlanSmallItems], vf[kPlanSmallItems], xt = 0, xf = 0;
 #pragma unroll
     for (int k = 0; k < kPlanSmallItems; k++) {
-        if (i0 + k <= n)
-            seg_first[i0 + k] = run;  // seg_first[n] = the total
-        run += v[k];
+        const uint64_t L = i0 + k < n ? sizes[i0 + k] : 0;
+        const uint64_t c = (L + kSegBytes - 1) / kSegBytes;
+        vt[k] = L < kFoldMinBytes ? c : 0;
+        vf[k] = L < kFoldMinBytes ? 0 : c;
+        xt += vt[k];
+        xf += vf[k];
+        if (i0 + k < n)
+            crc_out[i0 + k] = 0;  // empty files keep CRC 0; multi-segment files accumulate by XOR
+    }
+    uint64_t rt = block_scan_u64(xt, wsum), rf = block_scan_u64(xf, wsum);
+#pragma unroll
+    for (int k = 0; k < kPlanSmallItems; k++) {
+        if (i0 + k <= n) {
+            seg_first[i0 + k] = rt;  // seg_first[n] = the total
+            seg_first[n + 1 + i0 + k] = rf;
+        }
+        rt += vt[k];
+        rf += vf[k];
     }
 }
 
@@ -151,7 +267,9 @@ __global__ void plan_nseg_kernel(const uint64_t *__restrict__ sizes, uint32_t n,
     if (i >= n)
         return;
     const uint64_t L = sizes[i];
-    nseg[i] = (L + kSegBytes - 1) / kSegBytes;
+    const uint64_t c = (L + kSegBytes - 1) / kSegBytes;
+    nseg[i] = L < kFoldMinBytes ? c : 0;  // the table kernel's list
+    nseg[n + i] = L < kFoldMinBytes ? 0 : c;  // the fold kernel's
     crc_out[i] = 0;  // empty files keep CRC 0; multi-segment files accumulate by XOR
 }
 
@@ -719,7 +837,7 @@ uint64_t scan_workspace_elems(uint64_t n) { return (n + kScanTile - 1) / kScanTi
 
 static hipError_t crc_seg_run(bool sar, const uint8_t *base, const uint64_t *offs, const uint64_t *sizes,
                               const uint64_t *seg_first, uint32_t n, const uint32_t *n_dev,
-                              const DevTables *tabs, uint32_t *crc_out, unsigned grid, hipStream_t st);
+                              const DevTables *tabs, uint32_t *crc_out, unsigned ncu, hipStream_t st);
 
 hipError_t launch_sig_lane(bool sar, int method, const uint8_t *base, const uint64_t *offs,
                            const uint64_t *sizes, uint32_t n, uint32_t *hist, uint32_t *order,
@@ -749,7 +867,7 @@ hipError_t launch_sig_lane(bool sar, int method, const uint8_t *base, const uint
                                             big->big_min, big->offs, big->sizes, big->seg_first, big->crc, big->poly,
                                             err);
         if ((e = crc_seg_run(sar, base, big->offs, big->sizes, big->seg_first, n, big->nbig, tabs, big->crc,
-                             seg_grid, st)) != hipSuccess)
+                             big->ncu, st)) != hipSuccess)
             return e;
         // poly_seg_kernel: 2 workgroups of 4 waves per CU (its own grid; the
         // CRC kernel's is one 8-wave workgroup per CU)
@@ -779,8 +897,10 @@ hipError_t launch_sig_lane(bool sar, int method, const uint8_t *base, const uint
 
 static hipError_t crc_seg_run(bool sar, const uint8_t *base, const uint64_t *offs, const uint64_t *sizes,
                               const uint64_t *seg_first, uint32_t n, const uint32_t *n_dev,
-                              const DevTables *tabs, uint32_t *crc_out, unsigned grid, hipStream_t st)
+                              const DevTables *tabs, uint32_t *crc_out, unsigned ncu, hipStream_t st)
 {
+    static const int bpc = crc_seg_blocks_per_cu();
+    const unsigned grid = ncu * (unsigned)bpc;
     if (sar)
         crc_seg_kernel<true><<<grid, kSegBlock, kSegRingBytes, st>>>(base, offs, sizes, seg_first, n, n_dev, tabs, crc_out);
     else
@@ -788,22 +908,38 @@ static hipError_t crc_seg_run(bool sar, const uint8_t *base, const uint64_t *off
     return hipGetLastError();
 }
 
+static hipError_t crc_tab_run(bool sar, const uint8_t *base, const uint64_t *offs, const uint64_t *sizes,
+                              const uint64_t *seg_first, uint32_t n, const DevTables *tabs, uint32_t *crc_out,
+                              unsigned ncu, hipStream_t st)
+{
+    static const int bpc = crc_tab_blocks_per_cu();
+    const unsigned grid = ncu * (unsigned)bpc;
+    if (sar)
+        crc_tab_kernel<true><<<grid, kSegBlock, 0, st>>>(base, offs, sizes, seg_first, n, nullptr, tabs, crc_out);
+    else
+        crc_tab_kernel<false><<<grid, kSegBlock, 0, st>>>(base, offs, sizes, seg_first, n, nullptr, tabs, crc_out);
+    return hipGetLastError();
+}
+
 hipError_t launch_crc_seg(bool sar, const uint8_t *base, const uint64_t *offs, const uint64_t *sizes,
                           uint32_t n, uint64_t *nseg, uint64_t *seg_first, uint64_t *bsum,
-                          const DevTables *tabs, uint32_t *crc_out, unsigned grid, hipStream_t st,
+                          const DevTables *tabs, uint32_t *crc_out, unsigned ncu, hipStream_t st,
                           hipEvent_t ev0, hipEvent_t ev1)
 {
     hipError_t e;
+    uint64_t *first_tab = seg_first, *first_fold = seg_first + (size_t)n + 1;
     if (n < kPlanSmall) {
         plan_small_kernel<<<1, 1024, 0, st>>>(sizes, n, seg_first, crc_out);
     } else {
         plan_nseg_kernel<<<(n + 255) / 256, 256, 0, st>>>(sizes, n, nseg, crc_out);
-        if ((e = launch_exclusive_scan(nseg, n, seg_first, bsum, st)) != hipSuccess)
+        if ((e = launch_exclusive_scan(nseg, n, first_tab, bsum, st)) != hipSuccess ||
+            (e = launch_exclusive_scan(nseg + n, n, first_fold, bsum + scan_workspace_elems(n), st)) != hipSuccess)
             return e;
     }
     if (ev0)
         (void)hipEventRecord(ev0, st);
-    if ((e = crc_seg_run(sar, base, offs, sizes, seg_first, n, nullptr, tabs, crc_out, grid, st)) != hipSuccess)
+    if ((e = crc_tab_run(sar, base, offs, sizes, first_tab, n, tabs, crc_out, ncu, st)) != hipSuccess ||
+        (e = crc_seg_run(sar, base, offs, sizes, first_fold, n, nullptr, tabs, crc_out, ncu, st)) != hipSuccess)
         return e;
     if (ev1)
         (void)hipEventRecord(ev1, st);
@@ -814,6 +950,14 @@ int crc_seg_blocks_per_cu()
 {
     int nb = 0;
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, crc_seg_kernel<true>, kSegBlock, kSegRingBytes) != hipSuccess)
+        return 1;
+    return nb > 0 ? nb : 1;
+}
+
+int crc_tab_blocks_per_cu()
+{
+    int nb = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, crc_tab_kernel<true>, kSegBlock, 0) != hipSuccess)
         return 1;
     return nb > 0 ? nb : 1;
 }

@@ -101,6 +101,7 @@ bool build_crc_tables(CrcTables &t, bool arithmetic_shift)
     byte_tables_of(t, t.ADV4032, 4032);
     for (int l = 0; l < 6; l++)
         byte_tables_of(t, t.ADVRED[l], (uint64_t)64 << l);
+    byte_tables_of(t, t.ADVSEG, kSegBytes);
 
     for (int i = 0; i < 32; i++)
         t.MPOW[0][i] = crc_step(t, 1u << i, 0);

@@ -45,6 +45,7 @@ struct CrcTables {
     uint32_t K8;              // chain8 sign fix: M^8(c) = sum_j D[8+j][byte_j(c)] ^ (c<0 ? K8 : 0)
     uint32_t ADV4032[4][256]; // advance by 4032 zero bytes (a 4 KiB block - a lane's 64-byte piece)
     uint32_t ADVRED[6][4][256]; // advance by 64<<t bytes, t = 0..5 (wave reduction tree)
+    uint32_t ADVSEG[4][256];  // advance by one segment (kSegBytes; crc_tab_kernel's runs)
     uint32_t MPOW[48][32];    // columns of M^(2^k), k = 0..47 (arbitrary advance)
     int sar;                  // 1 = arithmetic shift (signed state)
 };

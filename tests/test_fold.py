@@ -19,13 +19,14 @@ HDR = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
 def exponents():
     """(sar, lsr) exponent lists parsed from kFoldTerms / fold_exp in the header."""
     src = open(HDR).read()
-    terms = int(re.search(r"constexpr int kFoldTerms = (\d+);", src).group(1))
+    t = int(re.search(r"constexpr int kFoldTerms = (\d+);", src).group(1))
+    terms = (t, t)
     body = src[src.index("constexpr int fold_exp"):]
     body = body[:body.index("}")]
     out = []
     for part in re.findall(r"\(k == 0 \? 0 :(.*?)\)", body):
         out.append([0] + [int(x) for x in re.findall(r"(\d+)", part)[1::2]] + [int(re.findall(r"(\d+)", part)[-1])])
-    assert len(out) == 2 and all(len(e) == terms for e in out), out
+    assert len(out) == 2 and (len(out[0]), len(out[1])) == terms, out
     return out[0], out[1]
 
 
