@@ -21,7 +21,6 @@ struct fdfs_gpu_ctx {
     unsigned flags = 0;
     bool sar = true;
     fdfs::DevTables *d_tabs = nullptr;
-    unsigned seg_grid = 0;
     uint32_t lat_files = 0;  // lane batches up to one wave per SIMD (BigCrcWs::lat_files)
     uint32_t ncu = 0;        // the device's CU count, read once at open (BigCrcWs::ncu)
     uint64_t lane_err_seen = 0;  // lane-path error count already reported (lane_err_check)
@@ -371,7 +370,6 @@ int fdfs_gpu_open(int device, unsigned flags, fdfs_gpu_ctx **out)
     int ncu = 256;
     if (hipGetDeviceProperties(&prop, device) == hipSuccess && prop.multiProcessorCount > 0)
         ncu = prop.multiProcessorCount;
-    ctx->seg_grid = (unsigned)ncu;  // the CRC launchers size their grids per kernel
     ctx->lat_files = (uint32_t)ncu * 4 * 64;
     ctx->ncu = (uint32_t)ncu;
     *out = ctx;
@@ -506,7 +504,7 @@ int fdfs_gpu_sig_batch(fdfs_gpu_ctx *ctx, const fdfs_gpu_batch *batch, int metho
         hipEvent_t a, b;
         timing_pair(ctx, FDFS_KERNEL_CRC_SEG, a, b);
         e = fdfs::launch_crc_seg(ctx->sar, base, batch->offset, batch->size, n, nseg, first, bsum,
-                                 ctx->d_tabs, crc_out, ctx->seg_grid, st, a, b);
+                                 ctx->d_tabs, crc_out, ctx->ncu, st, a, b);
     } else {
         uint32_t *hist = cv.take<uint32_t>(fdfs::kLaneWsDwords);
         uint32_t *order = cv.take<uint32_t>(n);
@@ -515,7 +513,7 @@ int fdfs_gpu_sig_batch(fdfs_gpu_ctx *ctx, const fdfs_gpu_batch *batch, int metho
         timing_pair(ctx, FDFS_KERNEL_SIG_LANE, a, b);
         e = fdfs::launch_sig_lane(ctx->sar, method, base, batch->offset, batch->size, n, hist,
                                   order, &big, ctx->d_tabs, crc_out, sig_out, codes_out, nullptr, nullptr,
-                                  ctx->seg_grid, st, a, b);
+                                  ctx->ncu, st, a, b);
         if (e == hipSuccess)
             e = lane_err_note(ctx, hist, st);
     }
@@ -600,7 +598,7 @@ static int update_batch(fdfs_gpu_ctx *ctx, const fdfs_gpu_batch *chunks, const u
         hipEvent_t a, b;
         timing_pair(ctx, FDFS_KERNEL_CRC_SEG, a, b);
         e = fdfs::launch_crc_seg(ctx->sar, base, chunks->offset, chunks->size, n, nseg, first, bsum,
-                                 ctx->d_tabs, tmp, ctx->seg_grid, st, a, b);
+                                 ctx->d_tabs, tmp, ctx->ncu, st, a, b);
         if (e == hipSuccess)
             e = fdfs::launch_crc_carry(tmp, chunks->size, n, state_idx, states, ctx->d_tabs, st);
     } else {
@@ -610,7 +608,7 @@ static int update_batch(fdfs_gpu_ctx *ctx, const fdfs_gpu_batch *chunks, const u
         hipEvent_t a, b;
         timing_pair(ctx, FDFS_KERNEL_SIG_LANE, a, b);
         e = fdfs::launch_sig_lane(ctx->sar, method, base, chunks->offset, chunks->size, n, hist, order, &big,
-                                  ctx->d_tabs, nullptr, nullptr, nullptr, states, state_idx, ctx->seg_grid,
+                                  ctx->d_tabs, nullptr, nullptr, nullptr, states, state_idx, ctx->ncu,
                                   st, a, b);
         if (e == hipSuccess)
             e = lane_err_note(ctx, hist, st);
@@ -1690,7 +1688,7 @@ static hipError_t cg_pieces(fdfs_gpu_ctx *ctx, const fdfs_gpu_batch *pieces, con
     hipEvent_t a, b;
     timing_pair(ctx, FDFS_KERNEL_CRC_SEG, a, b);
     e = fdfs::launch_crc_seg(ctx->sar, static_cast<const uint8_t *>(pieces->base), pieces->offset, pieces->size, np,
-                             nseg, first, bsum, ctx->d_tabs, crc, ctx->seg_grid, st, a, b);
+                             nseg, first, bsum, ctx->d_tabs, crc, ctx->ncu, st, a, b);
     if (e == hipSuccess)
         e = fdfs::launch_crc_pieces(crc, pfile, pstart, pieces->size, np, fsize, nfiles, mine, ctx->d_tabs, st);
     return e;

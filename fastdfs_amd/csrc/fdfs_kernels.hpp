@@ -58,7 +58,7 @@ hipError_t launch_sig_lane(bool sar, int method, const uint8_t *base, const uint
                            const uint64_t *sizes, uint32_t n, uint32_t *hist, uint32_t *order,
                            const BigCrcWs *big, const DevTables *tabs, uint32_t *crc_out,
                            uint8_t *sig_out, int32_t *codes_out, fdfs_gpu_file_state *states,
-                           const uint32_t *sidx, unsigned seg_grid, hipStream_t st,
+                           const uint32_t *sidx, unsigned ncu, hipStream_t st,
                            hipEvent_t ev0, hipEvent_t ev1);
 // The CRC of n files, CRC only: the files below kFoldMinBytes through
 // crc_tab_kernel, the others through crc_seg_kernel (the sparse fold), each
