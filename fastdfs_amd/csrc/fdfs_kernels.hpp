@@ -64,7 +64,10 @@ hipError_t launch_sig_lane(bool sar, int method, const uint8_t *base, const uint
 // crc_tab_kernel, the others through crc_seg_kernel (the sparse fold), each
 // over its own segment list.  Workspace: nseg[2 n], seg_first[2 (n + 1)],
 // bsum[2 scan_workspace_elems(n)] (crc_plan_elems).
-constexpr uint64_t kFoldMinBytes = 256 * 1024;
+// (the measured crossover: 64 KiB files 0.92 ms per 4 GiB on the fold
+// against 0.80 on the table kernel, 128 KiB files 0.69-0.71 against 0.78;
+// profiles/r05/crc_size_sweep.txt)
+constexpr uint64_t kFoldMinBytes = 96 * 1024;
 hipError_t launch_crc_seg(bool sar, const uint8_t *base, const uint64_t *offs, const uint64_t *sizes,
                           uint32_t n, uint64_t *nseg, uint64_t *seg_first, uint64_t *bsum,
                           const DevTables *tabs, uint32_t *crc_out, unsigned ncu, hipStream_t st,

@@ -141,17 +141,17 @@ def test_crc_plan_small_boundary(oracle, ctxs, n):
 @pytest.mark.parametrize("variant", [0, 1])
 @pytest.mark.parametrize("n", [300, 4200])
 def test_crc_fold_split(oracle, ctxs, variant, n):
-    """CRC only, one batch across the kernel split (kFoldMinBytes = 256 KiB:
+    """CRC only, one batch across the kernel split (kFoldMinBytes = 96 KiB:
     smaller files take the table kernel, the others the sparse fold): sizes
     on both sides of and at the threshold, runs shorter and longer than the
     fold relation's degree (575 / 300 vectors) and than its ring (1024
     vectors), byte-aligned starts, both plans (one workgroup below 4,096
     files, the two scans above), both shift variants."""
     rng = np.random.default_rng(71 + variant + n)
-    edge = [0, 1, 15, 16, 17, (256 << 10) - 1, 256 << 10, (256 << 10) + 1, (256 << 10) + 4000,
+    edge = [0, 1, 15, 16, 17, (96 << 10) - 1, 96 << 10, (96 << 10) + 1, (96 << 10) + 4000,
             16 * 575, 16 * 575 + 1, 16 * 1088 + 5, (1 << 20) + 7, (3 << 20) + 11]
     sizes = np.concatenate([edge, rng.integers(0, 300_000, n - len(edge) - 8),
-                            rng.integers(256 << 10, 2 << 20, 8)])
+                            rng.integers(96 << 10, 2 << 20, 8)])
     rng.shuffle(sizes)
     buf, offs, sz = _packed(sizes, 1, rng)
     _check(oracle, ctxs[variant], variant, buf, offs, sz, methods=(0,))
