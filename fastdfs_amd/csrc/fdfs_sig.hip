@@ -43,6 +43,7 @@ __global__ __launch_bounds__(kSegBlock) void crc_seg_kernel(
     // advance and the byte table in LDS; the reduction tables stay in global
     // memory (24 lookups per run)
     __shared__ uint32_t smem[16 * 256 + 4 * 256 + 256];
+    static_assert(sizeof(smem) + kSegRingBytes <= 160 * 1024, "one workgroup's LDS fits the CU's 160 KiB");
     uint32_t *sD = smem, *sA = smem + 16 * 256, *sT = sA + 4 * 256;
     const uint32_t *sR = &tabs->t.ADVRED[0][0][0];
     lds_fill(sD, &tabs->t.D[0][0], 16 * 256);
