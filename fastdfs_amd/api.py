@@ -549,13 +549,17 @@ class Comm:
         L = ctx._L
         rank, world = dist.get_rank(group), dist.get_world_size(group)
         buf = ctypes.create_string_buffer(_lib.COMM_ID_BYTES)
-        if rank == 0 and L.fdfs_gpu_comm_unique_id(buf):
-            raise FdfsGpuError(errno.EIO, "fdfs_gpu_comm_unique_id")
+        # the id travels with a status byte, so a failure on rank 0 is every
+        # rank's error instead of leaving the others in the broadcast
+        ok = not (rank == 0 and L.fdfs_gpu_comm_unique_id(buf))
         backend = dist.get_backend(group)
         dev = torch.device("cuda", ctx.device) if backend == "nccl" else torch.device("cpu")
-        t = torch.frombuffer(bytearray(buf.raw), dtype=torch.uint8).to(dev)
+        t = torch.frombuffer(bytearray(buf.raw + bytes([ok])), dtype=torch.uint8).to(dev)
         dist.broadcast(t, src=dist.get_global_rank(group, 0) if group is not None else 0, group=group)
-        uid = bytes(t.cpu().numpy().tobytes())
+        raw = bytes(t.cpu().numpy().tobytes())
+        if not raw[-1]:
+            raise FdfsGpuError(errno.EIO, "fdfs_gpu_comm_unique_id (rank 0)")
+        uid = raw[:-1]
         h = ctypes.c_void_p()
         ctx._rc(L.fdfs_gpu_comm_init(ctx._h, uid, world, rank, ctypes.byref(h)), "fdfs_gpu_comm_init")
         self._L, self.handle, self.rank, self.world = L, h, rank, world
