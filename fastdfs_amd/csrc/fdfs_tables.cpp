@@ -2,6 +2,7 @@
 #include "fdfs_tables.hpp"
 
 #include <cstring>
+#include <utility>
 
 namespace fdfs {
 
@@ -115,6 +116,56 @@ bool build_crc_tables(CrcTables &t, bool arithmetic_shift)
         for (int k = 0; k < kFoldTerms; k++)
             v ^= crc_advance(t, 1u << i, 16ull * (uint64_t)fold_exp(t.sar != 0, k));
         if (v != 0)
+            return false;
+    }
+    // The lane fold's relation R(A4) = 0 on every basis vector, and Y4: a
+    // state c enters a lane's fold as the data dword c ^ (c < 0 ? Y4 : 0),
+    // since M^4(c) = crc0(c as 4 data bytes) ^ (c < 0 ? crc0(Y4) : 0).
+    for (int i = 0; i < 32; i++) {
+        uint32_t v = 0;
+        for (int k = 0; k < lane_fold_terms(t.sar != 0); k++)
+            v ^= crc_advance(t, 1u << i, 4ull * (uint64_t)lane_fold_exp(t.sar != 0, k));
+        if (v != 0)
+            return false;
+    }
+    {
+        auto crc0_4 = [&](uint32_t y) {
+            return t.D[12][y & 0xFFu] ^ t.D[13][(y >> 8) & 0xFFu] ^ t.D[14][(y >> 16) & 0xFFu] ^ t.D[15][y >> 24];
+        };
+        const uint32_t k4 = adv_bytes(t, 0x80000000u, 4) ^ crc0_4(0x80000000u);
+        // solve crc0_4(y) = k4 over GF(2): eliminate on the basis images
+        uint32_t img[32], pre[32];
+        for (int i = 0; i < 32; i++) {
+            img[i] = crc0_4(1u << i);
+            pre[i] = 1u << i;
+        }
+        uint32_t rhs = k4, y = 0;
+        for (int bit = 31, row = 0; bit >= 0; bit--) {
+            int piv = -1;
+            for (int i = row; i < 32; i++)
+                if (img[i] >> bit & 1u) {
+                    piv = i;
+                    break;
+                }
+            if (piv < 0)
+                return false;  // crc0 of 4 bytes is a bijection
+            std::swap(img[row], img[piv]);
+            std::swap(pre[row], pre[piv]);
+            for (int i = 0; i < 32; i++)
+                if (i != row && (img[i] >> bit & 1u)) {
+                    img[i] ^= img[row];
+                    pre[i] ^= pre[row];
+                }
+            if (rhs >> bit & 1u) {
+                rhs ^= img[row];
+                y ^= pre[row];
+            }
+            row++;
+        }
+        if (rhs != 0 || crc0_4(y) != k4)
+            return false;
+        t.Y4 = y;
+        if (!t.sar && t.Y4 != 0)
             return false;
     }
     // Self-check the power matrices against direct stepping.

@@ -36,6 +36,24 @@ __host__ __device__ constexpr int fold_exp(bool sar, int k)
                : (k == 0 ? 0 : k == 1 ? 89 : k == 2 ? 117 : k == 3 ? 155 : 300);
 }
 
+// The lane fold of sig_hash_kernel: R(y) = sum_k y^r_k, the
+// minimal polynomial of A4 = the advance by 4 zero bytes (degree 32; 13 terms
+// for the arithmetic shift, 15 for the logical one; Gaussian elimination over
+// the powers of A4, scripts/fold_search.py lane).  Because A4^32 =
+// sum_{k<last} A4^r_k, a lane folds its file's dwords as
+// c'_j = x_j ^ sum_{k<last} c'_{j - (32 - r_k)} in 32 registers -- no table
+// lookup -- and takes the crc0 of the last 32 c' (after a correction inside
+// that window) with the slice-by-16 tables.  build_crc_tables re-verifies
+// R(A4) = 0 on the 32 basis vectors.
+constexpr int kLaneFoldMaxTerms = 15;
+__host__ __device__ constexpr int lane_fold_terms(bool sar) { return sar ? 13 : 15; }
+__host__ __device__ constexpr int lane_fold_exp(bool sar, int k)
+{
+    constexpr int es[13] = {0, 1, 2, 3, 6, 7, 11, 19, 20, 22, 24, 31, 32};
+    constexpr int el[15] = {0, 1, 2, 4, 5, 7, 8, 10, 11, 12, 16, 22, 23, 26, 32};
+    return sar ? es[k] : el[k];
+}
+
 // Zero-input byte step M (advance by one zero byte) is GF(2)-linear in the
 // state for both shift semantics, which is what every table below relies on.
 struct CrcTables {
@@ -47,6 +65,7 @@ struct CrcTables {
     uint32_t ADVRED[6][4][256]; // advance by 64<<t bytes, t = 0..5 (wave reduction tree)
     uint32_t ADVSEG[4][256];  // advance by one segment (kSegBytes; crc_tab_kernel's runs)
     uint32_t MPOW[48][32];    // columns of M^(2^k), k = 0..47 (arbitrary advance)
+    uint32_t Y4;              // lane fold: the dword y with crc0(y) = M^4(e_31) ^ crc0(e_31) (0 for a logical shift)
     int sar;                  // 1 = arithmetic shift (signed state)
 };
 
