@@ -131,6 +131,52 @@ __device__ __forceinline__ uint32_t chain16(const uint32_t *__restrict__ D, uint
     return r;
 }
 
+// One dword of the lane fold (fdfs_tables.hpp lane_fold_exp): c'_s = x ^
+// sum_{k<last} ring[(s - (32 - r_k)) & 31].  ring holds c' of the step's
+// dwords 0..s-1 and of the previous step's s..31, so every source is there
+// (the lag-32 one is read before slot s is overwritten).  Oldest terms first:
+// the newest source is on the last bitop3 alone.  6 VALU (arithmetic shift)
+// or 7 (logical) per dword, against ~7.5 VALU + 4 LDS lookups for the
+// slice-by-16 fold of the same 4 bytes.
+template <bool SAR>
+__device__ __forceinline__ uint32_t lane_fold_dw(const uint32_t (&ring)[32], int s, uint32_t x)
+{
+    constexpr int nt = lane_fold_terms(SAR) - 1;  // sources
+    uint32_t acc = x;
+#pragma unroll
+    for (int k = 0; k + 1 < nt; k += 2)
+        acc = __builtin_amdgcn_bitop3_b32(acc, ring[(s - (32 - lane_fold_exp(SAR, k))) & 31],
+                                          ring[(s - (32 - lane_fold_exp(SAR, k + 1))) & 31], 0x96);
+    if constexpr ((nt & 1) != 0)
+        acc ^= ring[(s - (32 - lane_fold_exp(SAR, nt - 1))) & 31];
+    return acc;
+}
+
+// The lane's CRC state after its steps: ring = c' of its last 32 dwords
+// (positions n - 32 .. n - 1).  The unfolded recursion also passed on values
+// from inside that window, which the fold must not (only positions <= n - 33
+// carry on), so each window dword first takes back its in-window sources
+// (descending: the sources are still the unfolded c'); then the crc0 of the
+// window's 128 bytes is the state.
+template <bool SAR>
+__device__ __forceinline__ uint32_t lane_fold_finish(const uint32_t *sD, uint32_t K16, uint32_t (&ring)[32])
+{
+#pragma unroll
+    for (int i = 31; i >= 0; i--) {
+#pragma unroll
+        for (int k = 0; k < lane_fold_terms(SAR) - 1; k++) {
+            const int src = i - (32 - lane_fold_exp(SAR, k));
+            if (src >= 0)
+                ring[i] ^= ring[src];
+        }
+    }
+    uint32_t a = 0;
+#pragma unroll
+    for (int v = 0; v < 8; v++)
+        a = chain16<SAR>(sD, a, make_uint4(ring[4 * v], ring[4 * v + 1], ring[4 * v + 2], ring[4 * v + 3]), K16);
+    return a;
+}
+
 // chain16 in two halves (probe build, sig_hash_kernel MODE 3): the 16
 // lookups, then -- after other work has hidden their LDS latency -- the XOR
 // tree.

@@ -438,16 +438,31 @@ __global__ __launch_bounds__(128) void md5_pair_kernel(
                     *reinterpret_cast<u32x4 *>(tile + (k * FPI + fsub) * STRIDE + piece * 16) = R[k];
             };
             uint32_t c = 0xFFFFFFFFu;  // CRC32_XINIT (storage/storage_service.c:7149)
+            // The CRC of the whole blocks: the lane fold (fdfs_device.hpp) in
+            // 32 registers, one round's 32 dwords; XINIT enters as the first
+            // block's first dword (fdfs_tables.hpp Y4).
+            static_assert(CH == 128, "a round is the fold's 32 dwords");
+            uint32_t ring[32];
+#pragma unroll
+            for (int k = 0; k < 32; k++)
+                ring[k] = 0;
+            uint32_t zin = c ^ ((SAR && (int32_t)c < 0) ? tabs->t.Y4 : 0u);
             auto crc_round = [&](uint64_t r, const uint8_t *tile) {
                 const uint4 *q = reinterpret_cast<const uint4 *>(tile + lane * STRIDE);
 #pragma unroll
                 for (int b = 0; b < BPR; b++)
                     if (small && r * BPR + b < nblk) {
-                        c = chain16<SAR>(sD, c, q[4 * b + 0], K16);
-                        c = chain16<SAR>(sD, c, q[4 * b + 1], K16);
-                        c = chain16<SAR>(sD, c, q[4 * b + 2], K16);
-                        c = chain16<SAR>(sD, c, q[4 * b + 3], K16);
+#pragma unroll
+                        for (int k = 0; k < 4; k++) {
+                            const uint4 w = q[4 * b + k];
+                            const int s0 = 16 * b + 4 * k;
+                            ring[s0 + 0] = lane_fold_dw<SAR>(ring, s0 + 0, (b == 0 && k == 0) ? w.x ^ zin : w.x);
+                            ring[s0 + 1] = lane_fold_dw<SAR>(ring, s0 + 1, w.y);
+                            ring[s0 + 2] = lane_fold_dw<SAR>(ring, s0 + 2, w.z);
+                            ring[s0 + 3] = lane_fold_dw<SAR>(ring, s0 + 3, w.w);
+                        }
                     }
+                zin = 0;  // taken by round 0
             };
             issue(RA, 0);
             for (uint64_t r = 0; r < rounds; r += 2) {
@@ -469,6 +484,18 @@ __global__ __launch_bounds__(128) void md5_pair_kernel(
                            "+v"(RA[6]), "+v"(RA[7]), "+v"(RB[0]), "+v"(RB[1]), "+v"(RB[2]), "+v"(RB[3]),
                            "+v"(RB[4]), "+v"(RB[5]), "+v"(RB[6]), "+v"(RB[7]) :: "memory");
             if (valid && small) {
+                if (nblk > 0) {
+                    // the last 32 dwords in position order: an odd block
+                    // count ends mid-ring (slot 15)
+                    const bool odd = nblk & 1;
+#pragma unroll
+                    for (int k = 0; k < 16; k++) {
+                        const uint32_t lo = ring[k], hi = ring[k + 16];
+                        ring[k] = odd ? hi : lo;
+                        ring[k + 16] = odd ? lo : hi;
+                    }
+                    c = lane_fold_finish<SAR>(sD, K16, ring);
+                }
                 const uint32_t rt = (uint32_t)(L & 63u);
                 for (uint32_t k = 0; k < rt; k++)  // CRC of the tail bytes
                     c = crc_byte<SAR>(sT, c, tp[k]);
