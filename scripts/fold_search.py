@@ -10,6 +10,11 @@ search) -- a few seconds per D for D < 200.  Every hit is verified on the
 32 basis vectors; build_crc_tables verifies the chosen one again at open.
 
 usage: python3 scripts/fold_search.py sar|lsr [Dmax] [GAP] [TERMS=6|7]
+       python3 scripts/fold_search.py lane sar|lsr
+The lane mode prints the minimal polynomial of A4 = the advance by 4 zero
+bytes (Gaussian elimination over A4^e s0, e = 0..32, then verified on the
+basis): the relation of the kernels' lane fold (fdfs_tables.hpp
+lane_fold_exp; sar 13 terms, lsr 15).
 (the shipped exponents: sar 0 20 22 41 53 56 135, lsr 0 37 68 69 77 93 161)
 """
 import random
@@ -36,7 +41,50 @@ def zero_byte(c, sar):
     return (T[c & 0xFF] ^ sh) & 0xFFFFFFFF
 
 
+def lane(sar):
+    cols = []
+    for i in range(32):
+        c = 1 << i
+        for _ in range(4):
+            c = zero_byte(c, sar)
+        cols.append(c)
+
+    def apply(v):
+        r = 0
+        for i in range(32):
+            if (v >> i) & 1:
+                r ^= cols[i]
+        return r
+
+    random.seed(11)
+    p = [random.getrandbits(32)]
+    for _ in range(40):
+        p.append(apply(p[-1]))
+    basis = {}
+    for e in range(41):
+        val, comb = p[e], 1 << e
+        while val:
+            hb = val.bit_length() - 1
+            if hb not in basis:
+                basis[hb] = (val, comb)
+                break
+            val, comb = val ^ basis[hb][0], comb ^ basis[hb][1]
+        if not val:
+            ex = [i for i in range(e + 1) if (comb >> i) & 1]
+            for i in range(32):  # R(A4) e_i == 0
+                cur, acc = 1 << i, 0
+                for k in range(ex[-1] + 1):
+                    if k in ex:
+                        acc ^= cur
+                    cur = apply(cur)
+                assert acc == 0
+            print("degree", e, "terms", len(ex), "exponents", ex)
+            return
+
+
 def main():
+    if sys.argv[1] == "lane":
+        return lane(sys.argv[2] == "sar")
     sar = sys.argv[1] == "sar"
     dmax = int(sys.argv[2]) if len(sys.argv) > 2 else 200
     gap = int(sys.argv[3]) if len(sys.argv) > 3 else 64

@@ -5,7 +5,8 @@ gap between the top two exponents must let 64 consecutive vectors fold at
 once, and the fold itself (c_j = x_j ^ sum_k c_{j - (D - e_k)}, D the top
 exponent, positions <= n - 1 - D passing on, crc0 of the last D vectors)
 must give the byte loop's crc0 on random runs of every length class the
-kernel distinguishes."""
+kernel distinguishes.  The same for the lane fold of the lane-per-file
+kernels (fdfs_tables.hpp lane_fold_exp, below)."""
 import os
 import random
 import re
@@ -95,3 +96,85 @@ def test_fold_matches_byte_loop(exps, sar):
             c.append(x)
         rem = b"".join(v.to_bytes(16, "little") for v in c[max(0, n - d):])
         assert crc0(rem, sar) == crc0(data, sar), (sar, n)
+
+
+# ---- the lane fold of sig_hash_kernel / md5_pair_kernel (fdfs_tables.hpp
+# lane_fold_exp, fdfs_device.hpp lane_fold_dw / lane_fold_finish): the
+# minimal polynomial R of A4 = the advance by 4 zero bytes, a 32-dword
+# register ring per lane, the state so far entering as the first dword
+# (with Y4 for the arithmetic shift), the in-window correction at the end.
+
+def lane_exponents():
+    src = open(HDR).read()
+    terms = [int(x) for x in re.search(r"lane_fold_terms\(bool sar\) \{ return sar \? (\d+) : (\d+); \}", src).groups()]
+    es = [int(x) for x in re.search(r"constexpr int es\[\d+\] = \{([^}]*)\}", src).group(1).split(",")]
+    el = [int(x) for x in re.search(r"constexpr int el\[\d+\] = \{([^}]*)\}", src).group(1).split(",")]
+    assert (len(es), len(el)) == tuple(terms)
+    return {True: es, False: el}
+
+
+def crc_state(c, data, sar):
+    for b in data:
+        c = step(c, b, sar)
+    return c
+
+
+def y4(sar):
+    """The dword y with crc0(y) = M^4(e_31) ^ crc0(e_31) (fdfs_tables.cpp)."""
+    k4 = crc_state(0x80000000, b"\0" * 4, sar) ^ crc0((0x80000000).to_bytes(4, "little"), sar)
+    basis = {}
+    for i in range(32):  # eliminate on the images of the unit dwords
+        val, comb = crc0((1 << i).to_bytes(4, "little"), sar), 1 << i
+        while val:
+            hb = val.bit_length() - 1
+            if hb not in basis:
+                basis[hb] = (val, comb)
+                break
+            val, comb = val ^ basis[hb][0], comb ^ basis[hb][1]
+    assert len(basis) == 32, "crc0 of 4 bytes is a bijection"
+    y, val = 0, k4
+    while val:
+        bv, bc = basis[val.bit_length() - 1]
+        val, y = val ^ bv, y ^ bc
+    return y
+
+
+@pytest.mark.parametrize("sar", [True, False])
+def test_lane_relation(sar):
+    e = lane_exponents()[sar]
+    assert e == sorted(e) and e[0] == 0 and e[-1] == 32
+    for i in range(32):
+        acc, cur, k = 0, 1 << i, 0
+        for p in range(33):
+            if p == e[k]:
+                acc ^= cur
+                k += 1
+            cur = crc_state(cur, b"\0" * 4, sar)
+        assert acc == 0, (sar, i)
+
+
+@pytest.mark.parametrize("sar", [True, False])
+def test_lane_fold_matches_byte_loop(sar):
+    """The kernels' lane fold, step by step: 32-dword steps (md5_pair_kernel:
+    64-byte blocks, so a run may end mid-ring), from a random state."""
+    e = lane_exponents()[sar]
+    lags = [32 - x for x in e[:-1]]
+    Y = y4(sar)
+    rng = random.Random(5)
+    for ndw in (16, 32, 48, 64, 96, 112, 160, 1024):
+        cpre = rng.getrandbits(32)
+        data = bytes(rng.getrandbits(8) for _ in range(4 * ndw))
+        ring = [0] * 32
+        zin = cpre ^ (Y if (sar and cpre & 0x80000000) else 0)
+        for j in range(ndw):
+            x = int.from_bytes(data[4 * j:4 * j + 4], "little") ^ (zin if j == 0 else 0)
+            for lag in lags:  # ring[(j - lag) & 31] holds c'_{j - lag} (0 before the run)
+                x ^= ring[(j - lag) & 31]
+            ring[j & 31] = x
+        u = [ring[(ndw - 32 + i) & 31] for i in range(32)]  # positions ndw - 32 .. ndw - 1
+        for i in range(31, -1, -1):
+            for lag in lags:
+                if i - lag >= 0:
+                    u[i] ^= u[i - lag]
+        got = crc0(b"".join(v.to_bytes(4, "little") for v in u), sar)
+        assert got == crc_state(cpre, data, sar), (sar, ndw)
