@@ -434,9 +434,9 @@ def batch_line(args, ctx, world, rank, dev, config, sizes, method, workload, ste
     if tsrc:
         roof["traffic_source"] = tsrc
     if config == "c2" and method == F.SIG_HASH:
-        roof["note"] = ("below the HBM roof: the hash step is co-bound by VALU issue and the LDS "
-                        "pipe, and the chip holds ~2.0 of its 2.4 GHz under this load (loads or "
-                        "compute alone keep 2.4); DESIGN.md 4.2, profiles/r04/clock_ablation_c2.txt")
+        roof["note"] = ("below the HBM roof: the hash step is bound by VALU issue (ELF 4 VALU per byte, "
+                        "the CRC's lane fold 1.5) at the ~1.6-1.75 of 2.4 GHz the chip holds under this "
+                        "load; DESIGN.md 4.2, profiles/r05/issue_clock_c2.txt, profiles/r05/lane_fold_ab.txt")
     if config in ("c1", "c3", "c4") and method != F.SIG_CRC_ONLY:
         # lane-per-file batches whose largest file's dependent chain (MD5
         # / ELFHash) outlasts the HBM stream: the roof is that chain (c4
