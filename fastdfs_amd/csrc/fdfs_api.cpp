@@ -98,6 +98,9 @@ struct Carve {
     }
 };
 
+// CRC-only batches above this many waves per SIMD take the lane path.
+constexpr uint32_t kCrcLaneMinFill = 3;
+
 size_t sig_ws_bytes(uint64_t n)
 {
     size_t lane = align_up(sizeof(uint32_t) * fdfs::kLaneWsDwords) + align_up(sizeof(uint32_t) * n) +
@@ -497,7 +500,13 @@ int fdfs_gpu_sig_batch(fdfs_gpu_ctx *ctx, const fdfs_gpu_batch *batch, int metho
     Carve cv{static_cast<char *>(ctx->ws)};
     const uint8_t *base = static_cast<const uint8_t *>(batch->base);
     hipError_t e;
-    if (method == FDFS_SIG_CRC_ONLY) {
+    // CRC only: batches of up to kCrcLaneMinFill waves per SIMD keep a wave
+    // per file (crc_tab_kernel) or per run (the sparse fold); larger ones
+    // hash their files below kFoldMinBytes one lane per file in the size
+    // order (crc_lane_kernel, the lane fold), the rest by the sparse fold.
+    const bool crc_lanes = method == FDFS_SIG_CRC_ONLY && ctx->lat_files &&
+                           (uint64_t)n > (uint64_t)kCrcLaneMinFill * ctx->lat_files;
+    if (method == FDFS_SIG_CRC_ONLY && !crc_lanes) {
         uint64_t *nseg = cv.take<uint64_t>(2 * (size_t)n);
         uint64_t *first = cv.take<uint64_t>(2 * ((size_t)n + 1));
         uint64_t *bsum = cv.take<uint64_t>(2 * fdfs::scan_workspace_elems(n));
@@ -510,10 +519,10 @@ int fdfs_gpu_sig_batch(fdfs_gpu_ctx *ctx, const fdfs_gpu_batch *batch, int metho
         uint32_t *order = cv.take<uint32_t>(n);
         const fdfs::BigCrcWs big = carve_big(ctx, cv, n);
         hipEvent_t a, b;
-        timing_pair(ctx, FDFS_KERNEL_SIG_LANE, a, b);
+        timing_pair(ctx, crc_lanes ? FDFS_KERNEL_CRC_SEG : FDFS_KERNEL_SIG_LANE, a, b);
         e = fdfs::launch_sig_lane(ctx->sar, method, base, batch->offset, batch->size, n, hist,
-                                  order, &big, ctx->d_tabs, crc_out, sig_out, codes_out, nullptr, nullptr,
-                                  ctx->ncu, st, a, b);
+                                  order, &big, ctx->d_tabs, crc_out, crc_lanes ? nullptr : sig_out,
+                                  crc_lanes ? nullptr : codes_out, nullptr, nullptr, ctx->ncu, st, a, b);
         if (e == hipSuccess)
             e = lane_err_note(ctx, hist, st);
     }

@@ -454,6 +454,190 @@ __global__ __launch_bounds__(kHashBlock) __attribute__((amdgpu_waves_per_eu(1)))
         reinterpret_cast<int4 *>(codes_out)[f] = make_int4((int)c, (int)e, (int)s, (int)t);
 }
 
+// crc_lane_kernel: CRC32 only (FDFS_SIG_CRC_ONLY) for large batches of small
+// files, one lane per file in the size-binned order, the same 128-byte steps
+// and pair-cooperative loads as sig_hash_kernel and the lane fold for the
+// CRC (fdfs_device.hpp): ~29 VALU per 16 bytes, no table lookups, so the
+// loads bound it.  Files >= *big_min_p (kFoldMinBytes for CRC_ONLY,
+// big_plan_kernel) take crc_seg_kernel's sparse fold and are skipped here.
+// fdfs_gpu_sig_batch routes CRC-only batches of more than 3 lat_files files
+// here; smaller ones keep crc_tab_kernel's wave per file (latency).
+// Reference loop replaced: storage/storage_dio.c:465-467 (CRC32_ex per
+// chunk), storage/storage_dio.c:500 (CRC32_FINAL).
+template <bool SAR>
+// 137 VGPRs: three waves per SIMD.  Forcing four makes hipcc spill, and a
+// spill or copy of a load register an asm load is still writing reads it
+// early (measured: half the CRCs wrong), so none is asked for.
+__global__ __launch_bounds__(kHashBlock) void crc_lane_kernel(
+    const uint8_t *__restrict__ base, const uint64_t *__restrict__ offs,
+    const uint64_t *__restrict__ sizes, const uint32_t *__restrict__ order, uint32_t n,
+    const DevTables *__restrict__ tabs, const uint64_t *__restrict__ big_min_p,
+    uint32_t *__restrict__ crc_out)
+{
+    __shared__ uint32_t sD[16 * 256];
+    __shared__ uint32_t sT[256];
+    constexpr int SV = 8;
+    constexpr int NSETS = 2;
+    constexpr uint32_t SB = 16 * SV;
+    lds_fill(sD, &tabs->t.D[0][0], 16 * 256);
+    lds_fill(sT, tabs->t.T, 256);
+    __syncthreads();
+    const int lane = threadIdx.x & 63;
+    const uint32_t wave0 = blockIdx.x * blockDim.x + (threadIdx.x & ~63u);
+    if (wave0 >= n)
+        return;
+    const uint32_t i = wave0 + lane;
+    bool valid = i < n;
+    const uint32_t K16 = tabs->t.K16;
+    const uint8_t *safe = reinterpret_cast<const uint8_t *>(tabs);  // >= 128 readable bytes
+    uint32_t f = valid ? order[i] : 0;
+    if (f >= n) {  // a stale order entry (the binning flagged it): no file
+        valid = false;
+        f = 0;
+    }
+    const uint64_t big_min = big_min_p ? *big_min_p : ~0ull;
+    const uint64_t L0 = valid ? sizes[f] : 0;
+    const bool mine = valid && L0 < big_min;  // else crc_seg_kernel's
+    const uint64_t L = mine ? L0 : 0;
+    const uint8_t *p = mine ? base + offs[f] : safe;
+    uint32_t c = 0xFFFFFFFFu;  // CRC32_XINIT (storage/storage_service.c:7149)
+    // the lane's geometry: bytes to 16-byte alignment, vectors to the line,
+    // whole lines; recomputed after the steps (fewer registers live in them)
+    struct Geo {
+        uint64_t head, nvec, lead;
+    };
+    auto geo = [&]() {
+        Geo g;
+        g.head = (16u - ((uintptr_t)p & 15u)) & 15u;
+        if (g.head > L)
+            g.head = L;
+        g.nvec = (L - g.head) >> 4;
+        const uintptr_t va = (uintptr_t)(p + g.head);
+        g.lead = ((SB - (va & (SB - 1))) & (SB - 1)) >> 4;
+        if (g.lead > g.nvec)
+            g.lead = g.nvec;
+        return g;
+    };
+    uint32_t nsteps;
+    {
+        const Geo g = geo();
+        for (uint64_t k = 0; k < g.head; k++)
+            c = crc_byte<SAR>(sT, c, p[k]);
+        const uint4 *v = reinterpret_cast<const uint4 *>(p + g.head);
+        for (uint64_t j = 0; j < g.lead; j++)
+            c = chain16<SAR>(sD, c, v[j], K16);
+        nsteps = (uint32_t)((g.nvec - g.lead) / SV);
+    }
+    uint32_t nmax = nsteps;
+#pragma unroll
+    for (int o = 32; o; o >>= 1) {
+        const uint32_t y = __shfl_xor(nmax, o);
+        nmax = y > nmax ? y : nmax;
+    }
+    if (nmax) {
+        const uint4 *w = reinterpret_cast<const uint4 *>(p + geo().head) + geo().lead;
+        uint32_t ring[32];
+#pragma unroll
+        for (int k = 0; k < 32; k++)
+            ring[k] = 0;
+        uint32_t zin = c ^ ((SAR && (int32_t)c < 0) ? tabs->t.Y4 : 0u);
+        typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+        auto ptr = [](u32x4 (&a)[SV], int q2) {
+            uint32_t r0[4], r1[4], t[4];
+#pragma unroll
+            for (int d = 0; d < 4; d++) {
+                r0[d] = a[2 * q2][d];
+                r1[d] = a[2 * q2 + 1][d];
+            }
+            pair_transpose(r0, r1, t);
+#pragma unroll
+            for (int d = 0; d < 4; d++) {
+                a[2 * q2][d] = r0[d];
+                a[2 * q2 + 1][d] = t[d];
+            }
+        };
+        auto step = [&](u32x4 (&a)[SV], bool ok) {
+#pragma unroll
+            for (int q = 0; q < SV; q++) {
+                if ((q & 1) == 0) {
+                    __builtin_amdgcn_sched_barrier(0);
+                    ptr(a, q >> 1);
+                    __builtin_amdgcn_sched_barrier(0);
+                }
+                if (ok) {
+                    ring[4 * q + 0] = lane_fold_dw<SAR>(ring, 4 * q + 0, q == 0 ? a[q][0] ^ zin : a[q][0]);
+                    ring[4 * q + 1] = lane_fold_dw<SAR>(ring, 4 * q + 1, a[q][1]);
+                    ring[4 * q + 2] = lane_fold_dw<SAR>(ring, 4 * q + 2, a[q][2]);
+                    ring[4 * q + 3] = lane_fold_dw<SAR>(ring, 4 * q + 3, a[q][3]);
+                }
+            }
+            zin = 0;
+        };
+        u32x4 RS[NSETS][SV];
+        // sig_hash_kernel's pair-cooperative loads (past-the-end steps read `safe`)
+        auto issue_p = [&](u32x4 (&R)[SV], uint32_t stp) {
+            const uint8_t *ln = stp < nsteps ? reinterpret_cast<const uint8_t *>(w + SV * (uint64_t)stp) : safe;
+            const uint64_t a = reinterpret_cast<uint64_t>(ln);
+            const uint32_t lo = (uint32_t)a, hi = (uint32_t)(a >> 32);
+            auto ld = [&](int k, uint32_t lk, uint32_t hk) {
+                const uint8_t *pk = reinterpret_cast<const uint8_t *>(((uint64_t)hk << 32 | lk) + 16u * (lane & 1));
+                asm volatile("global_load_dwordx4 %0, %1, off offset:0" : "=v"(R[k]) : "v"(pk) : "memory");
+                asm volatile("global_load_dwordx4 %0, %1, off offset:32" : "=v"(R[2 + k]) : "v"(pk) : "memory");
+                asm volatile("global_load_dwordx4 %0, %1, off offset:64" : "=v"(R[4 + k]) : "v"(pk) : "memory");
+                asm volatile("global_load_dwordx4 %0, %1, off offset:96" : "=v"(R[6 + k]) : "v"(pk) : "memory");
+            };
+#define PBC(S) (uint32_t) __builtin_amdgcn_mov_dpp((int)lo, S, 0xF, 0xF, false), \
+               (uint32_t) __builtin_amdgcn_mov_dpp((int)hi, S, 0xF, 0xF, false)
+            ld(0, PBC(0xA0));
+            ld(1, PBC(0xF5));
+#undef PBC
+        };
+        auto wait_older = [&](u32x4 (&R)[SV]) {
+            asm volatile("s_waitcnt vmcnt(8)" : "+v"(R[0]), "+v"(R[1]), "+v"(R[2]), "+v"(R[3]) :: "memory");
+            asm volatile("" : "+v"(R[4]), "+v"(R[5]), "+v"(R[6]), "+v"(R[7]));
+        };
+        issue_p(RS[0], 0);
+        for (uint32_t st = 0; st < nmax; st += NSETS) {
+#pragma unroll
+            for (int k = 0; k < NSETS; k++) {
+                issue_p(RS[(k + 1) % NSETS], st + k + 1);
+                wait_older(RS[k]);
+                if (k == 0 || st + k < nmax)
+                    step(RS[k], st + k < nsteps);
+            }
+        }
+#pragma unroll
+        for (int k = 0; k < NSETS; k++)
+            asm volatile("s_waitcnt vmcnt(0)"
+                         : "+v"(RS[k][0]), "+v"(RS[k][1]), "+v"(RS[k][2]), "+v"(RS[k][3]), "+v"(RS[k][4]),
+                           "+v"(RS[k][5]), "+v"(RS[k][6]), "+v"(RS[k][7]) :: "memory");
+        if (nsteps > 0)
+            c = lane_fold_finish<SAR>(sD, K16, ring);
+    }
+    {
+        const Geo g = geo();
+        const uint4 *v = reinterpret_cast<const uint4 *>(p + g.head);
+        for (uint64_t jv = g.lead + SV * (uint64_t)nsteps; jv < g.nvec; jv++)
+            c = chain16<SAR>(sD, c, v[jv], K16);
+        for (uint64_t k = g.head + (g.nvec << 4); k < L; k++)
+            c = crc_byte<SAR>(sT, c, p[k]);
+    }
+    if (mine)
+        crc_out[f] = c ^ 0xFFFFFFFFu;  // CRC32_FINAL (storage/storage_dio.c:500)
+}
+
+hipError_t launch_crc_lane(bool sar, const uint8_t *base, const uint64_t *offs, const uint64_t *sizes, uint32_t n,
+                           const uint32_t *order, const DevTables *tabs, const uint64_t *big_min, uint32_t *crc_out,
+                           hipStream_t st)
+{
+    const unsigned grid = (n + kHashBlock - 1) / kHashBlock;
+    if (sar)
+        crc_lane_kernel<true><<<grid, kHashBlock, 0, st>>>(base, offs, sizes, order, n, tabs, big_min, crc_out);
+    else
+        crc_lane_kernel<false><<<grid, kHashBlock, 0, st>>>(base, offs, sizes, order, n, tabs, big_min, crc_out);
+    return hipGetLastError();
+}
+
 // simple_hash_ex / Time33Hash_ex of the big files (>= T), segment-parallel
 // (INIT_HASH_CODES4 starts both at 0, so a file's hash is the polynomial
 // sum_pos b_pos M^(L-1-pos) mod 2^32 and splits over any cut).  One wave per

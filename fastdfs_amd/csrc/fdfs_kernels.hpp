@@ -77,6 +77,11 @@ hipError_t launch_md5_stage(bool sar, const uint8_t *base, const uint64_t *offs,
                             const DevTables *tabs, const uint64_t *big_min, uint32_t *queue, uint32_t *crc_out,
                             uint8_t *sig_out, int32_t *codes_out, fdfs_gpu_file_state *states,
                             const uint32_t *sidx, unsigned ncu, hipStream_t st);
+// CRC32 only, one lane per file of a size-binned order (large batches of
+// files below *big_min; fdfs_hash.hip crc_lane_kernel).
+hipError_t launch_crc_lane(bool sar, const uint8_t *base, const uint64_t *offs, const uint64_t *sizes, uint32_t n,
+                           const uint32_t *order, const DevTables *tabs, const uint64_t *big_min, uint32_t *crc_out,
+                           hipStream_t st);
 hipError_t launch_sig_hash(bool sar, const uint8_t *base, const uint64_t *offs,
                            const uint64_t *sizes, uint32_t n, const uint32_t *order,
                            const DevTables *tabs, const uint64_t *big_min, uint32_t *crc_out, uint8_t *sig_out,

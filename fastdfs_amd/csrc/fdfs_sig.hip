@@ -537,7 +537,8 @@ __global__ __launch_bounds__(1024) void big_plan_kernel(
     const int mi = method == 2 ? 1 : 0;
     if (n > lat_files) {
         if (threadIdx.x == 0)
-            b0_s = mi ? (uint32_t)kSizeBins : size_bin(kBigCrcMin);  // MD5: no offload
+            b0_s = mi ? (uint32_t)kSizeBins  // MD5: no offload
+                      : size_bin(method == 0 ? kFoldMinBytes : kBigCrcMin);  // CRC only: the fold's files
     } else {
         // thread t: bins 2t, 2t + 1, both of exponent t >> 4
         const int t = threadIdx.x;
@@ -860,6 +861,8 @@ hipError_t launch_sig_lane(bool sar, int method, const uint8_t *base, const uint
     uint32_t *err = hist + kLaneErrWord;
     bin_scatter_kernel<<<sb, 1024, 0, st>>>(sizes, n, cursor, order, err, bmask);
     const bool offload = big != nullptr;
+    if (ev0 && method == 0)  // CRC only: the events cover the fold of the big files too
+        (void)hipEventRecord(ev0, st);
     if (offload) {
         // the segmented passes over the files >= T (CRC; HASH: simple_hash,
         // Time33 too), before the lane kernel (beside it on a second stream
@@ -877,12 +880,15 @@ hipError_t launch_sig_lane(bool sar, int method, const uint8_t *base, const uint
             return e;
     }
     const uint64_t *bmin = offload ? big->big_min : nullptr;
-    if (ev0)
+    if (ev0 && method != 0)
         (void)hipEventRecord(ev0, st);
-    e = (method == 2) ? launch_md5_stage(sar, base, offs, sizes, n, order, tabs, bmin, hist + 2 * kSizeBins,
-                                         crc_out, sig_out, codes_out, states, sidx, big ? big->ncu : 0, st)
-                      : launch_sig_hash(sar, base, offs, sizes, n, order, tabs, bmin, crc_out, sig_out,
-                                        codes_out, states, sidx, st);
+    if (method == 0 && (states || !offload))
+        return hipErrorInvalidValue;  // the CRC-only lane path is one-shot, big files offloaded
+    e = (method == 2)   ? launch_md5_stage(sar, base, offs, sizes, n, order, tabs, bmin, hist + 2 * kSizeBins,
+                                           crc_out, sig_out, codes_out, states, sidx, big ? big->ncu : 0, st)
+        : (method == 1) ? launch_sig_hash(sar, base, offs, sizes, n, order, tabs, bmin, crc_out, sig_out,
+                                          codes_out, states, sidx, st)
+                        : launch_crc_lane(sar, base, offs, sizes, n, order, tabs, bmin, crc_out, st);
     if (e != hipSuccess)
         return e;
     if (ev1)

@@ -358,7 +358,10 @@ int fdfs_gpu_comm_destroy(void *comm);
  * records a HIP event pair on its stream around its main kernel:
  *   FDFS_KERNEL_SIG_LANE  sig_hash_kernel / md5_pair_kernel (md5_stage_kernel for
  *                         update_batch) (FDFS_SIG_HASH / FDFS_SIG_MD5)
- *   FDFS_KERNEL_CRC_SEG   crc_seg_kernel    (FDFS_SIG_CRC_ONLY)
+ *   FDFS_KERNEL_CRC_SEG   the CRC-only kernels (FDFS_SIG_CRC_ONLY): crc_tab_kernel +
+ *                         crc_seg_kernel, or for batches of more than three
+ *                         waves per SIMD of files crc_seg_kernel (files >= 96 KiB)
+ *                         + crc_lane_kernel (the rest)
  *   FDFS_KERNEL_DEDUP     dp_tile .. dp_group_slow, the whole grouping chain (fdfs_gpu_dedup / _group)
  *   FDFS_KERNEL_BUCKET    count + scatter   (fdfs_gpu_dedup_bucket)
  * fdfs_gpu_read_timing waits for the recorded events, returns the summed

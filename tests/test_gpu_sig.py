@@ -266,6 +266,41 @@ def test_offload_regime_boundary(oracle, ctxs, extra):
     torch.cuda.empty_cache()
 
 
+@pytest.mark.parametrize("variant", [0, 1])
+def test_crc_lane_path(oracle, ctxs, variant):
+    """CRC-only batches of more than 3 lat_files files take crc_lane_kernel
+    (one lane per file, the lane fold) for files below kFoldMinBytes and the
+    sparse fold for the rest (fdfs_gpu_sig_batch).  3 lat_files + 1 files of
+    0 B .. 200 KiB packed at byte offsets, with sizes on both sides of 96 KiB
+    and of the lane's 128-byte steps: every CRC equals the wave-per-file
+    path's (the same files in sub-batches of lat_files), and a sample
+    matches the oracle."""
+    from fastdfs_amd import corpus as C
+    lat = torch.cuda.get_device_properties(0).multi_processor_count * 4 * 64
+    n = 3 * lat + 1
+    rng = np.random.default_rng(71 + variant)
+    sizes = rng.integers(0, 100_000, n)
+    edge = rng.choice(n, size=3000, replace=False)
+    sizes[edge[:1000]] = (96 << 10) + rng.integers(-2, 3, 1000)
+    sizes[edge[1000:2000]] = rng.integers(100_000, 200 << 10, 1000)
+    sizes[edge[2000:2500]] = 128 * rng.integers(0, 8, 500) + rng.integers(0, 2, 500)
+    sizes[edge[2500:]] = rng.integers(0, 20, 500)
+    data, offs_t, sizes_t = C.device_batch(sizes, seed=13 + variant, device="cuda:0", align=1)
+    ctx = ctxs[variant]
+    crc, _, _ = ctx.sig_batch(data, offs_t, sizes_t, method=0)
+    ref = torch.cat([ctx.sig_batch(data, offs_t[a:a + lat], sizes_t[a:a + lat], method=0)[0]
+                     for a in range(0, n, lat)])
+    torch.cuda.synchronize()
+    assert torch.equal(crc, ref)
+    crc_np = crc.cpu().numpy().view(np.uint32)
+    offs = offs_t.cpu().numpy()
+    for i in np.concatenate([edge[::25], rng.choice(n, size=200, replace=False)]):
+        d = data[int(offs[i]): int(offs[i] + sizes[i])].cpu().numpy()
+        assert oracle.dio_file(d, 0, variant)[0] == crc_np[i], (i, sizes[i])
+    del data
+    torch.cuda.empty_cache()
+
+
 def test_md5_staged_multiwave(oracle, ctxs):
     """MD5 method over several waves of the staged kernel: files of 0 B to
     1.2 MiB in one aligned batch (lanes finish at different rounds, partial
