@@ -99,7 +99,10 @@ struct Carve {
 };
 
 // CRC-only batches above this many waves per SIMD take the lane path.
-constexpr uint32_t kCrcLaneMinFill = 3;
+#ifndef FDFS_CRC_LANE_MIN_FILL
+#define FDFS_CRC_LANE_MIN_FILL 3
+#endif
+constexpr uint32_t kCrcLaneMinFill = FDFS_CRC_LANE_MIN_FILL;
 
 size_t sig_ws_bytes(uint64_t n)
 {

@@ -5,7 +5,7 @@ production library and once with FDFS_GPU_PROBE_LIB=ab (e.g. `make ab
 AB_REV=8201397`: the slice-by-8 kernel for every size) to place the split
 between crc_tab_kernel and the sparse fold (kFoldMinBytes).
 
-usage: [FDFS_GPU_PROBE_LIB=ab] python3 scripts/crc_size_sweep.py [--total GiB] [--reps N]
+usage: [FDFS_GPU_PROBE_LIB=ab] python3 scripts/crc_size_sweep.py [--total GiB] [--reps N] [--kib 32,64,...]
 """
 import argparse
 import json
@@ -26,11 +26,12 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--total", type=float, default=4.0)
     ap.add_argument("--reps", type=int, default=5)
+    ap.add_argument("--kib", default="32,64,128,192,256,384,512,1024,4096", help="file sizes (KiB)")
     a = ap.parse_args()
     dev = torch.device("cuda", 0)
     ctx = F.Context(0)
     ctx.set_timing(True)
-    for kib in (32, 64, 128, 192, 256, 384, 512, 1024, 4096):
+    for kib in [int(x) for x in a.kib.split(",")]:
         size = kib << 10
         n = max(1, int(a.total * (1 << 30)) // size)
         sizes = np.full(n, size, dtype=np.int64)
