@@ -848,6 +848,8 @@ hipError_t launch_sig_lane(bool sar, int method, const uint8_t *base, const uint
                            const uint32_t *sidx, unsigned ncu, hipStream_t st,
                            hipEvent_t ev0, hipEvent_t ev1)
 {
+    if (method == 0 && (states || big == nullptr))
+        return hipErrorInvalidValue;  // the CRC-only lane path is one-shot, big files offloaded
     hipError_t e = launch_zero_u32(hist, kLaneWsDwords, st);
     if (e != hipSuccess)
         return e;
@@ -882,8 +884,6 @@ hipError_t launch_sig_lane(bool sar, int method, const uint8_t *base, const uint
     const uint64_t *bmin = offload ? big->big_min : nullptr;
     if (ev0 && method != 0)
         (void)hipEventRecord(ev0, st);
-    if (method == 0 && (states || !offload))
-        return hipErrorInvalidValue;  // the CRC-only lane path is one-shot, big files offloaded
     e = (method == 2)   ? launch_md5_stage(sar, base, offs, sizes, n, order, tabs, bmin, hist + 2 * kSizeBins,
                                            crc_out, sig_out, codes_out, states, sidx, big ? big->ncu : 0, st)
         : (method == 1) ? launch_sig_hash(sar, base, offs, sizes, n, order, tabs, bmin, crc_out, sig_out,
