@@ -301,6 +301,35 @@ def test_crc_lane_path(oracle, ctxs, variant):
     torch.cuda.empty_cache()
 
 
+@pytest.mark.parametrize("variant", [0, 1])
+def test_lane_fold_short_files(oracle, ctxs, variant):
+    """The lane fold's edges: files of 0-700 B packed at every
+    byte offset, so lanes run 0, 1, 2 or more 128-byte steps after a head of
+    0-15 bytes and a lead of 0-7 vectors -- one step is exactly the fold's
+    32-dword window, two put the window across the ring's wrap.  200K files
+    (the CRC-only batch takes crc_lane_kernel): CRC-only and HASH CRCs agree
+    for every file and a sample matches the oracle, with HASH signatures."""
+    from fastdfs_amd import corpus as C
+    rng = np.random.default_rng(83 + variant)
+    n = 200_000
+    sizes = rng.integers(0, 701, n)
+    sizes[:2000] = 128 * rng.integers(0, 6, 2000) + rng.integers(-1, 2, 2000).clip(0)
+    data, offs_t, sizes_t = C.device_batch(sizes, seed=21 + variant, device="cuda:0", align=1)
+    ctx = ctxs[variant]
+    crc0, _, _ = ctx.sig_batch(data, offs_t, sizes_t, method=0)
+    crc1, sig1, _ = ctx.sig_batch(data, offs_t, sizes_t, method=1)
+    torch.cuda.synchronize()
+    assert torch.equal(crc0, crc1)
+    crc_np, sig_np = crc1.cpu().numpy().view(np.uint32), sig1.cpu().numpy()
+    offs = offs_t.cpu().numpy()
+    for i in np.concatenate([np.arange(0, 2000, 7), rng.choice(n, size=600, replace=False)]):
+        d = data[int(offs[i]): int(offs[i] + sizes[i])].cpu().numpy()
+        c, sg, _ = oracle.dio_file(d, 1, variant)
+        assert c == crc_np[i] and sg == sig_np[i].tobytes(), (i, sizes[i], offs[i] % 16)
+    del data
+    torch.cuda.empty_cache()
+
+
 def test_md5_staged_multiwave(oracle, ctxs):
     """MD5 method over several waves of the staged kernel: files of 0 B to
     1.2 MiB in one aligned batch (lanes finish at different rounds, partial
