@@ -306,7 +306,7 @@ def test_lane_fold_short_files(oracle, ctxs, variant):
     """The lane fold's edges: files of 0-700 B packed at every
     byte offset, so lanes run 0, 1, 2 or more 128-byte steps after a head of
     0-15 bytes and a lead of 0-7 vectors -- one step is exactly the fold's
-    32-dword window, two put the window across the ring's wrap.  200K files
+    32-dword window, so nothing passes on before the window.  200K files
     (the CRC-only batch takes crc_lane_kernel): CRC-only and HASH CRCs agree
     for every file and a sample matches the oracle, with HASH signatures."""
     from fastdfs_amd import corpus as C
