@@ -10,7 +10,7 @@ search) -- a few seconds per D for D < 200.  Every hit is verified on the
 32 basis vectors; build_crc_tables verifies the chosen one again at open.
 
 usage: python3 scripts/fold_search.py sar|lsr [Dmax] [GAP] [TERMS=6|7]
-       python3 scripts/fold_search.py lane sar|lsr
+       python3 scripts/fold_search.py lane sar|lsr [unit bytes, default 4]
 The lane mode prints the minimal polynomial of A4 = the advance by 4 zero
 bytes (Gaussian elimination over A4^e s0, e = 0..32, then verified on the
 basis): the relation of the kernels' lane fold (fdfs_tables.hpp
@@ -41,11 +41,11 @@ def zero_byte(c, sar):
     return (T[c & 0xFF] ^ sh) & 0xFFFFFFFF
 
 
-def lane(sar):
+def lane(sar, unit=4):
     cols = []
     for i in range(32):
         c = 1 << i
-        for _ in range(4):
+        for _ in range(unit):
             c = zero_byte(c, sar)
         cols.append(c)
 
@@ -84,7 +84,7 @@ def lane(sar):
 
 def main():
     if sys.argv[1] == "lane":
-        return lane(sys.argv[2] == "sar")
+        return lane(sys.argv[2] == "sar", int(sys.argv[3]) if len(sys.argv) > 3 else 4)
     sar = sys.argv[1] == "sar"
     dmax = int(sys.argv[2]) if len(sys.argv) > 2 else 200
     gap = int(sys.argv[3]) if len(sys.argv) > 3 else 64
