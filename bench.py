@@ -395,6 +395,9 @@ def batch_line(args, ctx, world, rank, dev, config, sizes, method, workload, ste
     CPU baseline on rank 0 at N = 1.  The batch is freed on return."""
     n = len(sizes)
     kernel, kname = KERNEL_OF[method]
+    if method == F.SIG_CRC_ONLY and n > 3 * 256 * torch.cuda.get_device_properties(dev).multi_processor_count:
+        # fdfs_gpu_sig_batch's lane path (more than 3 waves per SIMD of files)
+        kname = "crc_lane_kernel<SAR> (+ crc_seg_kernel<SAR> for files >= 96 KiB)"
     workload += {F.SIG_CRC_ONLY: ", CRC32 only (check_file_duplicate=0)",
                  F.SIG_HASH: ", CRC32 + HASH_CODES4 signature + bulk dedup per step",
                  F.SIG_MD5: ", CRC32 + MD5 signature + bulk dedup per step"}[method]
