@@ -31,7 +31,8 @@ if part bench; then
   step bench_c1 900 python3 bench.py --config c1 --steps 3 --warmup 1 || exit $?
   step bench_c4_hash 600 python3 bench.py --config c4 --method hash --steps 2 --warmup 1 || exit $?
   step bench_c4_md5 600 python3 bench.py --config c4 --method md5 --steps 2 --warmup 1 || exit $?
-  for c in c1 c2 c3 c4 c5 c4_hash c4_md5; do tail -1 $O/bench_$c.log | cut -c1-300; done
+  step bench_c2_crc 600 python3 bench.py --config c2 --method crc || exit $?
+  for c in c1 c2 c3 c4 c5 c4_hash c4_md5 c2_crc; do tail -1 $O/bench_$c.log | cut -c1-300; done
 fi
 if part stats; then
   step stats_c2 600 rocprofv3 --kernel-trace --stats -d $O/stats_c2 -o run --output-format csv -- $B --steps 10 --warmup 3 || exit $?

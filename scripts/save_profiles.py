@@ -46,7 +46,7 @@ def steady(trace, out_path):
 
 def main(src, dst):
     os.makedirs(dst, exist_ok=True)
-    for c in ("c1", "c2", "c3", "c4", "c5", "c4_hash", "c4_md5"):
+    for c in ("c1", "c2", "c3", "c4", "c5", "c4_hash", "c4_md5", "c2_crc"):
         log = os.path.join(src, f"bench_{c}.log")
         if os.path.exists(log):
             line = open(log).read().strip().split("\n")[-1]
