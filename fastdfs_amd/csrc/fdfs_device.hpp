@@ -16,6 +16,18 @@ struct DevTables {
     PolyMfmaTables pm;
 };
 
+// A value the code knows to be wave-uniform (a shuffle-max, say), moved to
+// SGPRs so that loops and branches on it are scalar.  Left in a VGPR, a loop
+// on it is exec-masked: each body is guarded by s_cbranch_execz, and a path
+// that skips the body skips its asm `s_waitcnt` too (tests/isa_check.py
+// vm_hazards counts such paths as loads still in flight).
+__device__ __forceinline__ uint64_t uniform64(uint64_t x)
+{
+    const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)x);
+    const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(x >> 32));
+    return (uint64_t)hi << 32 | lo;
+}
+
 // a ^ b ^ c in one VALU op (gfx950 v_bitop3_b32, truth table 0x96).
 __device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c)
 {
@@ -175,29 +187,6 @@ __device__ __forceinline__ uint32_t lane_fold_finish(const uint32_t *sD, uint32_
     for (int v = 0; v < 8; v++)
         a = chain16<SAR>(sD, a, make_uint4(ring[4 * v], ring[4 * v + 1], ring[4 * v + 2], ring[4 * v + 3]), K16);
     return a;
-}
-
-// chain16 in two halves (probe build, sig_hash_kernel MODE 3): the 16
-// lookups, then -- after other work has hidden their LDS latency -- the XOR
-// tree.
-__device__ __forceinline__ void chain16_issue(const uint32_t *__restrict__ D, uint32_t c, uint4 w,
-                                              uint32_t (&v)[16])
-{
-    const uint32_t x = c ^ w.x;
-    const uint32_t wd[4] = {x, w.y, w.z, w.w};
-#pragma unroll
-    for (int j = 0; j < 16; j++)
-        v[j] = D[j * 256 + ((wd[j >> 2] >> (8 * (j & 3))) & 0xFFu)];
-}
-
-template <bool SAR>
-__device__ __forceinline__ uint32_t chain16_finish(const uint32_t (&v)[16], uint32_t c, uint32_t K16)
-{
-    uint32_t r = xor3(xor3(v[0], v[1], v[2]), xor3(v[3], v[4], v[5]), xor3(v[6], v[7], v[8]));
-    r = xor3(r, xor3(v[9], v[10], v[11]), xor3(v[12], v[13], v[14])) ^ v[15];
-    if (SAR)
-        r ^= (uint32_t)((int32_t)c >> 31) & K16;
-    return r;
 }
 
 // Linear map given as 4 byte tables (LDS, [4][256]).
@@ -425,44 +414,10 @@ __device__ __forceinline__ void count_add(uint32_t (&cnt)[2], uint64_t nbytes)
     cnt[1] = (uint32_t)(c >> 32);
 }
 
-// Quad transpose of one dword position: lane j of a lane quad holds r_k =
-// dword of piece j of quad-file k; afterwards r_k = dword of piece k of its
-// own file j.  Two butterfly stages (lane xor 1, lane xor 2); each output is
-// one v_cndmask_b32 whose src0 is the partner lane's register read through
-// DPP quad_perm, with VCC = the lanes that keep their own value: 8 VALU per
-// 4 x 4 block.  The leading s_nop covers the VALU-write -> DPP-read hazard
-// for inputs written just before the block, the middle one the same hazard
-// between the stages (hipcc does not look inside an asm statement).
-__device__ __forceinline__ void quad_transpose(uint32_t &r0, uint32_t &r1, uint32_t &r2, uint32_t &r3)
-{
-    uint32_t o0, o1, o2, o3;
-#define QDPP(D, S0, S1, P) "v_cndmask_b32_dpp %[" D "], %[" S0 "], %[" S1 "], vcc quad_perm:" P " row_mask:0xf bank_mask:0xf\n\t"
-    asm volatile(
-        "s_nop 1\n\t"
-        "s_mov_b32 vcc_lo, 0x55555555\n\t"  // even lanes keep
-        "s_mov_b32 vcc_hi, 0x55555555\n\t"
-        QDPP("o0", "r1", "r0", "[1,0,3,2]") QDPP("o2", "r3", "r2", "[1,0,3,2]")
-        "s_mov_b32 vcc_lo, 0xaaaaaaaa\n\t"  // odd lanes keep
-        "s_mov_b32 vcc_hi, 0xaaaaaaaa\n\t"
-        QDPP("o1", "r0", "r1", "[1,0,3,2]") QDPP("o3", "r2", "r3", "[1,0,3,2]")
-        "s_mov_b32 vcc_lo, 0x33333333\n\t"  // lanes 0, 1 of the quad keep
-        "s_mov_b32 vcc_hi, 0x33333333\n\t"
-        "s_nop 1\n\t"
-        QDPP("r0", "o2", "o0", "[2,3,0,1]") QDPP("r1", "o3", "o1", "[2,3,0,1]")
-        "s_mov_b32 vcc_lo, 0xcccccccc\n\t"  // lanes 2, 3 keep
-        "s_mov_b32 vcc_hi, 0xcccccccc\n\t"
-        QDPP("r2", "o0", "o2", "[2,3,0,1]") QDPP("r3", "o1", "o3", "[2,3,0,1]")
-        : [r0] "+v"(r0), [r1] "+v"(r1), [r2] "+v"(r2), [r3] "+v"(r3), [o0] "=&v"(o0), [o1] "=&v"(o1),
-          [o2] "=&v"(o2), [o3] "=&v"(o3)
-        :
-        : "vcc");
-#undef QDPP
-}
-
-// Pair transpose of one quarter line (probe, sig_hash_kernel MODE 14): lane
+// Pair transpose of one quarter line (sig_hash_kernel, crc_lane_kernel): lane
 // j of a lane pair holds in r0 / r1 piece j of pair-file 0 / 1; afterwards
 // lane j holds pieces 0 and 1 of its own file, in r0 and t.  One stage (lane
-// xor 1): 8 VALU per two vectors instead of the quad form's 16.
+// xor 1): 8 VALU per two vectors (round 4: the quad form's two stages took 16).
 __device__ __forceinline__ void pair_transpose(uint32_t (&r0)[4], const uint32_t (&r1)[4], uint32_t (&t)[4])
 {
 #define PD(D, S0, S1) "v_cndmask_b32_dpp %[" D "], %[" S0 "], %[" S1 "], vcc quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf\n\t"

@@ -10,7 +10,10 @@
 // ubench_valu_rate2.txt), so the per-byte cost is counted in full-rate slots
 // and each hash is placed where it is cheapest:
 //
-//  * CRC32_ex: slice-by-16 byte tables in LDS (1 lookup per byte).
+//  * CRC32_ex: the lane fold over whole 128-byte steps (fdfs_device.hpp
+//    lane_fold_dw: a 32-register ring, 6-7 v_bitop3 per dword, no table
+//    lookups); slice-by-16 tables in LDS only for the lane-serial
+//    head and tail bytes and the fold's final 128 bytes.
 //  * ELFHash_ex: 4 VALU per byte (shift, SDWA byte add, shift, bitop3),
 //    one asm statement per word (fdfs_device.hpp elf_word4).
 //  * simple_hash_ex / Time33Hash_ex: over a 128-byte step each hash is

@@ -408,7 +408,7 @@ __global__ __launch_bounds__(128) void md5_pair_kernel(
             const uint64_t y = __shfl_xor(mx, o);
             mx = y > mx ? y : mx;
         }
-        const uint64_t rounds = (mx + BPR - 1) / BPR;
+        const uint64_t rounds = uniform64((mx + BPR - 1) / BPR);  // SGPRs: scalar round loops
         const uint8_t *tp = p + (nblk << 6);
         if (loader) {
             const bool small = L < big_min;  // else the CRC comes from crc_seg_kernel
@@ -430,9 +430,15 @@ __global__ __launch_bounds__(128) void md5_pair_kernel(
                     asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(R[k]) : "v"(a) : "memory");
                 }
             };
-            auto stage = [&](u32x4 (&R)[NLD], uint8_t *tile) {
+            // R is the older of the two sets in flight.  The wait is taken on
+            // every path through the loop body (only the staging is
+            // conditional), so no path reaches the next issue into R's
+            // registers with R's loads still in flight (tests/test_isa.py).
+            auto wait_older = [&](u32x4 (&R)[NLD]) {
                 asm volatile("s_waitcnt vmcnt(8)" : "+v"(R[0]), "+v"(R[1]), "+v"(R[2]), "+v"(R[3]) :: "memory");
                 asm volatile("" : "+v"(R[4]), "+v"(R[5]), "+v"(R[6]), "+v"(R[7]));
+            };
+            auto stage = [&](u32x4 (&R)[NLD], uint8_t *tile) {
 #pragma unroll
                 for (int k = 0; k < NLD; k++)
                     *reinterpret_cast<u32x4 *>(tile + (k * FPI + fsub) * STRIDE + piece * 16) = R[k];
@@ -469,20 +475,22 @@ __global__ __launch_bounds__(128) void md5_pair_kernel(
                 if ((r & 255) == 0)
                     prio_by_remaining(rounds - r);
                 issue(RB, r + 1);
+                wait_older(RA);
                 stage(RA, sbuf[0]);
                 pair_barrier();
                 crc_round(r, sbuf[0]);
                 issue(RA, r + 2);
+                wait_older(RB);
                 if (r + 1 < rounds) {
                     stage(RB, sbuf[1]);
                     pair_barrier();
                     crc_round(r + 1, sbuf[1]);
                 }
             }
+            // the last (past-the-end) set
             asm volatile("s_waitcnt vmcnt(0)"
                          : "+v"(RA[0]), "+v"(RA[1]), "+v"(RA[2]), "+v"(RA[3]), "+v"(RA[4]), "+v"(RA[5]),
-                           "+v"(RA[6]), "+v"(RA[7]), "+v"(RB[0]), "+v"(RB[1]), "+v"(RB[2]), "+v"(RB[3]),
-                           "+v"(RB[4]), "+v"(RB[5]), "+v"(RB[6]), "+v"(RB[7]) :: "memory");
+                           "+v"(RA[6]), "+v"(RA[7]) :: "memory");
             if (valid && small) {
                 if (nblk > 0) {
                     // the last 32 dwords in position order: an odd block
