@@ -318,17 +318,17 @@ def load_valu(config: str, avg_ms: float):
 
 
 def peer_bytes(ctx, sig, gidx, world):
-    """Bytes this rank sends to other ranks in one global dedup: its rows
-    for other owners (32 B each) and the answers it returns for theirs
-    (16 B each), from one bucket pass and a count exchange (untimed)."""
+    """Bytes this rank sends to other ranks in one global dedup (one untimed
+    call): (rows, answers).  libfdfs_gpu's exchange reports them itself
+    (fdfs_gpu_dedup_global_stats: the 32-byte rows for other owners, and the
+    16-byte answer records of multi-member classes it returns to their
+    senders); the torch form sends 32 B per row out and 16 B per row back."""
     if world == 1:
-        return 0.0
-    _, counts, _ = ctx.dedup_bucket(sig, gidx, world)
-    recv = torch.empty_like(counts)
-    dist.all_to_all_single(recv, counts)
-    me = dist.get_rank()
-    send, recv = counts.cpu().tolist(), recv.cpu().tolist()
-    return float(32 * (sum(send) - send[me]) + 16 * (sum(recv) - recv[me]))
+        return 0.0, 0.0
+    stats = {}
+    dedup_step(ctx, sig, gidx, world, stats=stats)
+    torch.cuda.synchronize()
+    return float(stats.get("row_bytes", 0)), float(stats.get("answer_bytes", 0))
 
 
 def dedup_strong(ctx, sig, gidx, world, steps, warmup):
@@ -341,7 +341,8 @@ def dedup_strong(ctx, sig, gidx, world, steps, warmup):
     dt = timed(lambda: dedup_step(ctx, sig, gidx, world), steps, warmup, world)
     kms, launches = ctx.read_timing(_lib.KERNEL_DEDUP)
     ctx.set_timing(False)
-    peer = sum_over_ranks(peer_bytes(ctx, sig, gidx, world), world)
+    rows, answers = peer_bytes(ctx, sig, gidx, world)
+    peer = {"rows": sum_over_ranks(rows, world), "answers": sum_over_ranks(answers, world)}
     return dt, kms / max(launches, 1), peer
 
 
@@ -594,8 +595,11 @@ def main():
                                  "scaling": "strong", "group_kernel_ms_avg": round(dms, 4),
                                  "workload": "config 5 (10% duplicates), bucket + RCCL all-to-all + group"}
             if world > 1:
-                res["dedup_100m"]["xgmi_bytes_per_step"] = round(peer)
-                res["dedup_100m"]["xgmi_gbs"] = round(peer / (ddt / st5) / 1e9, 1)
+                tot = peer["rows"] + peer["answers"]
+                res["dedup_100m"]["xgmi_bytes_per_step"] = round(tot)
+                res["dedup_100m"]["xgmi_row_bytes_per_step"] = round(peer["rows"])
+                res["dedup_100m"]["xgmi_answer_bytes_per_step"] = round(peer["answers"])
+                res["dedup_100m"]["xgmi_gbs"] = round(tot / (ddt / st5) / 1e9, 1)
             del sig5, gidx5
             torch.cuda.empty_cache()
             # the north star's large-file corpus (config 4: 8 x 1 GiB per
@@ -620,7 +624,10 @@ def main():
                                            else "fdfs_gpu_dedup (rep u64[n] + ref u32[n])") if world == 1
                                else "fdfs_gpu_dedup_global (rep u64[n] + ref u32[n])"}})
         if world > 1:  # all ranks' bytes to peers per step, over the step time
-            res["xgmi"] = {"bytes_per_step": round(peer), "gbs": round(peer / (dt / args.steps) / 1e9, 1),
+            tot = peer["rows"] + peer["answers"]
+            res["xgmi"] = {"bytes_per_step": round(tot), "row_bytes_per_step": round(peer["rows"]),
+                           "answer_bytes_per_step": round(peer["answers"]),
+                           "gbs": round(tot / (dt / args.steps) / 1e9, 1),
                            "links_peak_gbs": 7 * 153.0 * world}
         # algorithmic bytes per record: one GPU reads the 24-byte signature
         # and writes rep (8 B) + ref (4 B); N GPUs group the 32-byte exchange

@@ -62,6 +62,7 @@ EXPORTS = (
     "fdfs_gpu_dedup_packed",
     "fdfs_gpu_dedup_global",
     "fdfs_gpu_dedup_global_local",
+    "fdfs_gpu_dedup_global_stats",
     "fdfs_gpu_crc_batch_global",
     "fdfs_gpu_crc_batch_global_local",
     "fdfs_gpu_comm_unique_id",
@@ -193,6 +194,9 @@ def _bind(path: str) -> ctypes.CDLL:
     L.fdfs_gpu_dedup_global.argtypes = [vp, vp, vp, vp, u64, vp, vp, vp]
     L.fdfs_gpu_dedup_global_local.restype = i32
     L.fdfs_gpu_dedup_global_local.argtypes = [vp, i32, vp, vp, vp, vp, vp, vp]
+    if hasattr(L, "fdfs_gpu_dedup_global_stats"):  # (absent from A/B builds of round 5)
+        L.fdfs_gpu_dedup_global_stats.restype = i32
+        L.fdfs_gpu_dedup_global_stats.argtypes = [vp, vp, vp]
     L.fdfs_gpu_crc_batch_global.restype = i32
     L.fdfs_gpu_crc_batch_global.argtypes = [vp, vp, ctypes.POINTER(FdfsGpuBatch), vp, vp, vp, u64, vp, vp]
     L.fdfs_gpu_crc_batch_global_local.restype = i32

@@ -338,6 +338,16 @@ class Context:
             _stream_handle(stream)), "fdfs_gpu_dedup_global_local")
         return outs
 
+    def dedup_global_stats(self) -> dict:
+        """fdfs_gpu_dedup_global_stats: bytes the last dedup_global(_local)
+        call moved between ranks (this rank's sends; every virtual rank's for
+        _local): 32-byte rows to the other owners, 16-byte answer records
+        back."""
+        rb, ab = ctypes.c_uint64(), ctypes.c_uint64()
+        self._rc(self._L.fdfs_gpu_dedup_global_stats(self._h, ctypes.byref(rb), ctypes.byref(ab)),
+                 "fdfs_gpu_dedup_global_stats")
+        return {"row_bytes": rb.value, "answer_bytes": ab.value}
+
     # ------------------------------------------------- split-file CRC (N GPUs)
     @staticmethod
     def _check_pieces(data, offsets, sizes, piece_file, piece_start):

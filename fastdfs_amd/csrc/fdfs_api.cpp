@@ -55,6 +55,9 @@ struct fdfs_gpu_ctx {
     void *xa = nullptr, *xb = nullptr;
     size_t xa_bytes = 0, xb_bytes = 0;
     uint64_t *dann = nullptr, *hann = nullptr;
+    // bytes the last dedup_global(_local) call moved between ranks: rows,
+    // answers (fdfs_gpu_dedup_global_stats)
+    uint64_t x_row_bytes = 0, x_ans_bytes = 0;
 };
 
 namespace {
@@ -138,8 +141,13 @@ size_t dedup_ws_bytes(uint64_t n) { return fdfs::dedup_ws_bytes(n) + align_up(8 
 constexpr int kAnnTail = 3;
 constexpr size_t kAnnMax = 64 + kAnnTail;                   // words of one announcement
 constexpr size_t kErrRing = 64;  // lane_err_note's per-launch slots
-constexpr size_t kAnnDevWords = kAnnMax + 64 * kAnnMax + 8 + kErrRing;  // own, all ranks', agreement flag, ring
-constexpr size_t kAnnHostWords = 64 * kAnnTail + 64 * kAnnMax + 8 + kErrRing;  // tails, all ranks', flag, ring
+// fdfs_gpu_dedup_global's answer counts: every owner's sink-record count
+// per segment (64 x u32 per rank), all-gathered, at the end of both areas
+constexpr size_t kAnsAllWords = 64 * 64 / 2;
+constexpr size_t kAnnDevWords = kAnnMax + 64 * kAnnMax + 8 + kErrRing + kAnsAllWords;  // own, all ranks', flag, ring, counts
+constexpr size_t kAnnHostWords = 64 * kAnnTail + 64 * kAnnMax + 8 + kErrRing + kAnsAllWords;  // tails, all ranks', flag, ring, counts
+constexpr size_t kAnsAllDev = kAnnMax + 64 * kAnnMax + 8 + kErrRing;
+constexpr size_t kAnsAllHost = 64 * kAnnTail + 64 * kAnnMax + 8 + kErrRing;
 
 bool capturing(hipStream_t st)
 {
@@ -1227,10 +1235,16 @@ int fdfs_gpu_comm_destroy(void *comm)
 //    every rank's error, returned before any row moves, so no rank is left
 //    waiting in a send or receive;
 //  * the transport: one rank of an RCCL communicator (ncclAllGather, grouped
-//    ncclSend / ncclRecv, the rank's own segment by a device copy), or N
-//    virtual ranks in one process on one device (every segment a
-//    hipMemcpyAsync).
-// Bucket, group, answer pack and answer gather are the same kernels for both.
+//    ncclSend / ncclRecv), or N virtual ranks in one process on one device
+//    (every segment a hipMemcpyAsync).
+// Round 6: the bucket pass writes the rank's own rows
+// straight into the front of its owner-side buffer (no self copy over the
+// RCCL transport) and pre-fills every record's singleton answer; the owner
+// answers only the rows of multi-member classes, as 16-byte sink records
+// {sender row, ref, rep} per source segment (fdfs_dedup.hip DpSink), whose
+// counts one small all-gather tells every rank before the way back; the
+// sender applies them over its pre-filled answers.  Bucket, group, sink and
+// apply are the same kernels for both transports.
 
 extern "C++" {
 
@@ -1240,8 +1254,8 @@ struct DgPlan {
     uint64_t m[64];        // rows owner q groups
     int err = 0, err_rank = -1;
     bool grow = false;     // an owner's buffers must grow: the ranks agree on the outcome first
-    // where p's rows for owner q start among p's rows (and where q's answers
-    // for them land in p's answer buffer)
+    // where p's rows for owner q start among p's rows in send order (the
+    // sender row its answers name)
     uint64_t soff(int p, int q) const
     {
         uint64_t s = 0;
@@ -1249,24 +1263,52 @@ struct DgPlan {
             s += cnt[p][k];
         return s;
     }
-    // where p's rows start among owner q's received rows (and q's answers to p)
+    // where p's rows start among owner q's received rows: q's own rows
+    // first, then the other ranks' in rank order (fdfs::dg_seg_src; the
+    // device's sink_plan_kernel derives the same table)
     uint64_t roff(int q, int p) const
     {
-        uint64_t s = 0;
+        if (p == q)
+            return 0;
+        uint64_t s = cnt[q][q];
         for (int k = 0; k < p; k++)
-            s += cnt[k][q];
+            if (k != q)
+                s += cnt[k][q];
         return s;
     }
 };
 
+// Sink-record counts after the owners' groups: a[q][p] = records owner q
+// returns to rank p, from each owner's per-segment counters (all-gathered).
+struct DgAns {
+    uint64_t a[64][64];
+    void load(const uint32_t *all, int nranks)
+    {
+        for (int q = 0; q < nranks; q++)
+            for (int k = 0; k < nranks; k++)
+                a[q][fdfs::dg_seg_src((uint32_t)q, (uint32_t)k)] = all[(size_t)q * nranks + k];
+    }
+    // where owner q's records start in rank p's receive buffer (the other
+    // owners' records, in owner order)
+    uint64_t boff(int p, int q) const
+    {
+        uint64_t s = 0;
+        for (int k = 0; k < q; k++)
+            if (k != p)
+                s += a[k][p];
+        return s;
+    }
+    uint64_t recv_total(int p, int nranks) const { return boff(p, nranks); }
+};
+
 static size_t dg_a_bytes(uint64_t n)
 {
-    return align_up(32 * n) + align_up(8 * n) + align_up(16 * n) + align_up(8 * fdfs::bucket_ws_elems(n));
+    return align_up(32 * n) + align_up(4 * n) + align_up(16 * n) + align_up(8 * fdfs::bucket_ws_elems(n));
 }
 
 static size_t dg_b_bytes(uint64_t m)
 {
-    return align_up(32 * m) + align_up(16 * m);
+    return align_up(32 * m) + align_up(16 * m) + align_up(8 * fdfs::kSinkSegWords) + align_up(4 * 64);
 }
 
 // ann: nranks announcements of nranks + kAnnTail words, rank p's at p.
@@ -1299,30 +1341,6 @@ static void dg_plan(const uint64_t *ann, int nranks, DgPlan &pl)
     }
 }
 
-// Every segment of one exchange.  Forward: rows from rank p to owner q, p's
-// rows at soff(p, q) -> q's received rows at roff(q, p).  Back: the answers
-// from owner q to rank p, q's at roff(q, p) -> p's at soff(p, q).
-struct DgSeg {
-    int src, dst;
-    uint64_t soff, doff, count;  // elements
-};
-
-template <typename F>
-static int dg_segments(const DgPlan &pl, bool back, F &&f)
-{
-    for (int p = 0; p < pl.nranks; p++)
-        for (int q = 0; q < pl.nranks; q++) {
-            const uint64_t c = pl.cnt[p][q];
-            if (!c)
-                continue;
-            const uint64_t a = pl.soff(p, q), b = pl.roff(q, p);
-            const int rc = back ? f(DgSeg{q, p, b, a, c}) : f(DgSeg{p, q, a, b, c});
-            if (rc)
-                return rc;
-        }
-    return 0;
-}
-
 // One rank's side: its records and the buffers of both directions.
 struct DgSide {
     const uint8_t *sig = nullptr;
@@ -1330,21 +1348,23 @@ struct DgSide {
     uint64_t n = 0;
     uint64_t *rep_out = nullptr;
     uint32_t *ref_out = nullptr;
-    uint8_t *rows = nullptr;     // [n] 32-byte rows grouped by owner
-    uint64_t *row_of = nullptr;  // [n] row of each record
-    uint64_t *back = nullptr;    // [n] {rep, ref} answers, in row order
-    uint64_t *bws = nullptr;     // the bucket's tile counts and their scan (bucket_ws_elems)
-    uint64_t m = 0;              // rows this rank groups as owner
-    uint8_t *rows_in = nullptr;  // [m]
-    uint64_t *ans = nullptr;     // [m] {rep, ref} for the way back (the group's packed answers)
+    uint8_t *rows = nullptr;      // [n] 32-byte rows in send order, grouped by owner
+    uint32_t *rec_of = nullptr;   // [n] record of each send position
+    uint8_t *back = nullptr;      // [n] 16-byte sink records from the other owners
+    uint64_t *bws = nullptr;      // the bucket's tile counts and their scan (bucket_ws_elems)
+    uint64_t m = 0;               // rows this rank groups as owner
+    uint8_t *rows_in = nullptr;   // [m] received rows, own segment first (always at the buffer's start)
+    uint8_t *ans = nullptr;       // [m] sink records, segment k's from ans + 16 seg_start[k]
+    uint64_t *seg = nullptr;      // [kSinkSegWords] the segment table (launch_sink_plan)
+    uint32_t *cntr = nullptr;     // [64] sink records per segment
 };
 
 static void dg_carve_a(DgSide &s, void *mem)
 {
     Carve c{static_cast<char *>(mem)};
     s.rows = c.take<uint8_t>(32 * s.n);
-    s.row_of = c.take<uint64_t>(s.n);
-    s.back = c.take<uint64_t>(2 * s.n);
+    s.rec_of = c.take<uint32_t>(s.n);
+    s.back = c.take<uint8_t>(16 * s.n);
     s.bws = c.take<uint64_t>(fdfs::bucket_ws_elems(s.n));
 }
 
@@ -1353,7 +1373,9 @@ static void dg_carve_b(DgSide &s, void *mem, uint64_t m)
     Carve c{static_cast<char *>(mem)};
     s.m = m;
     s.rows_in = c.take<uint8_t>(32 * m);
-    s.ans = c.take<uint64_t>(2 * m);
+    s.ans = c.take<uint8_t>(16 * m);
+    s.seg = c.take<uint64_t>(fdfs::kSinkSegWords);
+    s.cntr = c.take<uint32_t>(64);
 }
 
 // Argument check of one rank's share (0 or EINVAL).
@@ -1374,12 +1396,18 @@ static int dg_check(const uint8_t *sig, const uint64_t *gidx, uint64_t n, const 
     return 0;
 }
 
-// Phase 1: rows by owner; the counts are the first nranks words of `ann`.
-static hipError_t dg_bucket(fdfs_gpu_ctx *ctx, DgSide &s, int nranks, uint64_t *ann, hipStream_t st)
+// Phase 1: rows by owner (the counts are the first nranks words of `ann`),
+// the record of each send position, every record's singleton answer; rank
+// `me`'s own rows to `self_rows` when given (the RCCL form: the front of its
+// owner-side buffer), else to their send slots (the local form copies them).
+static hipError_t dg_bucket(fdfs_gpu_ctx *ctx, DgSide &s, int nranks, int me, uint8_t *self_rows, uint64_t *ann,
+                            hipStream_t st)
 {
     hipEvent_t a, b;
     timing_pair(ctx, FDFS_KERNEL_BUCKET, a, b);
-    return fdfs::launch_dedup_bucket(s.sig, s.gidx, s.n, (uint32_t)nranks, s.rows, ann, s.bws, s.row_of, st, a, b);
+    const fdfs::BucketExtra x{(uint32_t)me, self_rows, s.rec_of, s.rep_out, s.ref_out};
+    return fdfs::launch_dedup_bucket(s.sig, s.gidx, s.n, (uint32_t)nranks, s.rows, ann, s.bws, nullptr, st, a, b,
+                                     &x);
 }
 
 // The announcement's tail {owner-side room, workspace room, errno}, staged
@@ -1393,67 +1421,56 @@ static hipError_t dg_announce(uint64_t *ann_tail, uint64_t *h, uint64_t b_room, 
     return hipMemcpyAsync(ann_tail, h, 8 * kAnnTail, hipMemcpyHostToDevice, st);
 }
 
-// Phase 3: the owner groups its rows (min gidx from the rows' own word 3),
-// its answers written packed, {rep, ref} per row, as the way back sends them.
-static hipError_t dg_group(fdfs_gpu_ctx *ctx, DgSide &s, hipStream_t st)
+// Phase 3: owner q's segment table from the announcements (`all`, w words
+// each), then its group of the received rows (min gidx from the rows' own
+// word 3) into sink records.
+static hipError_t dg_group(fdfs_gpu_ctx *ctx, DgSide &s, const uint64_t *all, size_t w, int nranks, int q,
+                           hipStream_t st)
 {
+    hipError_t e = fdfs::launch_sink_plan(all, (uint32_t)w, (uint32_t)nranks, (uint32_t)q, s.seg, s.cntr, st);
+    if (e != hipSuccess)
+        return e;
     hipEvent_t a, b;
     timing_pair(ctx, FDFS_KERNEL_DEDUP, a, b);
+    const fdfs::DedupSink xs{s.ans, s.cntr, s.seg, (uint32_t)nranks};
     return fdfs::launch_dedup_group(s.rows_in, 32, reinterpret_cast<const uint64_t *>(s.rows_in + 24), 4, s.m,
-                                    ctx->ws, s.ans, nullptr, true, st, a, b);
+                                    ctx->ws, nullptr, nullptr, true, st, a, b, &xs);
 }
 
-// Phase 5: the answers into record order.
-static hipError_t dg_gather(DgSide &s, hipStream_t st)
+// Phase 5: the sink records over the pre-filled answers: the rank's own
+// owner's (segment 0 of its owner side, counted on the device) and `nb`
+// received from the other owners.
+static hipError_t dg_apply(DgSide &s, uint64_t self_rows, uint64_t nb, hipStream_t st)
 {
-    return fdfs::launch_answer_gather(s.back, s.row_of, s.n, s.rep_out, s.ref_out, st);
+    return fdfs::launch_answer_apply(s.ans, s.cntr, self_rows, s.back, nb, s.rec_of, s.rep_out, s.ref_out, st);
 }
 
-// RCCL transport of one exchange for rank `me`: its own segment by a device
-// copy, the others by one group of sends and receives.
-static int dg_nccl_exchange(fdfs_gpu_ctx *ctx, ncclComm_t c, int me, const DgPlan &pl, bool back, const void *sbuf,
-                            void *rbuf, size_t elem, hipStream_t st)
+// One point-to-point move of an exchange.
+struct DgMove {
+    int peer;
+    char *ptr;  // send: source, receive: destination
+    size_t bytes;
+};
+
+// RCCL transport of one exchange: one group of sends and receives.
+static int dg_nccl_group(fdfs_gpu_ctx *ctx, ncclComm_t c, const std::vector<DgMove> &sends,
+                         const std::vector<DgMove> &recvs, hipStream_t st)
 {
-    const char *sb = static_cast<const char *>(sbuf);
-    char *rb = static_cast<char *>(rbuf);
-    hipError_t e = hipSuccess;
-    int rc = dg_segments(pl, back, [&](const DgSeg &g) -> int {
-        if (g.src != me || g.dst != me)
-            return 0;
-        e = hipMemcpyAsync(rb + g.doff * elem, sb + g.soff * elem, g.count * elem, hipMemcpyDeviceToDevice, st);
-        return e == hipSuccess ? 0 : EIO;
-    });
-    if (rc)
-        return fail(ctx, e, "exchange self copy");
-    if (pl.nranks == 1)
+    if (sends.empty() && recvs.empty())
         return 0;
     ncclResult_t r = ncclGroupStart();
     if (r != ncclSuccess)
         return nccl_fail(ctx, r, "ncclGroupStart");
-    rc = dg_segments(pl, back, [&](const DgSeg &g) -> int {
-        if (g.src == me && g.dst != me)
-            r = ncclSend(sb + g.soff * elem, g.count * elem, ncclUint8, g.dst, c, st);
-        else if (g.dst == me && g.src != me)
-            r = ncclRecv(rb + g.doff * elem, g.count * elem, ncclUint8, g.src, c, st);
-        return r == ncclSuccess ? 0 : EIO;
-    });
+    for (const DgMove &g : sends)
+        if (r == ncclSuccess)
+            r = ncclSend(g.ptr, g.bytes, ncclUint8, g.peer, c, st);
+    for (const DgMove &g : recvs)
+        if (r == ncclSuccess)
+            r = ncclRecv(g.ptr, g.bytes, ncclUint8, g.peer, c, st);
     const ncclResult_t r2 = ncclGroupEnd();
-    if (rc || r2 != ncclSuccess)
+    if (r != ncclSuccess || r2 != ncclSuccess)
         return nccl_fail(ctx, r != ncclSuccess ? r : r2, "exchange");
     return 0;
-}
-
-// In-process transport: every rank's buffers are on this device.
-static int dg_local_exchange(fdfs_gpu_ctx *ctx, const DgPlan &pl, bool back, const std::vector<const char *> &sbuf,
-                             const std::vector<char *> &rbuf, size_t elem, hipStream_t st)
-{
-    hipError_t e = hipSuccess;
-    const int rc = dg_segments(pl, back, [&](const DgSeg &g) -> int {
-        e = hipMemcpyAsync(rbuf[g.dst] + g.doff * elem, sbuf[g.src] + g.soff * elem, g.count * elem,
-                           hipMemcpyDeviceToDevice, st);
-        return e == hipSuccess ? 0 : EIO;
-    });
-    return rc ? fail(ctx, e, "local exchange copy") : 0;
 }
 
 static int dg_plan_error(fdfs_gpu_ctx *ctx, const DgPlan &pl, int me)
@@ -1463,6 +1480,33 @@ static int dg_plan_error(fdfs_gpu_ctx *ctx, const DgPlan &pl, int me)
                       pl.err == EINVAL ? "invalid arguments or over 2^32-2 rows for one owner"
                                        : pl.err == ENOMEM ? "out of memory" : "HIP error");
     return pl.err;
+}
+
+// Grow the owner-side buffer keeping its first `keep` bytes (the own rows the
+// bucket pass wrote there).
+static int grow_keep(fdfs_gpu_ctx *ctx, void **buf, size_t *have, size_t bytes, size_t keep, hipStream_t st)
+{
+    if (bytes <= *have)
+        return 0;
+    void *nb = nullptr;
+    const size_t sz = bytes + bytes / 4;
+    hipError_t e = hipMalloc(&nb, sz);
+    if (e != hipSuccess) {
+        std::snprintf(ctx->err, sizeof(ctx->err), "hipMalloc(%zu): %s", sz, hipGetErrorString(e));
+        return ENOMEM;
+    }
+    if (keep && (e = hipMemcpyAsync(nb, *buf, keep, hipMemcpyDeviceToDevice, st)) != hipSuccess) {
+        (void)hipFree(nb);
+        return fail(ctx, e, "exchange buffer growth copy");
+    }
+    if ((e = hipStreamSynchronize(st)) != hipSuccess) {
+        (void)hipFree(nb);
+        return fail(ctx, e, "exchange buffer growth sync");
+    }
+    (void)hipFree(*buf);
+    *buf = nb;
+    *have = sz;
+    return 0;
 }
 
 }  // extern "C++"
@@ -1493,13 +1537,19 @@ int fdfs_gpu_dedup_global(fdfs_gpu_ctx *ctx, void *comm, const uint8_t *sig, con
         std::snprintf(ctx->err, sizeof(ctx->err), "dedup_global synchronises; not capturable");
         return EINVAL;
     }
+    ctx->x_row_bytes = ctx->x_ans_bytes = 0;
     int err = dg_check(sig, gidx, n, rep_out, ref_out, nranks);
     if (!err)
         err = ensure_buf(ctx, &ctx->xa, &ctx->xa_bytes, dg_a_bytes(n), st);
+    // room for the own rows the bucket pass writes in place (<= n of them)
+    if (!err)
+        err = ensure_buf(ctx, &ctx->xb, &ctx->xb_bytes, dg_b_bytes(n), st);
     WsScope wsc(ctx, st);
     const size_t w = (size_t)nranks + kAnnTail;
     uint64_t *ann = ctx->dann, *all = ctx->dann + kAnnMax, *dflag = ctx->dann + kAnnMax + 64 * kAnnMax;
     uint64_t *htail = ctx->hann, *hall = ctx->hann + 64 * kAnnTail, *hflag = hall + 64 * kAnnMax;
+    uint32_t *dans = reinterpret_cast<uint32_t *>(ctx->dann + kAnsAllDev);
+    uint32_t *hans = reinterpret_cast<uint32_t *>(ctx->hann + kAnsAllHost);
     DgSide s;
     s.sig = sig;
     s.gidx = gidx;
@@ -1509,15 +1559,15 @@ int fdfs_gpu_dedup_global(fdfs_gpu_ctx *ctx, void *comm, const uint8_t *sig, con
     hipError_t e;
     if (!err) {
         dg_carve_a(s, ctx->xa);
-        if ((e = dg_bucket(ctx, s, nranks, ann, st)) != hipSuccess)
+        if ((e = dg_bucket(ctx, s, nranks, me, static_cast<uint8_t *>(ctx->xb), ann, st)) != hipSuccess)
             err = fail(ctx, e, "dedup_global bucket");
     }
     if (err && (e = fdfs::launch_zero_u32(ann, 2ull * nranks, st)) != hipSuccess)
         return fail(ctx, e, "dedup_global announce");  // the device is gone; so is the exchange
     if ((e = dg_announce(ann + nranks, htail, ctx->xb_bytes, ctx->ws_bytes, err, st)) != hipSuccess)
         return fail(ctx, e, "dedup_global announce");
-    // 1. every rank's announcement to every rank, then to the host: the one
-    //    host synchronisation (the row exchange is sized by it)
+    // 1. every rank's announcement to every rank, then to the host (the row
+    //    exchange is sized by it)
     ncclResult_t r = ncclAllGather(ann, all, w, ncclUint64, c, st);
     if (r != ncclSuccess)
         return nccl_fail(ctx, r, "ncclAllGather announcements");
@@ -1529,9 +1579,10 @@ int fdfs_gpu_dedup_global(fdfs_gpu_ctx *ctx, void *comm, const uint8_t *sig, con
     if (pl.err)
         return dg_plan_error(ctx, pl, me);
     if (pl.grow) {
-        // some owner must grow its buffers: each grows its own, and the ranks
-        // agree on the outcome (max over ranks) before any row moves
-        int gerr = ensure_buf(ctx, &ctx->xb, &ctx->xb_bytes, dg_b_bytes(pl.m[me]), st);
+        // some owner must grow its buffers: each grows its own (keeping the
+        // own rows at the front), and the ranks agree on the outcome (max over
+        // ranks) before any row moves
+        int gerr = grow_keep(ctx, &ctx->xb, &ctx->xb_bytes, dg_b_bytes(pl.m[me]), 32 * pl.cnt[me][me], st);
         if (!gerr)
             gerr = ensure_ws(ctx, dedup_ws_bytes(pl.m[me]), st);
         hflag[0] = (uint64_t)gerr;
@@ -1549,16 +1600,55 @@ int fdfs_gpu_dedup_global(fdfs_gpu_ctx *ctx, void *comm, const uint8_t *sig, con
         }
     }
     dg_carve_b(s, ctx->xb, pl.m[me]);
+    // 2. rows to their owners over xGMI (the own rows are already in place)
+    std::vector<DgMove> sends, recvs;
+    for (int q = 0; q < nranks; q++)
+        if (q != me && pl.cnt[me][q]) {
+            sends.push_back({q, reinterpret_cast<char *>(s.rows) + 32 * pl.soff(me, q), 32 * pl.cnt[me][q]});
+            ctx->x_row_bytes += 32 * pl.cnt[me][q];
+        }
+    for (int p = 0; p < nranks; p++)
+        if (p != me && pl.cnt[p][me])
+            recvs.push_back({p, reinterpret_cast<char *>(s.rows_in) + 32 * pl.roff(me, p), 32 * pl.cnt[p][me]});
     int rc;
-    // 2. rows to their owners over xGMI, 3. group, 4. answers back, 5. gather
-    if ((rc = dg_nccl_exchange(ctx, c, me, pl, false, s.rows, s.rows_in, 32, st)))
+    if ((rc = dg_nccl_group(ctx, c, sends, recvs, st)))
         return rc;
-    if ((e = dg_group(ctx, s, st)) != hipSuccess)
+    // 3. the owner's group: sink records for the rows of multi-member classes
+    if ((e = dg_group(ctx, s, all, w, nranks, me, st)) != hipSuccess)
         return fail(ctx, e, "dedup_global group");
-    if ((rc = dg_nccl_exchange(ctx, c, me, pl, true, s.ans, s.back, 16, st)))
-        return rc;
-    e = dg_gather(s, st);
-    return e == hipSuccess ? 0 : fail(ctx, e, "dedup_global gather");
+    uint64_t nb = 0;
+    if (nranks > 1) {
+        // 4. every owner's record count per segment to every rank (the way
+        //    back is sized by it), then the records to their senders
+        if ((r = ncclAllGather(s.cntr, dans, (size_t)nranks, ncclUint32, c, st)) != ncclSuccess)
+            return nccl_fail(ctx, r, "ncclAllGather answer counts");
+        if ((e = hipMemcpyAsync(hans, dans, 4 * (size_t)nranks * nranks, hipMemcpyDeviceToHost, st)) != hipSuccess ||
+            (e = hipStreamSynchronize(st)) != hipSuccess)
+            return fail(ctx, e, "dedup_global answer counts");
+        DgAns *an = new (std::nothrow) DgAns;
+        if (!an) {
+            std::snprintf(ctx->err, sizeof(ctx->err), "dedup_global: host allocation");
+            return EIO;  // the other ranks are past the point of a common error
+        }
+        an->load(hans, nranks);
+        sends.clear();
+        recvs.clear();
+        for (int p = 0; p < nranks; p++)
+            if (p != me && an->a[me][p]) {
+                sends.push_back({p, reinterpret_cast<char *>(s.ans) + 16 * pl.roff(me, p), 16 * an->a[me][p]});
+                ctx->x_ans_bytes += 16 * an->a[me][p];
+            }
+        for (int q = 0; q < nranks; q++)
+            if (q != me && an->a[q][me])
+                recvs.push_back({q, reinterpret_cast<char *>(s.back) + 16 * an->boff(me, q), 16 * an->a[q][me]});
+        nb = an->recv_total(me, nranks);
+        delete an;
+        if ((rc = dg_nccl_group(ctx, c, sends, recvs, st)))
+            return rc;
+    }
+    // 5. the records over the pre-filled singleton answers
+    e = dg_apply(s, pl.cnt[me][me], nb, st);
+    return e == hipSuccess ? 0 : fail(ctx, e, "dedup_global apply");
 }
 
 int fdfs_gpu_dedup_global_local(fdfs_gpu_ctx *ctx, int nranks, const uint8_t *const *sig,
@@ -1579,10 +1669,12 @@ int fdfs_gpu_dedup_global_local(fdfs_gpu_ctx *ctx, int nranks, const uint8_t *co
         std::snprintf(ctx->err, sizeof(ctx->err), "dedup_global_local synchronises; not capturable");
         return EINVAL;
     }
+    ctx->x_row_bytes = ctx->x_ans_bytes = 0;
     WsScope wsc(ctx, st);
     const size_t w = (size_t)nranks + kAnnTail;
     uint64_t *all = ctx->dann + kAnnMax;
     uint64_t *htail = ctx->hann, *hall = ctx->hann + 64 * kAnnTail;
+    uint32_t *hans = reinterpret_cast<uint32_t *>(ctx->hann + kAnsAllHost);
     std::vector<DgSide> s(nranks);
     size_t abytes = 0;
     for (int p = 0; p < nranks; p++)
@@ -1594,7 +1686,10 @@ int fdfs_gpu_dedup_global_local(fdfs_gpu_ctx *ctx, int nranks, const uint8_t *co
         return ENOMEM;
     }
     int rc = 0;
-    DgPlan pl;
+    DgPlan *pl = new (std::nothrow) DgPlan;
+    DgAns *an = new (std::nothrow) DgAns;
+    if (!pl || !an)
+        rc = ENOMEM;
     size_t done = 0;
     for (int p = 0; p < nranks && !rc; p++) {
         s[p].sig = sig[p];
@@ -1604,9 +1699,10 @@ int fdfs_gpu_dedup_global_local(fdfs_gpu_ctx *ctx, int nranks, const uint8_t *co
         s[p].ref_out = ref_out[p];
         dg_carve_a(s[p], static_cast<char *>(amem) + done);
         done += dg_a_bytes(n[p]);
-        // 1. every virtual rank's bucket and announcement (no owner-side
-        //    buffers yet: room 0, so the plan always grows them below)
-        if ((e = dg_bucket(ctx, s[p], nranks, all + p * w, st)) != hipSuccess ||
+        // 1. every virtual rank's bucket (its own rows to their send slots:
+        //    this transport copies every segment) and announcement (no
+        //    owner-side buffers yet: room 0, so the plan always grows them)
+        if ((e = dg_bucket(ctx, s[p], nranks, p, nullptr, all + p * w, st)) != hipSuccess ||
             (e = dg_announce(all + p * w + nranks, htail + kAnnTail * p, 0, ctx->ws_bytes, 0, st)) != hipSuccess)
             rc = fail(ctx, e, "dedup_global_local bucket");
     }
@@ -1614,13 +1710,13 @@ int fdfs_gpu_dedup_global_local(fdfs_gpu_ctx *ctx, int nranks, const uint8_t *co
                 (e = hipStreamSynchronize(st)) != hipSuccess))
         rc = fail(ctx, e, "dedup_global_local announcements");
     if (!rc) {
-        dg_plan(hall, nranks, pl);
-        rc = pl.err ? dg_plan_error(ctx, pl, -1) : 0;
+        dg_plan(hall, nranks, *pl);
+        rc = pl->err ? dg_plan_error(ctx, *pl, -1) : 0;
     }
     size_t bbytes = 0, wsb = 0;
     for (int q = 0; q < nranks && !rc; q++) {
-        bbytes += dg_b_bytes(pl.m[q]);
-        wsb = std::max(wsb, dedup_ws_bytes(pl.m[q]));
+        bbytes += dg_b_bytes(pl->m[q]);
+        wsb = std::max(wsb, dedup_ws_bytes(pl->m[q]));
     }
     if (!rc && (e = hipMalloc(&bmem, bbytes)) != hipSuccess) {
         std::snprintf(ctx->err, sizeof(ctx->err), "hipMalloc(%zu): %s", bbytes, hipGetErrorString(e));
@@ -1629,28 +1725,46 @@ int fdfs_gpu_dedup_global_local(fdfs_gpu_ctx *ctx, int nranks, const uint8_t *co
     if (!rc)
         rc = ensure_ws(ctx, wsb, st);
     if (!rc) {
-        std::vector<const char *> rows(nranks), ans(nranks);
-        std::vector<char *> rows_in(nranks), back(nranks);
         done = 0;
         for (int q = 0; q < nranks; q++) {
-            dg_carve_b(s[q], static_cast<char *>(bmem) + done, pl.m[q]);
-            done += dg_b_bytes(pl.m[q]);
-            rows[q] = reinterpret_cast<const char *>(s[q].rows);
-            rows_in[q] = reinterpret_cast<char *>(s[q].rows_in);
-            ans[q] = reinterpret_cast<const char *>(s[q].ans);
-            back[q] = reinterpret_cast<char *>(s[q].back);
+            dg_carve_b(s[q], static_cast<char *>(bmem) + done, pl->m[q]);
+            done += dg_b_bytes(pl->m[q]);
         }
-        // 2. rows to their owners, 3. each owner's group (one workspace,
-        //    stream-ordered), 4. answers back, 5. gathers
-        rc = dg_local_exchange(ctx, pl, false, rows, rows_in, 32, st);
-        for (int q = 0; q < nranks && !rc; q++)
-            if ((e = dg_group(ctx, s[q], st)) != hipSuccess)
-                rc = fail(ctx, e, "dedup_global_local group");
-        if (!rc)
-            rc = dg_local_exchange(ctx, pl, true, ans, back, 16, st);
+        // 2. rows to their owners (every segment a device copy), 3. each
+        //    owner's group (one workspace, stream-ordered)
         for (int p = 0; p < nranks && !rc; p++)
-            if ((e = dg_gather(s[p], st)) != hipSuccess)
-                rc = fail(ctx, e, "dedup_global_local gather");
+            for (int q = 0; q < nranks && !rc; q++)
+                if (pl->cnt[p][q]) {
+                    if ((e = hipMemcpyAsync(s[q].rows_in + 32 * pl->roff(q, p), s[p].rows + 32 * pl->soff(p, q),
+                                            32 * pl->cnt[p][q], hipMemcpyDeviceToDevice, st)) != hipSuccess)
+                        rc = fail(ctx, e, "dedup_global_local row copy");
+                    if (p != q)
+                        ctx->x_row_bytes += 32 * pl->cnt[p][q];
+                }
+        for (int q = 0; q < nranks && !rc; q++)
+            if ((e = dg_group(ctx, s[q], all, w, nranks, q, st)) != hipSuccess)
+                rc = fail(ctx, e, "dedup_global_local group");
+        // 4. the owners' record counts, then the records back to the senders
+        for (int q = 0; q < nranks && !rc; q++)
+            if ((e = hipMemcpyAsync(hans + (size_t)q * nranks, s[q].cntr, 4 * (size_t)nranks,
+                                    hipMemcpyDeviceToHost, st)) != hipSuccess)
+                rc = fail(ctx, e, "dedup_global_local answer counts");
+        if (!rc && (e = hipStreamSynchronize(st)) != hipSuccess)
+            rc = fail(ctx, e, "dedup_global_local answer counts");
+        if (!rc)
+            an->load(hans, nranks);
+        for (int q = 0; q < nranks && !rc; q++)
+            for (int p = 0; p < nranks && !rc; p++)
+                if (p != q && an->a[q][p]) {
+                    if ((e = hipMemcpyAsync(s[p].back + 16 * an->boff(p, q), s[q].ans + 16 * pl->roff(q, p),
+                                            16 * an->a[q][p], hipMemcpyDeviceToDevice, st)) != hipSuccess)
+                        rc = fail(ctx, e, "dedup_global_local answer copy");
+                    ctx->x_ans_bytes += 16 * an->a[q][p];
+                }
+        // 5. every rank's records over its pre-filled answers
+        for (int p = 0; p < nranks && !rc; p++)
+            if ((e = dg_apply(s[p], pl->cnt[p][p], an->recv_total(p, nranks), st)) != hipSuccess)
+                rc = fail(ctx, e, "dedup_global_local apply");
     }
     // the buffers are freed only once the stream is done with them
     e = hipStreamSynchronize(st);
@@ -1659,7 +1773,19 @@ int fdfs_gpu_dedup_global_local(fdfs_gpu_ctx *ctx, int nranks, const uint8_t *co
     (void)hipFree(amem);
     if (bmem)
         (void)hipFree(bmem);
+    delete pl;
+    delete an;
     return rc;
+}
+
+int fdfs_gpu_dedup_global_stats(fdfs_gpu_ctx *ctx, uint64_t *row_bytes, uint64_t *answer_bytes)
+{
+    if (!ctx || !row_bytes || !answer_bytes)
+        return EINVAL;
+    std::lock_guard<std::recursive_mutex> lk(ctx->mu);
+    *row_bytes = ctx->x_row_bytes;
+    *answer_bytes = ctx->x_ans_bytes;
+    return 0;
 }
 
 // ---- split-file CRC over N GPUs -------------------------------

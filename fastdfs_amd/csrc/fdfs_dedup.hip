@@ -282,9 +282,40 @@ struct DpOut {
     }
 };
 
+// The owner side of fdfs_gpu_dedup_global (round 6): only the records of
+// multi-member classes are answered, as 16-byte records {sender row, ref,
+// rep lo, rep hi} appended per segment of the owner's rows (one segment per
+// sending rank, seg_start[k] .. seg_start[k + 1]; the sender pre-filled
+// every record's singleton answer in its bucket pass).  With the bench's 10 %
+// duplicates ~20 % of the rows are answered, so the way back carries ~0.2x
+// the bytes of an answer per row.  Segment k's records go to ans[seg_start[k]
+// + slot] (room for every row of the segment), slot from cntr[k]: one
+// device-scope atomic per (workgroup, segment) after an LDS count.
+struct DpSink {
+    uint4 *ans;              // null: answers go to DpOut (the one-GPU forms)
+    uint32_t *cntr;          // [nseg] records appended per segment
+    const uint64_t *seg;     // seg_start[0 .. nseg], then seg_soff[0 .. nseg - 1] at seg + kSinkSoff
+    uint32_t nseg;
+    // the segment holding owner row `row` (nseg <= 64: a uniform scan)
+    __device__ __forceinline__ uint32_t seg_of(uint64_t row) const
+    {
+        uint32_t s = 0;
+        for (uint32_t k = 1; k < nseg; k++)
+            s += row >= seg[k] ? 1u : 0u;
+        return s;
+    }
+    __device__ __forceinline__ void put(uint32_t s, uint32_t slot, uint64_t row, uint64_t rep, uint32_t ref) const
+    {
+        const uint32_t src = (uint32_t)(seg[kSinkSoff + s] + (row - seg[s]));  // the sender's row
+        ans[seg[s] + slot] = make_uint4(src, ref, (uint32_t)rep, (uint32_t)(rep >> 32));
+    }
+};
+
 // K1: keys, the singleton answer (rep = own gidx, ref = 1) of every record,
 // and the tile's entries sorted by digit (top d1 bits; unstable: order inside
-// a partition does not matter) written back as one contiguous run.
+// a partition does not matter) written back as one contiguous run.  With a
+// DpSink (out.rep null) no singleton answer is written here: the senders
+// wrote them.
 __global__ __launch_bounds__(kDpTileThreads) void dp_tile_kernel(
     const uint8_t *__restrict__ sig, uint32_t stride, const uint64_t *__restrict__ gidx,
     uint32_t gstride, uint64_t n, int d1, uint64_t tiles, uint64_t *__restrict__ ent1,
@@ -313,7 +344,8 @@ __global__ __launch_bounds__(kDpTileThreads) void dp_tile_kernel(
             // every record starts as its own class; dp_group overwrites the
             // records of classes with more than one member (writing these
             // from dp_split instead measured neutral)
-            out.store(r, gstride ? gidx[r * gstride] : r, 1u, true);
+            if (out.rep)
+                out.store(r, gstride ? gidx[r * gstride] : r, 1u, true);
         }
     }
 #pragma unroll
@@ -688,6 +720,7 @@ struct DpArgs {
     uint64_t *gword, *gmin;
     uint32_t *gcnt, *gslot;
     DpOut out;
+    DpSink sink;
 };
 
 // The gather's run table lives in the LDS table region (dead before the
@@ -795,6 +828,48 @@ __device__ __forceinline__ void dp_group_lds(DpLds<GM> &L, const DpArgs &A, cons
         L.jl[j] = l | own << 16;  // its class (itself if it claimed a slot)
     }
     __syncthreads();
+    if (A.sink.ans) {
+        // (3') exchange owner: the records of multi-member classes as sink
+        // records, counted per segment in LDS (the table's words are dead
+        // now), one device-scope atomic per segment this workgroup answers,
+        // then placed
+        uint32_t *lc = L.word, *lbase = L.word + 64;
+        auto each = [&](auto &&f) {
+#pragma unroll
+            for (int k = 0; k < kDpEpt; k++) {
+                const uint32_t l = threadIdx.x + k * NT;
+                if ((claim >> k) & 1u) {
+                    const uint32_t c = dp_cn(L.cn, l);
+                    if (c > 1)
+                        f(rc[k], (uint64_t)L.mn[l], c);
+                }
+            }
+            for (uint32_t j = threadIdx.x; j < nj; j += NT) {
+                const uint32_t e = L.jl[j];
+                const uint32_t own = e >> 16;
+                const uint32_t c = dp_cn(L.cn, own);
+                if (c > 1)
+                    f(L.rec[e & 0xFFFFu], (uint64_t)L.mn[own], c);
+            }
+        };
+        if (threadIdx.x < 64)
+            lc[threadIdx.x] = 0;
+        __syncthreads();
+        each([&](uint32_t r, uint64_t, uint32_t) { atomicAdd(&lc[A.sink.seg_of(r)], 1u); });
+        __syncthreads();
+        if (threadIdx.x < 64) {
+            const uint32_t cnt = lc[threadIdx.x];
+            lbase[threadIdx.x] = cnt ? atomicAdd(&A.sink.cntr[threadIdx.x], cnt) : 0u;
+            lc[threadIdx.x] = 0;
+        }
+        __syncthreads();
+        each([&](uint32_t r, uint64_t m, uint32_t c) {
+            const uint32_t s = A.sink.seg_of(r);
+            A.sink.put(s, lbase[s] + atomicAdd(&lc[s], 1u), r, m, c);
+        });
+        __syncthreads();
+        return;
+    }
     // (3) answers of the records of multi-member classes
 #pragma unroll
     for (int k = 0; k < kDpEpt; k++) {
@@ -911,7 +986,12 @@ __device__ __forceinline__ void dp_group_slow(DpLds<GM> &L, const DpArgs &A, con
             const uint32_t slot = A.gslot[vs + l];
             if (c[slot] > 1) {
                 const uint32_t r = (uint32_t)A.ent2[dp_src(l, nk, T.rpos, T.rsrc)];
-                A.out.store(r, m[slot], c[slot], true);
+                if (A.sink.ans) {  // rare path: one device-scope atomic per record
+                    const uint32_t s = A.sink.seg_of(r);
+                    A.sink.put(s, atomicAdd(&A.sink.cntr[s], 1u), r, m[slot], c[slot]);
+                } else {
+                    A.out.store(r, m[slot], c[slot], true);
+                }
             }
         }
         __syncthreads();
@@ -941,7 +1021,7 @@ template <int GM>
 __global__ __launch_bounds__(kDpGroupThreads) __attribute__((amdgpu_waves_per_eu(GM == GM_INDEX ? 8 : 6))) void dp_group_kernel(
     const uint64_t *__restrict__ ent2, int d2, uint64_t tiles, const uint64_t *__restrict__ off1,
     const uint32_t *__restrict__ cb, const uint16_t *__restrict__ cdo, const uint8_t *__restrict__ sig,
-    uint32_t stride, DpOut out, uint32_t *__restrict__ slow)
+    uint32_t stride, DpOut out, DpSink sink, uint32_t *__restrict__ slow)
 {
     __shared__ DpLds<GM> L;
     const DpRunTab T(L);
@@ -969,7 +1049,7 @@ __global__ __launch_bounds__(kDpGroupThreads) __attribute__((amdgpu_waves_per_eu
         dp_split_entry(ent2[dp_src(l < cnt ? l : cnt - 1, R.nch, T.rpos, T.rsrc)], kh[k], rc[k]);
     }
     __syncthreads();  // run table reads done before the table init
-    const DpArgs A{ent2, sig, stride, GM, nullptr, nullptr, nullptr, nullptr, out};
+    const DpArgs A{ent2, sig, stride, GM, nullptr, nullptr, nullptr, nullptr, out, sink};
     dp_group_lds<GM>(L, A, kh, rc, cnt);
 }
 
@@ -979,10 +1059,11 @@ __global__ __launch_bounds__(kDpGroupThreads) void dp_group_slow_kernel(
     const uint64_t *__restrict__ ent2, int d2, uint64_t tiles, const uint64_t *__restrict__ off1,
     const uint32_t *__restrict__ cb, const uint16_t *__restrict__ cdo, const uint8_t *__restrict__ sig,
     uint32_t stride, uint64_t *__restrict__ gword, uint64_t *__restrict__ gmin,
-    uint32_t *__restrict__ gcnt, uint32_t *__restrict__ gslot, DpOut out, const uint32_t *__restrict__ slow)
+    uint32_t *__restrict__ gcnt, uint32_t *__restrict__ gslot, DpOut out, DpSink sink,
+    const uint32_t *__restrict__ slow)
 {
     __shared__ DpLds<GM> L;
-    const DpArgs A{ent2, sig, stride, GM, gword, gmin, gcnt, gslot, out};
+    const DpArgs A{ent2, sig, stride, GM, gword, gmin, gcnt, gslot, out, sink};
     const uint32_t ns = slow[0];
     for (uint32_t i = blockIdx.x; i < ns; i += gridDim.x) {
         DpRuns R;
@@ -1015,7 +1096,8 @@ static unsigned grid_for(uint64_t n, unsigned block)
 
 hipError_t launch_dedup_group(const uint8_t *sig, uint32_t sig_stride, const uint64_t *gidx,
                               uint32_t gidx_stride, uint64_t n, void *ws, uint64_t *rep_out,
-                              uint32_t *ref_out, bool packed, hipStream_t st, hipEvent_t ev0, hipEvent_t ev1)
+                              uint32_t *ref_out, bool packed, hipStream_t st, hipEvent_t ev0, hipEvent_t ev1,
+                              const DedupSink *xs)
 {
     if (n == 0)
         return hipSuccess;
@@ -1042,7 +1124,12 @@ hipError_t launch_dedup_group(const uint8_t *sig, uint32_t sig_stride, const uin
     uint32_t *gcnt = reinterpret_cast<uint32_t *>(take(8 * n));
     uint32_t *slow = reinterpret_cast<uint32_t *>(take(4 * (pl.nparts() + 1)));  // count, partitions
     uint32_t *gslot = reinterpret_cast<uint32_t *>(ent1);  // ent1 is dead after dp_split
-    const DpOut out{rep_out, ref_out, packed};
+    // with a sink the answers go there (multi-member classes only) and no
+    // singleton answer is written (dp_tile skips its stores)
+    const DpOut out{xs ? nullptr : rep_out, xs ? nullptr : ref_out, packed};
+    DpSink sink{nullptr, nullptr, nullptr, 0};
+    if (xs)
+        sink = DpSink{static_cast<uint4 *>(xs->ans), xs->cntr, xs->seg, xs->nseg};
     hipError_t e;
     if (ev0)
         (void)hipEventRecord(ev0, st);
@@ -1066,7 +1153,7 @@ hipError_t launch_dedup_group(const uint8_t *sig, uint32_t sig_stride, const uin
                           : GM_REP;
 #define DP_GROUP(G)                                                                                       \
     dp_group_kernel<G><<<(unsigned)pl.nparts(), kDpGroupThreads, 0, st>>>(ent2, pl.d2, pl.tiles, off1, cb, cdo, sig, \
-                                                                        sig_stride, out, slow)
+                                                                        sig_stride, out, sink, slow)
     if (gmode == GM_ROW)
         DP_GROUP(GM_ROW);
     else if (gmode == GM_REP)
@@ -1076,13 +1163,13 @@ hipError_t launch_dedup_group(const uint8_t *sig, uint32_t sig_stride, const uin
 #undef DP_GROUP
     if (gmode == GM_ROW)
         dp_group_slow_kernel<GM_ROW><<<256, kDpGroupThreads, 0, st>>>(ent2, pl.d2, pl.tiles, off1, cb, cdo, sig,
-                                                                    sig_stride, gword, gmin, gcnt, gslot, out, slow);
+                                                                    sig_stride, gword, gmin, gcnt, gslot, out, sink, slow);
     else if (gmode == GM_REP)
         dp_group_slow_kernel<GM_REP><<<256, kDpGroupThreads, 0, st>>>(ent2, pl.d2, pl.tiles, off1, cb, cdo, sig,
-                                                                    sig_stride, gword, gmin, gcnt, gslot, out, slow);
+                                                                    sig_stride, gword, gmin, gcnt, gslot, out, sink, slow);
     else
         dp_group_slow_kernel<GM_INDEX><<<256, kDpGroupThreads, 0, st>>>(ent2, pl.d2, pl.tiles, off1, cb, cdo, sig,
-                                                                      sig_stride, gword, gmin, gcnt, gslot, out, slow);
+                                                                      sig_stride, gword, gmin, gcnt, gslot, out, sink, slow);
     if (ev1)
         (void)hipEventRecord(ev1, st);
     return hipGetLastError();
@@ -1146,10 +1233,16 @@ __global__ __launch_bounds__(kBkThreads) void bucket_count_kernel(const uint8_t 
 
 // off: the scan of cnt (off[nranks * tiles] = n).  Block 0 also writes each
 // owner's row count (counts_out[q], the announcement's first nranks words).
+// x (fdfs_gpu_dedup_global, round 6): the rank's own rows (owner x.me) go
+// straight to the front of its owner-side receive buffer (x.self_rows: no
+// self copy), rec_of[send position] = record (the owner answers by send
+// position), and every record's singleton answer (rep = gidx, ref = 1) is
+// written here, coalesced, so that the owners return only the records of
+// multi-member classes.
 __global__ __launch_bounds__(kBkThreads) void bucket_scatter_kernel(
     const uint8_t *__restrict__ sig, const uint64_t *__restrict__ gidx, uint64_t n, uint32_t nranks,
     uint64_t tiles, const uint64_t *__restrict__ off, uint8_t *__restrict__ rows, uint64_t *__restrict__ row_of,
-    uint64_t *__restrict__ counts_out)
+    uint64_t *__restrict__ counts_out, BucketExtra x)
 {
     __shared__ uint32_t cnt[64];
     __shared__ uint64_t bas[64];
@@ -1160,6 +1253,7 @@ __global__ __launch_bounds__(kBkThreads) void bucket_scatter_kernel(
             counts_out[threadIdx.x] = off[(uint64_t)(threadIdx.x + 1) * tiles] - off[(uint64_t)threadIdx.x * tiles];
     }
     __syncthreads();
+    const uint64_t self0 = x.self_rows ? off[(uint64_t)x.me * tiles] : 0;  // the own segment's first send position
     const uint64_t t0 = (uint64_t)blockIdx.x * kBkTile;
 #pragma unroll 4
     for (int it = 0; it < kBkItems; it++) {
@@ -1170,18 +1264,26 @@ __global__ __launch_bounds__(kBkThreads) void bucket_scatter_kernel(
             const uint32_t own = (uint32_t)((sig_hash(a, b, c) >> 32) % nranks);  // owner_of
             const uint64_t pos = bas[own] + atomicAdd(&cnt[own], 1u);
             const uint64_t g = gidx ? gidx[r] : r;
-            uint4 *d = reinterpret_cast<uint4 *>(rows + 32 * pos);  // two 16-byte stores per row
+            uint8_t *dst = (x.self_rows && own == x.me) ? x.self_rows + 32 * (pos - self0) : rows + 32 * pos;
+            uint4 *d = reinterpret_cast<uint4 *>(dst);  // two 16-byte stores per row
             d[0] = make_uint4((uint32_t)a, (uint32_t)(a >> 32), (uint32_t)b, (uint32_t)(b >> 32));
             d[1] = make_uint4((uint32_t)c, (uint32_t)(c >> 32), (uint32_t)g, (uint32_t)(g >> 32));
             if (row_of)
                 row_of[r] = pos;
+            if (x.rec_of)
+                x.rec_of[pos] = (uint32_t)r;
+            if (x.rep_out) {
+                x.rep_out[r] = g;
+                x.ref_out[r] = 1u;
+            }
         }
     }
 }
 
 // Multi-GPU dedup (fdfs_gpu_dedup_global): the exchanged {rep, ref} answers
 // (the owners' packed group output) mapped back to the rank's records
-// through row_of.
+// through row_of.  (The torch-form exchange of fastdfs_amd/dist.py routes
+// answers this way; the C ABI's own exchange applies sink records instead.)
 __global__ void answer_gather_kernel(const uint64_t *__restrict__ back, const uint64_t *__restrict__ row_of,
                                      uint64_t n, uint64_t *__restrict__ rep_out, uint32_t *__restrict__ ref_out)
 {
@@ -1201,11 +1303,71 @@ hipError_t launch_answer_gather(const uint64_t *back, const uint64_t *row_of, ui
     return hipGetLastError();
 }
 
+// Owner q's segment table from the all-gathered announcements (ann: rank p's
+// row counts per owner at ann[p * w + q]): segment k of q's received rows
+// holds the rows of rank dg_seg_src(q, k) (its own first), seg[k] = its first
+// row, seg[kSinkSoff + k] = where those rows start in their sender's send
+// order; the per-segment sink counters zeroed.  One thread: <= 64 ranks.
+__global__ void sink_plan_kernel(const uint64_t *__restrict__ ann, uint32_t w, uint32_t nranks, uint32_t q,
+                                 uint64_t *__restrict__ seg, uint32_t *__restrict__ cntr)
+{
+    if (threadIdx.x < 64)
+        cntr[threadIdx.x] = 0;
+    if (threadIdx.x != 0)
+        return;
+    uint64_t start = 0;
+    for (uint32_t k = 0; k < nranks; k++) {
+        const uint32_t p = dg_seg_src(q, k);
+        uint64_t soff = 0;
+        for (uint32_t j = 0; j < q; j++)
+            soff += ann[(uint64_t)p * w + j];
+        seg[k] = start;
+        seg[kSinkSoff + k] = soff;
+        start += ann[(uint64_t)p * w + q];
+    }
+    seg[nranks] = start;
+}
+
+hipError_t launch_sink_plan(const uint64_t *ann, uint32_t w, uint32_t nranks, uint32_t q, uint64_t *seg,
+                            uint32_t *cntr, hipStream_t st)
+{
+    sink_plan_kernel<<<1, 64, 0, st>>>(ann, w, nranks, q, seg, cntr);
+    return hipGetLastError();
+}
+
+// The sink records that reached this rank, applied over its pre-filled
+// singleton answers: list a (count on the device: its own segment's, still
+// in its owner-side buffer) and list b (count known on the host: the other
+// owners' records after the way back).
+__global__ void answer_apply_kernel(const uint4 *__restrict__ a, const uint32_t *__restrict__ na,
+                                    const uint4 *__restrict__ b, uint64_t nb, const uint32_t *__restrict__ rec_of,
+                                    uint64_t *__restrict__ rep_out, uint32_t *__restrict__ ref_out)
+{
+    const uint64_t n1 = na ? *na : 0;
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n1 + nb;
+         i += (uint64_t)gridDim.x * blockDim.x) {
+        const uint4 v = i < n1 ? a[i] : b[i - n1];
+        const uint32_t r = rec_of[v.x];
+        rep_out[r] = (uint64_t)v.w << 32 | v.z;
+        ref_out[r] = v.y;
+    }
+}
+
+hipError_t launch_answer_apply(const void *a, const uint32_t *na, uint64_t na_max, const void *b, uint64_t nb,
+                               const uint32_t *rec_of, uint64_t *rep_out, uint32_t *ref_out, hipStream_t st)
+{
+    if (na_max + nb)
+        answer_apply_kernel<<<grid_for(na_max + nb, 256), 256, 0, st>>>(
+            static_cast<const uint4 *>(a), na, static_cast<const uint4 *>(b), nb, rec_of, rep_out, ref_out);
+    return hipGetLastError();
+}
+
 hipError_t launch_dedup_bucket(const uint8_t *sig, const uint64_t *gidx, uint64_t n,
                                uint32_t nranks, uint8_t *records_out, uint64_t *counts_out,
                                uint64_t *ws, uint64_t *row_of_out, hipStream_t st,
-                               hipEvent_t ev0, hipEvent_t ev1)
+                               hipEvent_t ev0, hipEvent_t ev1, const BucketExtra *extra)
 {
+    const BucketExtra x = extra ? *extra : BucketExtra{0, nullptr, nullptr, nullptr, nullptr};
     hipError_t e;
     if (n == 0)
         return launch_zero_u32(counts_out, 2ull * nranks, st);
@@ -1217,7 +1379,7 @@ hipError_t launch_dedup_bucket(const uint8_t *sig, const uint64_t *gidx, uint64_
     if ((e = launch_exclusive_scan(cnt, nt, off, bsum, st)) != hipSuccess)
         return e;
     bucket_scatter_kernel<<<(unsigned)tiles, kBkThreads, 0, st>>>(sig, gidx, n, nranks, tiles, off, records_out,
-                                                                  row_of_out, counts_out);
+                                                                  row_of_out, counts_out, x);
     if (ev1)
         (void)hipEventRecord(ev1, st);
     return hipGetLastError();

@@ -171,14 +171,49 @@ hipError_t launch_scrub(const uint32_t *crc, const uint32_t *expect, uint32_t n,
 
 // dedup path (fdfs_dedup.hip)
 uint64_t dedup_ws_bytes(uint64_t n);
-// packed: rep_out is an array of 16-byte {rep, ref, 0} records (ref_out unused)
+
+// fdfs_gpu_dedup_global's owner side: only the records of multi-member
+// classes are answered, as 16-byte records {sender row, ref, rep lo, rep hi}
+// appended per segment of the owner's received rows (fdfs_dedup.hip DpSink).
+// seg: seg_start[0 .. nseg] (rows), then at seg + kSinkSoff the segments'
+// first rows in their senders' send order; written by launch_sink_plan.
+constexpr int kSinkSoff = 65;
+constexpr int kSinkSegWords = 2 * 65;
+struct DedupSink {
+    void *ans;            // uint4[rows]: segment k's records from ans + seg_start[k]
+    uint32_t *cntr;       // [64] records per segment
+    const uint64_t *seg;  // [kSinkSegWords]
+    uint32_t nseg;
+};
+// The source rank of segment k of owner q's received rows: its own rows
+// first (the bucket pass writes them in place), then the others in rank order.
+__host__ __device__ inline uint32_t dg_seg_src(uint32_t q, uint32_t k) { return k == 0 ? q : (k <= q ? k - 1 : k); }
+// launch_dedup_bucket's extras for fdfs_gpu_dedup_global (all optional):
+// rows of owner `me` straight into self_rows (the owner-side buffer), the
+// record of each send position, every record's singleton answer pre-filled.
+struct BucketExtra {
+    uint32_t me;
+    uint8_t *self_rows;
+    uint32_t *rec_of;
+    uint64_t *rep_out;
+    uint32_t *ref_out;
+};
+
+// packed: rep_out is an array of 16-byte {rep, ref, 0} records (ref_out unused);
+// xs: answers as sink records instead (rep_out / ref_out unused)
 hipError_t launch_dedup_group(const uint8_t *sig, uint32_t sig_stride, const uint64_t *gidx,
                               uint32_t gidx_stride, uint64_t n, void *ws, uint64_t *rep_out,
-                              uint32_t *ref_out, bool packed, hipStream_t st, hipEvent_t ev0, hipEvent_t ev1);
+                              uint32_t *ref_out, bool packed, hipStream_t st, hipEvent_t ev0, hipEvent_t ev1,
+                              const DedupSink *xs = nullptr);
 hipError_t launch_dedup_bucket(const uint8_t *sig, const uint64_t *gidx, uint64_t n,
                                uint32_t nranks, uint8_t *records_out, uint64_t *counts_out,
                                uint64_t *ws, uint64_t *row_of_out, hipStream_t st,
-                               hipEvent_t ev0, hipEvent_t ev1);
+                               hipEvent_t ev0, hipEvent_t ev1, const BucketExtra *extra = nullptr);
+hipError_t launch_sink_plan(const uint64_t *ann, uint32_t w, uint32_t nranks, uint32_t q, uint64_t *seg,
+                            uint32_t *cntr, hipStream_t st);
+// na: device count of list a (<= na_max records); nb: host count of list b
+hipError_t launch_answer_apply(const void *a, const uint32_t *na, uint64_t na_max, const void *b, uint64_t nb,
+                               const uint32_t *rec_of, uint64_t *rep_out, uint32_t *ref_out, hipStream_t st);
 // u64 words of launch_dedup_bucket's workspace for n records
 size_t bucket_ws_elems(uint64_t n);
 

@@ -142,10 +142,19 @@ def dedup_global(kernels, sig: torch.Tensor, gidx: torch.Tensor, group=None, sta
     ingest indices.  Returns (rep int64[n], ref int32[n]) for this rank's
     files, identical to single-process dedup over the concatenated input.
     stats: optional dict; "peer_bytes" accumulates the bytes this rank sent
-    to other ranks (32-byte rows out, 16-byte answers back; torch form only).
+    to other ranks, "row_bytes" / "answer_bytes" its two parts: with comm,
+    the 32-byte rows to the other owners and the 16-byte answer records of
+    multi-member classes back to their senders (fdfs_gpu_dedup_global_stats);
+    in the torch form 32 bytes per row out and a 16-byte answer per row back.
     """
     if comm is not None:
-        return kernels.dedup_global(comm, sig, gidx)
+        out = kernels.dedup_global(comm, sig, gidx)
+        if stats is not None:
+            b = kernels.dedup_global_stats()
+            for k, v in (("row_bytes", b["row_bytes"]), ("answer_bytes", b["answer_bytes"]),
+                         ("peer_bytes", b["row_bytes"] + b["answer_bytes"])):
+                stats[k] = stats.get(k, 0) + v
+        return out
     world = dist.get_world_size(group)
     dev = sig.device
     rows, counts, row_of = kernels.dedup_bucket(sig, gidx, world)
@@ -155,8 +164,9 @@ def dedup_global(kernels, sig: torch.Tensor, gidx: torch.Tensor, group=None, sta
     recv = recv_counts.cpu().tolist()
     if stats is not None:
         me = dist.get_rank(group)
-        stats["peer_bytes"] = stats.get("peer_bytes", 0) + 32 * (sum(send) - send[me]) + \
-            16 * (sum(recv) - recv[me])
+        rb, ab = 32 * (sum(send) - send[me]), 16 * (sum(recv) - recv[me])
+        for k, v in (("row_bytes", rb), ("answer_bytes", ab), ("peer_bytes", rb + ab)):
+            stats[k] = stats.get(k, 0) + v
     m = int(sum(recv))
     rows_in = torch.empty((m, 32), dtype=torch.uint8, device=dev)
     dist.all_to_all_single(rows_in, rows, output_split_sizes=recv, input_split_sizes=send,

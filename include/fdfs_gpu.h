@@ -269,13 +269,19 @@ int fdfs_gpu_index_slots(fdfs_gpu_index *index, uint64_t *slots);
  * than one rank); every rank calls it with its share and gets rep_out /
  * ref_out for its own records, identical to fdfs_gpu_dedup over the
  * concatenated ingest.  Inside: bucket by owner rank (the FastDHT key
- * partition, storage/fdht_client/fdht_client.c:301-305, as a GPU bucket);
- * one ncclAllGather of every rank's announcement (rows per owner, the room
- * of its owner-side buffers, any local error), from which every rank derives
- * the same exchange plan; grouped ncclSend/ncclRecv of the 32-byte rows; the
- * owner's group; the {rep, ref} answers sent back the same way.  The one
- * host synchronisation is the announcement (the row exchange is sized by
- * it), plus one small all-reduce when some owner's buffers must grow.
+ * partition, storage/fdht_client/fdht_client.c:301-305, as a GPU bucket),
+ * which also writes every record's singleton answer (rep = its gidx, ref =
+ * 1) and puts the rank's own rows straight into its owner-side buffer; one
+ * ncclAllGather of every rank's announcement (rows per owner, the room of
+ * its owner-side buffers, any local error), from which every rank derives
+ * the same exchange plan; grouped ncclSend/ncclRecv of the 32-byte rows to
+ * the other owners; the owner's group, which answers only the rows of
+ * multi-member classes (16-byte records {sender row, ref, rep}); one small
+ * ncclAllGather of those records' counts; the records sent back the same
+ * way and applied over the singleton answers.  Host synchronisations: the
+ * announcement (the row exchange is sized by it) and, with more than one
+ * rank, the record counts (the way back is sized by them), plus one small
+ * all-reduce when some owner's buffers must grow.
  * Errors: an argument error or allocation failure on ANY rank is returned by
  * EVERY rank (EINVAL / ENOMEM; fdfs_gpu_last_error names the rank) before
  * any row moves, so no rank is left waiting.  EIO after that point (a failed
@@ -293,7 +299,7 @@ int fdfs_gpu_dedup_global(fdfs_gpu_ctx *ctx, void *comm, const uint8_t *sig, con
 /* fdfs_gpu_dedup_global for `nranks` VIRTUAL ranks in this process, all on
  * this context's device: rank p's share is sig[p], gidx[p], n[p] -> rep_out[p],
  * ref_out[p] (host arrays of nranks device pointers / counts).  It runs the
- * same bucket, exchange plan, group and answer-gather code as the RCCL form;
+ * same bucket, exchange plan, group, sink and apply code as the RCCL form;
  * every (src, dst) segment moves by hipMemcpyAsync where RCCL would send it.
  * This is how the multi-rank offsets and answer routing are checked on one
  * GPU (tests/test_gpu_dedup.py), and a one-process fallback for a caller
@@ -301,6 +307,12 @@ int fdfs_gpu_dedup_global(fdfs_gpu_ctx *ctx, void *comm, const uint8_t *sig, con
 int fdfs_gpu_dedup_global_local(fdfs_gpu_ctx *ctx, int nranks, const uint8_t *const *sig,
                                 const uint64_t *const *gidx, const uint64_t *n, uint64_t *const *rep_out,
                                 uint32_t *const *ref_out, void *stream);
+
+/* Bytes the context's last fdfs_gpu_dedup_global(_local) call moved between
+ * ranks (sent by this rank; all virtual ranks for _local): the 32-byte rows
+ * to the other owners, and the 16-byte answer records back to the other
+ * ranks.  Measurement only (bench.py's xGMI bytes per step). */
+int fdfs_gpu_dedup_global_stats(fdfs_gpu_ctx *ctx, uint64_t *row_bytes, uint64_t *answer_bytes);
 
 /* Split-file CRC32 over N GPUs: the bytes of `nfiles` files
  * are spread over the ranks in pieces, cut anywhere (e.g. the files'

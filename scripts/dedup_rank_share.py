@@ -73,10 +73,19 @@ def main():
     bms, bn = ctx.read_timing(_lib.KERNEL_BUCKET)
     gms, gn = ctx.read_timing(_lib.KERNEL_DEDUP)
     ctx.set_timing(False)
-    print(json.dumps({"mode": a.mode, "world": a.world, "records_rank0": n0, "reps": a.reps,
-                      "wall_ms_per_call": round(wall, 4),
-                      "bucket_ms_per_call": round(bms / a.reps, 4), "bucket_launches": bn,
-                      "group_ms_per_call": round(gms / a.reps, 4), "group_launches": gn}), flush=True)
+    rec = {"mode": a.mode, "world": a.world, "records_rank0": n0, "reps": a.reps,
+           "wall_ms_per_call": round(wall, 4),
+           "bucket_ms_per_call": round(bms / a.reps, 4), "bucket_launches": bn,
+           "group_ms_per_call": round(gms / a.reps, 4), "group_launches": gn}
+    if a.mode != "single" and hasattr(ctx._L, "fdfs_gpu_dedup_global_stats"):
+        # bytes between ranks per call (all virtual ranks for --mode local);
+        # the round-5 protocol returned a 16-byte answer for every row it
+        # received, i.e. half the row bytes
+        b = ctx.dedup_global_stats()
+        rec.update({"row_bytes": b["row_bytes"], "answer_bytes": b["answer_bytes"],
+                    "answer_bytes_round5_protocol": b["row_bytes"] // 2,
+                    "answer_ratio_vs_round5": round(b["answer_bytes"] / max(b["row_bytes"] // 2, 1), 4)})
+    print(json.dumps(rec), flush=True)
     if comm is not None:
         comm.close()
     ctx.close()
