@@ -137,8 +137,9 @@ fdfs::BigCrcWs carve_big(const fdfs_gpu_ctx *ctx, Carve &cv, uint32_t n)
 size_t dedup_ws_bytes(uint64_t n) { return fdfs::dedup_ws_bytes(n) + align_up(8 * 64); }
 
 // fdfs_gpu_dedup_global announcement: rank p's row count per owner (nranks
-// words), then kAnnTail words {owner-side room, workspace room, errno}.
-constexpr int kAnnTail = 3;
+// words), then kAnnTail words {owner-side room, workspace room, errno, the
+// capacity of each owner region of its send order (0: exact prefix layout)}.
+constexpr int kAnnTail = 4;
 constexpr size_t kAnnMax = 64 + kAnnTail;                   // words of one announcement
 constexpr size_t kErrRing = 64;  // lane_err_note's per-launch slots
 // fdfs_gpu_dedup_global's answer counts: every owner's sink-record count
@@ -1252,16 +1253,27 @@ struct DgPlan {
     int nranks = 0;
     uint64_t cnt[64][64];  // cnt[p][q]: rows rank p sends to owner q
     uint64_t m[64];        // rows owner q groups
+    uint64_t cap[64];      // rank p's owner-region capacity (launch_bucket_place), 0: exact layout
     int err = 0, err_rank = -1;
     bool grow = false;     // an owner's buffers must grow: the ranks agree on the outcome first
+    bool over = false;     // some rank's owner count exceeds its cap: every rank buckets again exactly
     // where p's rows for owner q start among p's rows in send order (the
     // sender row its answers name)
     uint64_t soff(int p, int q) const
     {
+        if (cap[p])
+            return (uint64_t)q * cap[p];
         uint64_t s = 0;
         for (int k = 0; k < q; k++)
             s += cnt[p][k];
         return s;
+    }
+    // after an over-capacity owner: every rank's exact prefix layout
+    void exact()
+    {
+        for (int p = 0; p < nranks; p++)
+            cap[p] = 0;
+        over = false;
     }
     // where p's rows start among owner q's received rows: q's own rows
     // first, then the other ranks' in rank order (fdfs::dg_seg_src; the
@@ -1301,9 +1313,17 @@ struct DgAns {
     uint64_t recv_total(int p, int nranks) const { return boff(p, nranks); }
 };
 
-static size_t dg_a_bytes(uint64_t n)
+// send-order slots of a rank's rows: the fixed-capacity owner regions of
+// launch_bucket_place (nranks x cap, a little over n), or n
+static uint64_t dg_slots(uint64_t n, int nranks)
 {
-    return align_up(32 * n) + align_up(4 * n) + align_up(16 * n) + align_up(8 * fdfs::bucket_ws_elems(n));
+    return std::max<uint64_t>(n, (uint64_t)nranks * fdfs::bucket_cap(n, (uint32_t)nranks));
+}
+
+static size_t dg_a_bytes(uint64_t n, int nranks)
+{
+    const uint64_t sl = dg_slots(n, nranks);
+    return align_up(32 * sl) + align_up(4 * sl) + align_up(16 * n) + align_up(8 * fdfs::bucket_ws_elems(n));
 }
 
 static size_t dg_b_bytes(uint64_t m)
@@ -1320,9 +1340,12 @@ static void dg_plan(const uint64_t *ann, int nranks, DgPlan &pl)
         pl.m[q] = 0;
     for (int p = 0; p < nranks; p++) {
         const uint64_t *a = ann + p * w;
+        pl.cap[p] = a[nranks + 3];
         for (int q = 0; q < nranks; q++) {
             pl.cnt[p][q] = a[q];
             pl.m[q] += a[q];
+            if (pl.cap[p] && a[q] > pl.cap[p])
+                pl.over = true;
         }
         if (a[nranks + 2] && !pl.err) {
             pl.err = (int)a[nranks + 2];
@@ -1359,11 +1382,12 @@ struct DgSide {
     uint32_t *cntr = nullptr;     // [64] sink records per segment
 };
 
-static void dg_carve_a(DgSide &s, void *mem)
+static void dg_carve_a(DgSide &s, void *mem, int nranks)
 {
     Carve c{static_cast<char *>(mem)};
-    s.rows = c.take<uint8_t>(32 * s.n);
-    s.rec_of = c.take<uint32_t>(s.n);
+    const uint64_t sl = dg_slots(s.n, nranks);
+    s.rows = c.take<uint8_t>(32 * sl);
+    s.rec_of = c.take<uint32_t>(sl);
     s.back = c.take<uint8_t>(16 * s.n);
     s.bws = c.take<uint64_t>(fdfs::bucket_ws_elems(s.n));
 }
@@ -1400,24 +1424,29 @@ static int dg_check(const uint8_t *sig, const uint64_t *gidx, uint64_t n, const 
 // the record of each send position, every record's singleton answer; rank
 // `me`'s own rows to `self_rows` when given (the RCCL form: the front of its
 // owner-side buffer), else to their send slots (the local form copies them).
+// cap > 0: the one-pass fixed-capacity form (launch_bucket_place); 0: the
+// exact two-pass form (after a plan found an owner over some rank's cap).
 static hipError_t dg_bucket(fdfs_gpu_ctx *ctx, DgSide &s, int nranks, int me, uint8_t *self_rows, uint64_t *ann,
-                            hipStream_t st)
+                            uint64_t cap, hipStream_t st)
 {
     hipEvent_t a, b;
     timing_pair(ctx, FDFS_KERNEL_BUCKET, a, b);
     const fdfs::BucketExtra x{(uint32_t)me, self_rows, s.rec_of, s.rep_out, s.ref_out};
+    if (cap)
+        return fdfs::launch_bucket_place(s.sig, s.gidx, s.n, (uint32_t)nranks, cap, s.rows, ann, x, st, a, b);
     return fdfs::launch_dedup_bucket(s.sig, s.gidx, s.n, (uint32_t)nranks, s.rows, ann, s.bws, nullptr, st, a, b,
                                      &x);
 }
 
-// The announcement's tail {owner-side room, workspace room, errno}, staged
-// in pinned memory (`h`, untouched until the stream has copied it).
+// The announcement's tail {owner-side room, workspace room, errno, cap},
+// staged in pinned memory (`h`, untouched until the stream has copied it).
 static hipError_t dg_announce(uint64_t *ann_tail, uint64_t *h, uint64_t b_room, uint64_t ws_room, int err,
-                              hipStream_t st)
+                              uint64_t cap, hipStream_t st)
 {
     h[0] = b_room;
     h[1] = ws_room;
     h[2] = (uint64_t)err;
+    h[3] = cap;
     return hipMemcpyAsync(ann_tail, h, 8 * kAnnTail, hipMemcpyHostToDevice, st);
 }
 
@@ -1425,9 +1454,9 @@ static hipError_t dg_announce(uint64_t *ann_tail, uint64_t *h, uint64_t b_room, 
 // each), then its group of the received rows (min gidx from the rows' own
 // word 3) into sink records.
 static hipError_t dg_group(fdfs_gpu_ctx *ctx, DgSide &s, const uint64_t *all, size_t w, int nranks, int q,
-                           hipStream_t st)
+                           bool exact, hipStream_t st)
 {
-    hipError_t e = fdfs::launch_sink_plan(all, (uint32_t)w, (uint32_t)nranks, (uint32_t)q, s.seg, s.cntr, st);
+    hipError_t e = fdfs::launch_sink_plan(all, (uint32_t)w, (uint32_t)nranks, (uint32_t)q, exact, s.seg, s.cntr, st);
     if (e != hipSuccess)
         return e;
     hipEvent_t a, b;
@@ -1540,7 +1569,7 @@ int fdfs_gpu_dedup_global(fdfs_gpu_ctx *ctx, void *comm, const uint8_t *sig, con
     ctx->x_row_bytes = ctx->x_ans_bytes = 0;
     int err = dg_check(sig, gidx, n, rep_out, ref_out, nranks);
     if (!err)
-        err = ensure_buf(ctx, &ctx->xa, &ctx->xa_bytes, dg_a_bytes(n), st);
+        err = ensure_buf(ctx, &ctx->xa, &ctx->xa_bytes, dg_a_bytes(n, nranks), st);
     // room for the own rows the bucket pass writes in place (<= n of them)
     if (!err)
         err = ensure_buf(ctx, &ctx->xb, &ctx->xb_bytes, dg_b_bytes(n), st);
@@ -1557,14 +1586,15 @@ int fdfs_gpu_dedup_global(fdfs_gpu_ctx *ctx, void *comm, const uint8_t *sig, con
     s.rep_out = rep_out;
     s.ref_out = ref_out;
     hipError_t e;
+    const uint64_t cap = fdfs::bucket_cap(n, (uint32_t)nranks);
     if (!err) {
-        dg_carve_a(s, ctx->xa);
-        if ((e = dg_bucket(ctx, s, nranks, me, static_cast<uint8_t *>(ctx->xb), ann, st)) != hipSuccess)
+        dg_carve_a(s, ctx->xa, nranks);
+        if ((e = dg_bucket(ctx, s, nranks, me, static_cast<uint8_t *>(ctx->xb), ann, cap, st)) != hipSuccess)
             err = fail(ctx, e, "dedup_global bucket");
     }
     if (err && (e = fdfs::launch_zero_u32(ann, 2ull * nranks, st)) != hipSuccess)
         return fail(ctx, e, "dedup_global announce");  // the device is gone; so is the exchange
-    if ((e = dg_announce(ann + nranks, htail, ctx->xb_bytes, ctx->ws_bytes, err, st)) != hipSuccess)
+    if ((e = dg_announce(ann + nranks, htail, ctx->xb_bytes, ctx->ws_bytes, err, cap, st)) != hipSuccess)
         return fail(ctx, e, "dedup_global announce");
     // 1. every rank's announcement to every rank, then to the host (the row
     //    exchange is sized by it)
@@ -1578,6 +1608,15 @@ int fdfs_gpu_dedup_global(fdfs_gpu_ctx *ctx, void *comm, const uint8_t *sig, con
     dg_plan(hall, nranks, pl);
     if (pl.err)
         return dg_plan_error(ctx, pl, me);
+    const bool exact = pl.over;
+    if (pl.over) {
+        // an owner over some rank's cap (skewed owners): every rank sees it
+        // in the same counts and buckets again in the exact layout; the
+        // counts do not change, so nothing is announced again
+        pl.exact();
+        if ((e = dg_bucket(ctx, s, nranks, me, static_cast<uint8_t *>(ctx->xb), ann, 0, st)) != hipSuccess)
+            return fail(ctx, e, "dedup_global bucket");
+    }
     if (pl.grow) {
         // some owner must grow its buffers: each grows its own (keeping the
         // own rows at the front), and the ranks agree on the outcome (max over
@@ -1614,7 +1653,7 @@ int fdfs_gpu_dedup_global(fdfs_gpu_ctx *ctx, void *comm, const uint8_t *sig, con
     if ((rc = dg_nccl_group(ctx, c, sends, recvs, st)))
         return rc;
     // 3. the owner's group: sink records for the rows of multi-member classes
-    if ((e = dg_group(ctx, s, all, w, nranks, me, st)) != hipSuccess)
+    if ((e = dg_group(ctx, s, all, w, nranks, me, exact, st)) != hipSuccess)
         return fail(ctx, e, "dedup_global group");
     uint64_t nb = 0;
     if (nranks > 1) {
@@ -1678,7 +1717,7 @@ int fdfs_gpu_dedup_global_local(fdfs_gpu_ctx *ctx, int nranks, const uint8_t *co
     std::vector<DgSide> s(nranks);
     size_t abytes = 0;
     for (int p = 0; p < nranks; p++)
-        abytes += dg_a_bytes(n[p]);
+        abytes += dg_a_bytes(n[p], nranks);
     void *amem = nullptr, *bmem = nullptr;
     hipError_t e = hipMalloc(&amem, abytes);
     if (e != hipSuccess) {
@@ -1697,13 +1736,14 @@ int fdfs_gpu_dedup_global_local(fdfs_gpu_ctx *ctx, int nranks, const uint8_t *co
         s[p].n = n[p];
         s[p].rep_out = rep_out[p];
         s[p].ref_out = ref_out[p];
-        dg_carve_a(s[p], static_cast<char *>(amem) + done);
-        done += dg_a_bytes(n[p]);
+        dg_carve_a(s[p], static_cast<char *>(amem) + done, nranks);
+        done += dg_a_bytes(n[p], nranks);
         // 1. every virtual rank's bucket (its own rows to their send slots:
         //    this transport copies every segment) and announcement (no
         //    owner-side buffers yet: room 0, so the plan always grows them)
-        if ((e = dg_bucket(ctx, s[p], nranks, p, nullptr, all + p * w, st)) != hipSuccess ||
-            (e = dg_announce(all + p * w + nranks, htail + kAnnTail * p, 0, ctx->ws_bytes, 0, st)) != hipSuccess)
+        const uint64_t cap = fdfs::bucket_cap(n[p], (uint32_t)nranks);
+        if ((e = dg_bucket(ctx, s[p], nranks, p, nullptr, all + p * w, cap, st)) != hipSuccess ||
+            (e = dg_announce(all + p * w + nranks, htail + kAnnTail * p, 0, ctx->ws_bytes, 0, cap, st)) != hipSuccess)
             rc = fail(ctx, e, "dedup_global_local bucket");
     }
     if (!rc && ((e = hipMemcpyAsync(hall, all, 8 * w * nranks, hipMemcpyDeviceToHost, st)) != hipSuccess ||
@@ -1712,6 +1752,13 @@ int fdfs_gpu_dedup_global_local(fdfs_gpu_ctx *ctx, int nranks, const uint8_t *co
     if (!rc) {
         dg_plan(hall, nranks, *pl);
         rc = pl->err ? dg_plan_error(ctx, *pl, -1) : 0;
+    }
+    const bool exact = !rc && pl->over;
+    if (exact) {  // an owner over some rank's cap: every rank's exact layout
+        pl->exact();
+        for (int p = 0; p < nranks && !rc; p++)
+            if ((e = dg_bucket(ctx, s[p], nranks, p, nullptr, all + p * w, 0, st)) != hipSuccess)
+                rc = fail(ctx, e, "dedup_global_local bucket");
     }
     size_t bbytes = 0, wsb = 0;
     for (int q = 0; q < nranks && !rc; q++) {
@@ -1742,7 +1789,7 @@ int fdfs_gpu_dedup_global_local(fdfs_gpu_ctx *ctx, int nranks, const uint8_t *co
                         ctx->x_row_bytes += 32 * pl->cnt[p][q];
                 }
         for (int q = 0; q < nranks && !rc; q++)
-            if ((e = dg_group(ctx, s[q], all, w, nranks, q, st)) != hipSuccess)
+            if ((e = dg_group(ctx, s[q], all, w, nranks, q, exact, st)) != hipSuccess)
                 rc = fail(ctx, e, "dedup_global_local group");
         // 4. the owners' record counts, then the records back to the senders
         for (int q = 0; q < nranks && !rc; q++)

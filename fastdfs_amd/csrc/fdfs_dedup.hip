@@ -1280,6 +1280,108 @@ __global__ __launch_bounds__(kBkThreads) void bucket_scatter_kernel(
     }
 }
 
+// fdfs_gpu_dedup_global's bucket in one pass (round 6): owner q's rows go to
+// a fixed-capacity region [q cap, q cap + cnt_q) of the send order, and each
+// tile reserves its per-owner ranges with one device-scope atomic per owner
+// on the announcement's count words (12.5M records: ~3K tiles x 8 owners,
+// against round 4's 390K per-block atomics) -- no counting pass over the
+// signatures and no scan.  A tile's records stay in registers between the
+// LDS count (per wave, the atomic's return is the record's rank) and the
+// stores, so each signature is read once.  cap = n / nranks plus slack
+// (bucket_cap); an owner count above it (skewed owners: one signature
+// repeated many times) is not written, and every rank sees it in the
+// all-gathered counts and buckets again with the exact two-pass form.
+constexpr int kBpItems = 16, kBpTile = kBkThreads * kBpItems;  // 4096 records per tile
+
+uint64_t bucket_cap(uint64_t n, uint32_t nranks)
+{
+    if (nranks <= 1)
+        return n;
+    const uint64_t mean = (n + nranks - 1) / nranks;
+    uint64_t sd = 1;
+    while (sd * sd < mean)
+        sd++;
+    const uint64_t cap = mean + 8 * sd + 1024;  // binomial owner counts: 8 sigma
+    return cap < n ? cap : n;
+}
+
+__global__ __launch_bounds__(kBkThreads) void bucket_place_kernel(
+    const uint8_t *__restrict__ sig, const uint64_t *__restrict__ gidx, uint64_t n, uint32_t nranks, uint64_t cap,
+    uint8_t *__restrict__ rows, unsigned long long *__restrict__ counts, BucketExtra x)
+{
+    __shared__ uint32_t h[kBkThreads / 64][64];  // per wave: fewer lanes on one LDS counter
+    __shared__ uint64_t wb[kBkThreads / 64][64];  // the wave's first slot per owner
+    const int w = threadIdx.x >> 6;
+    for (int k = threadIdx.x; k < (kBkThreads / 64) * 64; k += kBkThreads)
+        (&h[0][0])[k] = 0;
+    __syncthreads();
+    const uint64_t t0 = (uint64_t)blockIdx.x * kBpTile;
+    uint64_t a[kBpItems], b[kBpItems], c[kBpItems];
+    uint32_t ok[kBpItems];  // owner << 16 | rank among the wave's records of that owner
+#pragma unroll
+    for (int it = 0; it < kBpItems; it++) {
+        const uint64_t r = t0 + (uint64_t)it * kBkThreads + threadIdx.x;
+        a[it] = b[it] = c[it] = 0;
+        ok[it] = 0;
+        if (r < n) {
+            load_sig(sig + 24 * r, a[it], b[it], c[it]);
+            const uint32_t own = (uint32_t)((sig_hash(a[it], b[it], c[it]) >> 32) % nranks);  // owner_of
+            ok[it] = own << 16 | atomicAdd(&h[w][own], 1u);
+        }
+    }
+    __syncthreads();
+    if (threadIdx.x < nranks) {
+        const uint32_t q = threadIdx.x;
+        uint32_t tot = 0;
+#pragma unroll
+        for (int v = 0; v < kBkThreads / 64; v++)
+            tot += h[v][q];
+        uint64_t base = tot ? (uint64_t)atomicAdd(&counts[q], (unsigned long long)tot) : 0;
+#pragma unroll
+        for (int v = 0; v < kBkThreads / 64; v++) {
+            wb[v][q] = base;
+            base += h[v][q];
+        }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int it = 0; it < kBpItems; it++) {
+        const uint64_t r = t0 + (uint64_t)it * kBkThreads + threadIdx.x;
+        if (r < n) {
+            const uint32_t own = ok[it] >> 16;
+            const uint64_t k = wb[w][own] + (ok[it] & 0xFFFFu);
+            const uint64_t g = gidx ? gidx[r] : r;
+            if (k < cap) {
+                const uint64_t pos = (uint64_t)own * cap + k;
+                uint8_t *dst = (x.self_rows && own == x.me) ? x.self_rows + 32 * k : rows + 32 * pos;
+                uint4 *d = reinterpret_cast<uint4 *>(dst);
+                d[0] = make_uint4((uint32_t)a[it], (uint32_t)(a[it] >> 32), (uint32_t)b[it], (uint32_t)(b[it] >> 32));
+                d[1] = make_uint4((uint32_t)c[it], (uint32_t)(c[it] >> 32), (uint32_t)g, (uint32_t)(g >> 32));
+                x.rec_of[pos] = (uint32_t)r;
+            }
+            x.rep_out[r] = g;
+            x.ref_out[r] = 1u;
+        }
+    }
+}
+
+hipError_t launch_bucket_place(const uint8_t *sig, const uint64_t *gidx, uint64_t n, uint32_t nranks,
+                               uint64_t cap, uint8_t *rows, uint64_t *counts, const BucketExtra &x, hipStream_t st,
+                               hipEvent_t ev0, hipEvent_t ev1)
+{
+    hipError_t e = launch_zero_u32(counts, 2ull * nranks, st);
+    if (e != hipSuccess)
+        return e;
+    if (ev0)
+        (void)hipEventRecord(ev0, st);
+    if (n)
+        bucket_place_kernel<<<(unsigned)((n + kBpTile - 1) / kBpTile), kBkThreads, 0, st>>>(
+            sig, gidx, n, nranks, cap, rows, reinterpret_cast<unsigned long long *>(counts), x);
+    if (ev1)
+        (void)hipEventRecord(ev1, st);
+    return hipGetLastError();
+}
+
 // Multi-GPU dedup (fdfs_gpu_dedup_global): the exchanged {rep, ref} answers
 // (the owners' packed group output) mapped back to the rank's records
 // through row_of.  (The torch-form exchange of fastdfs_amd/dist.py routes
@@ -1304,12 +1406,13 @@ hipError_t launch_answer_gather(const uint64_t *back, const uint64_t *row_of, ui
 }
 
 // Owner q's segment table from the all-gathered announcements (ann: rank p's
-// row counts per owner at ann[p * w + q]): segment k of q's received rows
+// row counts per owner at ann[p * w + q], its cap at ann[p * w + nranks + 3]):
+// segment k of q's received rows
 // holds the rows of rank dg_seg_src(q, k) (its own first), seg[k] = its first
 // row, seg[kSinkSoff + k] = where those rows start in their sender's send
 // order; the per-segment sink counters zeroed.  One thread: <= 64 ranks.
 __global__ void sink_plan_kernel(const uint64_t *__restrict__ ann, uint32_t w, uint32_t nranks, uint32_t q,
-                                 uint64_t *__restrict__ seg, uint32_t *__restrict__ cntr)
+                                 bool exact, uint64_t *__restrict__ seg, uint32_t *__restrict__ cntr)
 {
     if (threadIdx.x < 64)
         cntr[threadIdx.x] = 0;
@@ -1318,9 +1421,15 @@ __global__ void sink_plan_kernel(const uint64_t *__restrict__ ann, uint32_t w, u
     uint64_t start = 0;
     for (uint32_t k = 0; k < nranks; k++) {
         const uint32_t p = dg_seg_src(q, k);
+        // the sender's layout: fixed-capacity owner regions (its announced
+        // cap, launch_bucket_place) or, after a rebucket, the exact prefix
+        const uint64_t cap = exact ? 0 : ann[(uint64_t)p * w + nranks + 3];
         uint64_t soff = 0;
-        for (uint32_t j = 0; j < q; j++)
-            soff += ann[(uint64_t)p * w + j];
+        if (cap)
+            soff = (uint64_t)q * cap;
+        else
+            for (uint32_t j = 0; j < q; j++)
+                soff += ann[(uint64_t)p * w + j];
         seg[k] = start;
         seg[kSinkSoff + k] = soff;
         start += ann[(uint64_t)p * w + q];
@@ -1328,10 +1437,10 @@ __global__ void sink_plan_kernel(const uint64_t *__restrict__ ann, uint32_t w, u
     seg[nranks] = start;
 }
 
-hipError_t launch_sink_plan(const uint64_t *ann, uint32_t w, uint32_t nranks, uint32_t q, uint64_t *seg,
+hipError_t launch_sink_plan(const uint64_t *ann, uint32_t w, uint32_t nranks, uint32_t q, bool exact, uint64_t *seg,
                             uint32_t *cntr, hipStream_t st)
 {
-    sink_plan_kernel<<<1, 64, 0, st>>>(ann, w, nranks, q, seg, cntr);
+    sink_plan_kernel<<<1, 64, 0, st>>>(ann, w, nranks, q, exact, seg, cntr);
     return hipGetLastError();
 }
 

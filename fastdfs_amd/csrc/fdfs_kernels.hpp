@@ -209,7 +209,17 @@ hipError_t launch_dedup_bucket(const uint8_t *sig, const uint64_t *gidx, uint64_
                                uint32_t nranks, uint8_t *records_out, uint64_t *counts_out,
                                uint64_t *ws, uint64_t *row_of_out, hipStream_t st,
                                hipEvent_t ev0, hipEvent_t ev1, const BucketExtra *extra = nullptr);
-hipError_t launch_sink_plan(const uint64_t *ann, uint32_t w, uint32_t nranks, uint32_t q, uint64_t *seg,
+// fdfs_gpu_dedup_global's one-pass bucket: owner q's rows at [q cap, q cap +
+// counts[q]) of the send order (rows past cap not written: counts[q] > cap
+// tells the plan to bucket again with launch_dedup_bucket); x.rec_of,
+// x.rep_out and x.ref_out required.
+uint64_t bucket_cap(uint64_t n, uint32_t nranks);
+hipError_t launch_bucket_place(const uint8_t *sig, const uint64_t *gidx, uint64_t n, uint32_t nranks,
+                               uint64_t cap, uint8_t *rows, uint64_t *counts, const BucketExtra &x, hipStream_t st,
+                               hipEvent_t ev0, hipEvent_t ev1);
+// exact: every sender used the exact prefix layout (a rebucket after an
+// over-capacity owner), not its announced cap
+hipError_t launch_sink_plan(const uint64_t *ann, uint32_t w, uint32_t nranks, uint32_t q, bool exact, uint64_t *seg,
                             uint32_t *cntr, hipStream_t st);
 // na: device count of list a (<= na_max records); nb: host count of list b
 hipError_t launch_answer_apply(const void *a, const uint32_t *na, uint64_t na_max, const void *b, uint64_t nb,

@@ -314,6 +314,49 @@ def test_dedup_global_local_vs_oracle(oracle, ctx, nranks):
         assert np.array_equal(ref.cpu().numpy(), oref[lo:hi].astype(np.int32)), p
 
 
+def _owners(ctx, sig_t, nranks):
+    """Each record's owner rank, from the public bucket (rows grouped by owner)."""
+    _, counts, row_of = ctx.dedup_bucket(sig_t, None, nranks)
+    ends = np.cumsum(counts.cpu().numpy())
+    return np.searchsorted(ends, row_of.cpu().numpy(), side="right")
+
+
+@pytest.mark.parametrize("nranks,hot", [(4, 0.0), (4, 0.6), (8, 0.3)])
+def test_dedup_global_local_sink_bytes_and_skew(oracle, ctx, nranks, hot):
+    """Round 6's exchange: the owners return only the records of
+    multi-member classes (16-byte sink records), the rows of a rank's own
+    owner never cross, and a share whose owners are skewed far past the
+    one-pass bucket's fixed capacity (`hot` of all records one signature:
+    one owner gets them all) falls back to the exact layout on every rank.
+    Answers equal the oracle's; the bytes the library reports equal what the
+    owner of every record implies."""
+    n = 80_000
+    sig = _sigs(n, 50_000, 7 + nranks)
+    nh = int(hot * n)
+    if nh:
+        sig[np.random.default_rng(3).choice(n, nh, replace=False)] = sig[0]
+    gidx = np.arange(n, dtype=np.int64) * 3 + 11
+    bounds = np.linspace(0, n, nranks + 1).astype(np.int64)
+    sig_t, g_t = torch.from_numpy(sig).cuda(), torch.from_numpy(gidx).cuda()
+    shares = [(sig_t[bounds[p]:bounds[p + 1]].contiguous(), g_t[bounds[p]:bounds[p + 1]].contiguous())
+              for p in range(nranks)]
+    outs = ctx.dedup_global_local([s for s, _ in shares], [g for _, g in shares])
+    st = ctx.dedup_global_stats()
+    orep, oref = oracle.dedup(sig)
+    rows = ans = 0
+    for p in range(nranks):
+        lo, hi = bounds[p], bounds[p + 1]
+        rep, ref = outs[p]
+        assert np.array_equal(rep.cpu().numpy(), gidx[orep[lo:hi].astype(np.int64)]), p
+        assert np.array_equal(ref.cpu().numpy(), oref[lo:hi].astype(np.int32)), p
+        own = _owners(ctx, shares[p][0], nranks)
+        away = own != p
+        rows += int(away.sum())
+        ans += int((away & (oref[lo:hi] > 1)).sum())
+    assert st == {"row_bytes": 32 * rows, "answer_bytes": 16 * ans}
+    assert st["answer_bytes"] < st["row_bytes"] / 2  # the round-5 protocol's answers: 16 B per row
+
+
 def test_dedup_global_needs_gidx_over_ranks(ctx):
     """without ingest indices, records of different ranks share
     numbers and the class minimum would pick another rank's record.  More
