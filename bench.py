@@ -379,6 +379,72 @@ def chain_floor_ms(ctx, data, offs_t, sizes_t, sizes, method, kernel, alone=Fals
     return ms / max(cnt, 1), int(sizes[k])
 
 
+CLOCK_MAX_GHZ = 2.4  # MI355X_MICROARCH.md: peak engine clock
+SIMDS_PER_CU = 4
+
+
+def load_chain_ubench():
+    """Per-lane dependent-chain cost and per-SIMD throughput of the two
+    byte-serial recurrences (scripts/ubench/chain_ubench.hip, data in
+    registers, the library's own device code), from the newest committed
+    run (profiles/r06/chain_ubench.json), or None."""
+    path = os.path.join(ROOT, "profiles", "r06", "chain_ubench.json")
+    try:
+        runs = json.load(open(path))["runs"]
+    except (OSError, ValueError, KeyError):
+        return None
+    out = {"source": os.path.relpath(path, ROOT)}
+    for k in ("md5", "elf4", "elfc"):
+        rs = [r for r in runs if r["kernel"] == k]
+        if not rs:
+            return None
+        lat = min(rs, key=lambda r: r["waves_per_simd"])
+        out[k] = {"cycles_per_byte_lane": lat["cycles_per_byte_lane"],
+                  "simd_bytes_per_cycle": max(r["simd_bytes_per_cycle"] for r in rs),
+                  "clock_ghz_measured": lat["clock_ghz"]}
+    return out
+
+
+def chain_roof(method, sizes, ncu, kernel_ms):
+    """The hardware roof of a lane-per-file batch whose signature is a
+    byte-serial chain (MD5 / ELFHash: no intra-file parallel form): the
+    batch cannot end before its largest file's chain (that file's bytes x
+    the chain's cycles per byte on one lane) nor before every SIMD has
+    issued its share of the chain work (total bytes / the SIMD's best
+    bytes per cycle), both at the peak engine clock, with the cycle counts
+    measured by the chain microbenchmark.  Upper bounds: the data sits in
+    registers there and the CRC and the other hashes are not counted."""
+    ub = load_chain_ubench()
+    if ub is None:
+        return None
+    # sig_hash_kernel's big-file lanes (>= 4 MiB) run ELF in the 3-op chain
+    # form, its other lanes the asm 4-VALU form; md5_pair_kernel: MD5
+    big = method == F.SIG_HASH and int(sizes.max()) >= (4 << 20)
+    c = ub["md5"] if method == F.SIG_MD5 else ub["elfc" if big else "elf4"]
+    f = CLOCK_MAX_GHZ * 1e9
+    t_lat = float(sizes.max()) * c["cycles_per_byte_lane"] / f
+    t_thr = float(sizes.sum()) / (ncu * SIMDS_PER_CU * c["simd_bytes_per_cycle"] * f)
+    t = max(t_lat, t_thr)
+    return {"bound": "md5_chain" if method == F.SIG_MD5 else "elf_chain",
+            "peak": round(float(sizes.sum()) / t / 1e9, 3), "frac": round(t * 1e3 / kernel_ms, 4),
+            "roof_ms": round(t * 1e3, 3), "roof_term": "largest file's chain" if t_lat >= t_thr else "SIMD issue",
+            "chain_cycles_per_byte_lane": c["cycles_per_byte_lane"],
+            "simd_bytes_per_cycle": c["simd_bytes_per_cycle"], "clock_ghz": CLOCK_MAX_GHZ,
+            "ubench_clock_ghz": c["clock_ghz_measured"], "ubench_source": ub["source"]}
+
+
+def c1_sizes(rank):
+    """test/test_upload.c:32-39 (DEBUG): 65,560 files / 3,889,152,000 B of
+    the six gen_files sizes, in a seeded random order."""
+    mix = [(5 << 10, 50000), (50 << 10, 10000), (200 << 10, 5000), (1 << 20, 500),
+           (10 << 20, 50), (100 << 20, 10)]
+    sizes = np.concatenate([np.full(c, sz, np.int64) for sz, c in mix])
+    return sizes[np.random.default_rng(1 + 1000 * rank).permutation(sizes.size)]
+
+
+C1_WORKLOAD = "config 1: test_upload DEBUG mix (gen_files sizes 5K..100M, 65,560 files)"
+
+
 def c4_sizes(n):
     return np.full(n, 1 << 30, dtype=np.int64)
 
@@ -396,7 +462,7 @@ def batch_line(args, ctx, world, rank, dev, config, sizes, method, workload, ste
     CPU baseline on rank 0 at N = 1.  The batch is freed on return."""
     n = len(sizes)
     kernel, kname = KERNEL_OF[method]
-    if method == F.SIG_CRC_ONLY and n > 3 * 256 * torch.cuda.get_device_properties(dev).multi_processor_count:
+    if method == F.SIG_CRC_ONLY and n > ctx.crc_lane_min_files():
         # fdfs_gpu_sig_batch's lane path (more than 3 waves per SIMD of files)
         kname = "crc_lane_kernel<SAR> (+ crc_seg_kernel<SAR> for files >= 96 KiB)"
     workload += {F.SIG_CRC_ONLY: ", CRC32 only (check_file_duplicate=0)",
@@ -442,17 +508,23 @@ def batch_line(args, ctx, world, rank, dev, config, sizes, method, workload, ste
                         "the CRC's lane fold 1.5) at the ~1.6-1.75 of 2.4 GHz the chip holds under this "
                         "load; DESIGN.md 4.2, profiles/r05/issue_clock_c2.txt, profiles/r05/lane_fold_ab.txt")
     if config in ("c1", "c3", "c4") and method != F.SIG_CRC_ONLY:
-        # lane-per-file batches whose largest file's dependent chain (MD5
-        # / ELFHash) outlasts the HBM stream: the roof is that chain (c4
-        # with --method hash / md5: 1 GiB files, one lane each)
+        # lane-per-file batches whose dependent chains (MD5 / ELFHash)
+        # outlast the HBM stream: the roof is the chain's hardware cost
+        # (chain_roof); the largest file timed alone on
+        # the batch's own path stays beside it as a second figure
         fms, fbytes = chain_floor_ms(ctx, data, offs_t, sizes_t, sizes, method, kernel)
-        roof.update({"bound": "md5_chain" if method == F.SIG_MD5 else "elf_chain",
-                     "peak": round(per_launch / (fms * 1e-3) / 1e9, 1),
-                     "frac": round(fms / avg_ms, 4), "hbm_frac": round(achieved / HBM_PEAK_GBS, 4),
+        hw = chain_roof(method, sizes, torch.cuda.get_device_properties(dev).multi_processor_count, avg_ms)
+        roof.update({"hbm_frac": round(achieved / HBM_PEAK_GBS, 4),
                      "chain_floor_ms": round(fms, 3), "chain_floor_file_bytes": fbytes,
-                     "note": "peak = batch bytes over the time the same kernel takes for the "
-                             "largest file on the path it takes in the batch (one lane's serial "
-                             "chain; the other files of that timing batch are empty)"})
+                     "chain_floor_frac": round(fms / avg_ms, 4),
+                     "chain_floor_note": "the same kernel over a batch holding the largest file "
+                                         "alone on the path it takes in the batch (one lane's serial "
+                                         "chain; the other files of that timing batch are empty)"})
+        if hw:
+            roof.update(hw)
+        else:  # no committed microbenchmark run: the round-5 self-referential roof
+            roof.update({"bound": "md5_chain" if method == F.SIG_MD5 else "elf_chain",
+                         "peak": round(per_launch / (fms * 1e-3) / 1e9, 1), "frac": round(fms / avg_ms, 4)})
         if method == F.SIG_MD5 and config != "c4":
             ams, _ = chain_floor_ms(ctx, data, offs_t, sizes_t, sizes, method, kernel, alone=True)
             roof["md5_alone_floor_ms"] = round(ams, 3)
@@ -556,14 +628,9 @@ def main():
 
     if args.config in ("c1", "c2", "c3", "c4"):
         if args.config == "c1":
-            # test/test_upload.c:32-39 (DEBUG): 65,560 files / 3,889,152,000 B
-            # of the six gen_files sizes, in a seeded random order
-            mix = [(5 << 10, 50000), (50 << 10, 10000), (200 << 10, 5000), (1 << 20, 500),
-                   (10 << 20, 50), (100 << 20, 10)]
-            sizes = np.concatenate([np.full(c, sz, np.int64) for sz, c in mix])
-            sizes = sizes[np.random.default_rng(1 + 1000 * rank).permutation(sizes.size)]
+            sizes = c1_sizes(rank)
             method = F.SIG_HASH
-            workload = "config 1: test_upload DEBUG mix (gen_files sizes 5K..100M, 65,560 files)"
+            workload = C1_WORKLOAD
         elif args.config == "c2":
             sizes = C.small_files_sizes(args.files or 1_000_000, seed=1 + 1000 * rank)
             method = F.SIG_HASH
@@ -583,6 +650,19 @@ def main():
                               args.steps, args.warmup, threads, variant,
                               traffic_ok=args.align == 16 and not args.method))
         if args.config == "c2" and not args.files and not args.method and args.align == 16:
+            # configs 3 and 1 ride along, each with its
+            # own steps, roofline (the chain roof, hbm_frac beside it) and CPU
+            # baseline; config 3's 262 GB batch runs first, before the 100M
+            # dedup below reserves its workspace
+            keys = ("value", "unit", "ms_per_step", "scaling", "files_per_s", "roofline", "cpu_baseline",
+                    "dedup_files_per_s", "config")
+            ph = batch_line(args, ctx, world, rank, dev, "c3", C.photo_sizes(100_000, seed=3 + 1000 * rank),
+                            F.SIG_MD5, "config 3: 100000 files/GPU of U[1,4] MiB", min(args.steps, 3), 1,
+                            threads, variant, traffic_ok=True)
+            res["photos"] = {k: ph[k] for k in keys if k in ph}
+            um = batch_line(args, ctx, world, rank, dev, "c1", c1_sizes(rank), F.SIG_HASH, C1_WORKLOAD,
+                            min(args.steps, 3), 1, threads, variant, traffic_ok=True)
+            res["upload_mix"] = {k: um[k] for k in keys if k in um}
             # config 5's 100M-record dedup, strong-scaled over the ranks of
             # this run: the driver's 1/2/4/8-GPU runs of the default bench
             # give its scaling curve

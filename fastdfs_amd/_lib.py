@@ -45,6 +45,7 @@ EXPORTS = (
     "fdfs_gpu_dedup_group",
     "fdfs_gpu_set_timing",
     "fdfs_gpu_read_timing",
+    "fdfs_gpu_crc_lane_min_files",
     "fdfs_gpu_file_ids",
     "fdfs_gpu_parse_file_ids",
     "fdfs_gpu_trunk_pack",
@@ -153,6 +154,9 @@ def _bind(path: str) -> ctypes.CDLL:
     L.fdfs_gpu_dedup_group.argtypes = [vp, vp, u64, vp, vp, vp]
     L.fdfs_gpu_set_timing.restype = i32
     L.fdfs_gpu_set_timing.argtypes = [vp, i32]
+    if hasattr(L, "fdfs_gpu_crc_lane_min_files"):  # (absent from A/B builds of round 5)
+        L.fdfs_gpu_crc_lane_min_files.restype = i32
+        L.fdfs_gpu_crc_lane_min_files.argtypes = [vp, vp]
     L.fdfs_gpu_read_timing.restype = i32
     L.fdfs_gpu_read_timing.argtypes = [vp, i32, ctypes.POINTER(ctypes.c_double),
                                        ctypes.POINTER(ctypes.c_uint64)]

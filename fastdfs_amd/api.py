@@ -128,6 +128,13 @@ class Context:
                  "fdfs_gpu_read_timing")
         return ms.value, cnt.value
 
+    def crc_lane_min_files(self) -> int:
+        """fdfs_gpu_crc_lane_min_files: CRC-only batches of more files than
+        this take the lane path (crc_lane_kernel)."""
+        v = ctypes.c_uint64()
+        self._rc(self._L.fdfs_gpu_crc_lane_min_files(self._h, ctypes.byref(v)), "fdfs_gpu_crc_lane_min_files")
+        return v.value
+
     def inject_error(self, stream=None):
         """Test hook (fdfs_gpu_inject_error, contexts opened with
         test_hooks=True): queue a lane-path error on `stream`; a later call

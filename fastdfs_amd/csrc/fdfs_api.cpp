@@ -55,6 +55,10 @@ struct fdfs_gpu_ctx {
     void *xa = nullptr, *xb = nullptr;
     size_t xa_bytes = 0, xb_bytes = 0;
     uint64_t *dann = nullptr, *hann = nullptr;
+    // lane_err_note's per-slot events: a slot is reused only once the copy
+    // that last wrote it has landed
+    hipEvent_t err_ev[64] = {};
+    bool err_ev_rec[64] = {};
     // bytes the last dedup_global(_local) call moved between ranks: rows,
     // answers (fdfs_gpu_dedup_global_stats)
     uint64_t x_row_bytes = 0, x_ans_bytes = 0;
@@ -199,10 +203,28 @@ constexpr size_t kHannErrRing = 64 * kAnnTail + 64 * kAnnMax + 8;
 hipError_t lane_err_note(fdfs_gpu_ctx *ctx, const uint32_t *hist, hipStream_t st)
 {
     const uint32_t k = ctx->lane_err_next++ % kErrRing;  // under the context's mutex
+    // Slot k was last written by the copy of launch k - 64, possibly on
+    // another stream: wait for it before enqueueing this one, so that an
+    // older count can never land after a newer one (almost
+    // always long done).  Inside a stream capture nothing is recorded or
+    // waited on: a captured graph replays into the one slot it captured.
+    const bool cap = capturing(st);
+    if (!cap && ctx->err_ev_rec[k]) {
+        hipError_t e = hipEventSynchronize(ctx->err_ev[k]);
+        if (e != hipSuccess)
+            return e;
+    }
     hipError_t e = fdfs::launch_lane_err_count(hist ? hist + fdfs::kLaneErrWord : nullptr, ctx->dann + kAnnErrCount,
                                                ctx->dann + kAnnErrRing + k, st);
     if (e == hipSuccess)
         e = hipMemcpyAsync(ctx->hann + kHannErrRing + k, ctx->dann + kAnnErrRing + k, 8, hipMemcpyDeviceToHost, st);
+    if (e == hipSuccess && !cap) {
+        if (!ctx->err_ev[k])
+            e = hipEventCreateWithFlags(&ctx->err_ev[k], hipEventDisableTiming);
+        if (e == hipSuccess)
+            e = hipEventRecord(ctx->err_ev[k], st);
+        ctx->err_ev_rec[k] = e == hipSuccess;
+    }
     return e;
 }
 
@@ -417,6 +439,9 @@ int fdfs_gpu_close(fdfs_gpu_ctx *ctx)
         (void)hipFree(ctx->d_tabs);
     if (ctx->ws_ev)
         (void)hipEventDestroy(ctx->ws_ev);
+    for (hipEvent_t e : ctx->err_ev)
+        if (e)
+            (void)hipEventDestroy(e);
     delete ctx;
     return 0;
 }
@@ -455,6 +480,14 @@ int fdfs_gpu_set_timing(fdfs_gpu_ctx *ctx, int enable)
         return EINVAL;
     std::lock_guard<std::recursive_mutex> lk(ctx->mu);
     ctx->timing = enable != 0;
+    return 0;
+}
+
+int fdfs_gpu_crc_lane_min_files(fdfs_gpu_ctx *ctx, uint64_t *min_files)
+{
+    if (!ctx || !min_files)
+        return EINVAL;
+    *min_files = (uint64_t)kCrcLaneMinFill * ctx->lat_files;
     return 0;
 }
 

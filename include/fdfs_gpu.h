@@ -386,6 +386,13 @@ int fdfs_gpu_comm_destroy(void *comm);
 int fdfs_gpu_set_timing(fdfs_gpu_ctx *ctx, int enable);
 int fdfs_gpu_read_timing(fdfs_gpu_ctx *ctx, int kernel, double *ms_out, uint64_t *launches_out);
 
+/* The CRC-only batch size above which fdfs_gpu_sig_batch hashes the files
+ * below 96 KiB one lane per file (crc_lane_kernel) instead of a wave per
+ * file: more than min_files files (three waves per SIMD of this device,
+ * kCrcLaneMinFill x CUs x 256).  Measurement only: bench.py names the kernel
+ * its CRC-only line times from it. */
+int fdfs_gpu_crc_lane_min_files(fdfs_gpu_ctx *ctx, uint64_t *min_files);
+
 /* ---- Formats that consume the file CRC, FastDHT routing, scrub ---------- */
 
 #define FDFS_FILENAME_BASE64_LENGTH 27  /* tracker/tracker_types.h:35 */

@@ -208,3 +208,78 @@ def test_plan_crc_pieces_balance():
         pcs = sorted((a, ln) for pr in plan for g, a, ln in pr if g == f)
         assert pcs[0][0] == 0 and sum(ln for _, ln in pcs) == 1 << 30
     assert plan_crc_pieces(np.array([], np.int64), 3) == [[], [], []]
+
+
+class _CommLibDouble:
+    """Test double of the two communicator calls Comm makes:
+    the unique id fails on rank 0 when `fail`, else is 128 known bytes;
+    comm_init records the id it was given."""
+
+    def __init__(self, rank, fail):
+        self.rank, self.fail, self.init_ids = rank, fail, []
+
+    def fdfs_gpu_comm_unique_id(self, buf):
+        import errno
+        if self.fail:
+            return errno.EIO
+        for k in range(len(buf)):
+            buf[k] = (7 * k + 1) & 0xFF
+        return 0
+
+    def fdfs_gpu_comm_init(self, h, uid, world, rank, out):
+        self.init_ids.append(bytes(uid))
+        return 0
+
+    def fdfs_gpu_comm_destroy(self, h):
+        return 0
+
+
+class _CtxDouble:
+    def __init__(self, L):
+        self._L, self._h, self.device = L, None, 0
+
+    def _rc(self, rc, where):
+        assert rc == 0, where
+
+
+def _comm_worker(rank, world, port, fail, out_q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from fastdfs_amd.api import Comm, FdfsGpuError
+        L = _CommLibDouble(rank, fail and rank == 0)
+        try:
+            Comm(_CtxDouble(L))
+            out_q.put((rank, "ok", L.init_ids))
+        except FdfsGpuError as e:
+            out_q.put((rank, f"FdfsGpuError {e.errno}", L.init_ids))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("fail", [True, False])
+def test_comm_rank0_failure_reaches_every_rank(fail):
+    """api.Comm broadcasts rank 0's communicator id with a status byte: when
+    fdfs_gpu_comm_unique_id fails on rank 0, every rank raises FdfsGpuError
+    (EIO) and none calls fdfs_gpu_comm_init (none waits in it for a rank that
+    will not come); otherwise every rank initialises with rank 0's id.
+    gloo, world 3, the two library calls replaced by a test double."""
+    world = 3
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_comm_worker, args=(r, world, port, fail, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    got = {r: (what, ids) for r, what, ids in (q.get(timeout=120) for _ in range(world))}
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    want = bytes((7 * k + 1) & 0xFF for k in range(128))
+    for r in range(world):
+        what, ids = got[r]
+        if fail:
+            assert what == "FdfsGpuError 5" and ids == [], (r, what)
+        else:
+            assert what == "ok" and ids == [want], (r, what)
