@@ -100,9 +100,10 @@ int main()
             ns /= blocks;
             const double per_lane = cyc / (iters * bytes_per_iter);  // cycles per byte on one lane
             printf("%s{\"kernel\": \"%s\", \"waves_per_simd\": %d, \"cycles_per_byte_lane\": %.4f, "
-                   "\"cycles_per_%s_lane\": %.2f, \"simd_bytes_per_cycle\": %.3f, \"clock_ghz\": %.3f}",
-                   first ? "" : ",\n", name, w, per_lane, md5 ? "block" : "byte",
-                   md5 ? cyc / iters : per_lane, 64.0 * w / per_lane, cyc / ns);
+                   "\"cycles_per_step_lane\": %.2f, \"bytes_per_step\": %d, \"simd_bytes_per_cycle\": %.3f, "
+                   "\"clock_ghz\": %.3f}",
+                   first ? "" : ",\n", name, w, per_lane, cyc / iters, (int)bytes_per_iter, 64.0 * w / per_lane,
+                   cyc / ns);
             first = false;
         }
     }
