@@ -112,6 +112,78 @@ __global__ __launch_bounds__(256) void k_lane(const uint8_t *base, const uint64_
     out[i] = acc.x ^ acc.y ^ acc.z ^ acc.w;
 }
 
+// Mode glds (round 6): the 64 files' 128-byte rounds through a
+// per-wave LDS ring of R slots of 8 KiB by LDS-DMA (global_load_lds_dwordx4,
+// counted vmcnt waits in inline asm, no load registers): instruction q loads
+// files 8q .. 8q + 7, lanes 8j + i the pieces of file 8q + j (one 128-byte
+// line per 8 lanes), the piece order rotated by the file (f >> 1) so that
+// the 64 lanes' ds_read_b128 of one piece index are conflict-free; each lane
+// then reads its own file's 8 pieces from LDS and XORs them.
+template <int R, bool NT>
+__global__ __launch_bounds__(256) void k_glds(const uint8_t *base, const uint64_t *offs, const uint32_t *sizes,
+                                              const uint32_t *order, uint32_t n, uint32_t *out)
+{
+    extern __shared__ __attribute__((aligned(16))) uint8_t ring[];
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    uint8_t *my = ring + (size_t)wv * R * 8192;
+    const uint32_t w = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+    if (w * 64 >= n)
+        return;
+    const uint32_t myf = order[min(w * 64 + lane, n - 1)];
+    const uint32_t mysz = sizes[myf];
+    uint32_t mx = mysz;
+    for (int o = 32; o; o >>= 1)
+        mx = max(mx, (uint32_t)__shfl_xor((int)mx, o));
+    const uint64_t myoff = offs[myf];
+    const int i = lane & 7, j = lane >> 3;
+    uint64_t fo[8];
+    uint32_t fs[8], pc[8];
+#pragma unroll
+    for (int q = 0; q < 8; q++) {
+        const int f = 8 * q + j;
+        fo[q] = __shfl(myoff, f);
+        fs[q] = __shfl(mysz, f);
+        pc[q] = ((i + (f >> 1)) & 7) * 16;  // the piece this lane loads for file f
+    }
+    const uint32_t rounds = (mx + 127) / 128;
+    auto issue = [&](uint32_t r, int slot) {
+#pragma unroll
+        for (int q = 0; q < 8; q++) {
+            const uint32_t pos = r * 128 + pc[q];
+            const uint8_t *p = base + fo[q] + (pos + 16 <= fs[q] ? pos : 0);
+            const uint32_t dst = (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) void *)(my + slot * 8192 + q * 1024);
+            if (NT)
+                asm volatile("s_nop 0\n\tglobal_load_lds_dwordx4 %0, off nt" : : "v"(p), "{m0}"(dst) : "memory");
+            else
+                asm volatile("s_nop 0\n\tglobal_load_lds_dwordx4 %0, off" : : "v"(p), "{m0}"(dst) : "memory");
+        }
+    };
+#pragma unroll
+    for (int s = 0; s < R - 1; s++)
+        issue(s, s);
+    uint4 acc = make_uint4(0, 0, 0, 0);
+    int slot = 0;
+    for (uint32_t r = 0; r < rounds; r++) {
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        issue(r + R - 1, (slot + R - 1) % R);
+        if constexpr (R == 2)
+            asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+        else if constexpr (R == 3)
+            asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+        else
+            asm volatile("s_waitcnt vmcnt(24)" ::: "memory");
+        const uint8_t *row = my + slot * 8192 + lane * 128;
+#pragma unroll
+        for (int v = 0; v < 8; v++) {
+            const uint4 x = *reinterpret_cast<const uint4 *>(row + ((v - (lane >> 1)) & 7) * 16);
+            acc.x ^= x.x; acc.y ^= x.y; acc.z ^= x.z; acc.w ^= x.w;
+        }
+        slot = (slot + 1) % R;
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    out[w * 64 + lane] = acc.x ^ acc.y ^ acc.z ^ acc.w;
+}
+
 int main()
 {
     setvbuf(stdout, NULL, _IONBF, 0);
@@ -156,6 +228,10 @@ int main()
     run("c64pf8x16", [&] { hipLaunchKernelGGL((k_coal_pf<64, 8, 16>), dim3(g), dim3(256), 0, 0, d_base, d_offs, d_sizes, d_order, n, d_out); });
     run("c64pf16x16", [&] { hipLaunchKernelGGL((k_coal_pf<64, 16, 16>), dim3(g), dim3(256), 0, 0, d_base, d_offs, d_sizes, d_order, n, d_out); });
     run("c128pf8x8", [&] { hipLaunchKernelGGL((k_coal_pf<128, 8, 8>), dim3(g), dim3(256), 0, 0, d_base, d_offs, d_sizes, d_order, n, d_out); });
+    run("glds R2", [&] { hipLaunchKernelGGL((k_glds<2, false>), dim3(g), dim3(256), 4 * 2 * 8192, 0, d_base, d_offs, d_sizes, d_order, n, d_out); });
+    run("glds R2 nt", [&] { hipLaunchKernelGGL((k_glds<2, true>), dim3(g), dim3(256), 4 * 2 * 8192, 0, d_base, d_offs, d_sizes, d_order, n, d_out); });
+    run("glds R3 nt", [&] { hipLaunchKernelGGL((k_glds<3, true>), dim3(g), dim3(256), 4 * 3 * 8192, 0, d_base, d_offs, d_sizes, d_order, n, d_out); });
+    run("glds R4 nt", [&] { hipLaunchKernelGGL((k_glds<4, true>), dim3(g), dim3(256), 4 * 4 * 8192, 0, d_base, d_offs, d_sizes, d_order, n, d_out); });
     run("coal1024", [&] { hipLaunchKernelGGL(k_coal<1024>, dim3(g), dim3(256), 0, 0, d_base, d_offs, d_sizes, d_order, n, d_out); });
     // identity order (a wave's 64 files adjacent in memory)
     for (uint32_t i = 0; i < n; i++) order[i] = i;
