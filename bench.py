@@ -298,10 +298,10 @@ SQ_KERNEL = {"c2": ("sig_hash_kernel<true, false>", "sig_hash_kernel<true, 0, 0"
 
 def load_valu(config: str, avg_ms: float):
     """VALU issue of the dominant kernel: SQ_INSTS_VALU per launch from the
-    newest committed rocprofv3 --pmc pass (profiles/r05, else r04, r03, r02,
+    newest committed rocprofv3 --pmc pass (profiles/r06, else r05, r04, r03, r02,
     r01, pmc_sq_<config>.txt; the count does not depend on timing) over the
     live kernel time, in int32 lane-ops/s against VALU_PEAK_TOPS."""
-    for rnd in ("r05", "r04", "r03", "r02", "r01"):
+    for rnd in ("r06", "r05", "r04", "r03", "r02", "r01"):
         path = os.path.join(ROOT, "profiles", rnd, f"pmc_sq_{config}.txt")
         try:
             for line in open(path):
