@@ -4,7 +4,7 @@
 # Usage: TAG=r05 PART=tests|bench|stats|pmc bash scripts/gpu_round.sh
 #        (results under gpurun_out/round_$TAG; PART=all runs every part)
 export TMPDIR=/tmp
-TAG=${TAG:-r05}
+TAG=${TAG:-r06}
 PART=${PART:-all}
 O=gpurun_out/round_$TAG
 mkdir -p $O
@@ -35,7 +35,9 @@ if part bench; then
   for c in c1 c2 c3 c4 c5 c4_hash c4_md5 c2_crc; do tail -1 $O/bench_$c.log | cut -c1-300; done
 fi
 if part stats; then
-  step stats_c2 600 rocprofv3 --kernel-trace --stats -d $O/stats_c2 -o run --output-format csv -- $B --steps 10 --warmup 3 || exit $?
+  # config 2 alone (--files: without the default line's sub-lines, whose
+  # sig_hash_kernel / md5_pair_kernel dispatches would mix into its figures)
+  step stats_c2 600 rocprofv3 --kernel-trace --stats -d $O/stats_c2 -o run --output-format csv -- $B --config c2 --files 1000000 --steps 10 --warmup 3 || exit $?
   step stats_c3 600 rocprofv3 --kernel-trace --stats -d $O/stats_c3 -o run --output-format csv -- $B --config c3 --steps 2 --warmup 1 || exit $?
   step stats_c4 600 rocprofv3 --kernel-trace --stats -d $O/stats_c4 -o run --output-format csv -- $B --config c4 $S || exit $?
   step stats_c5 600 rocprofv3 --kernel-trace --stats -d $O/stats_c5 -o run --output-format csv -- $B --config c5 $S || exit $?
@@ -44,12 +46,13 @@ if part stats; then
 fi
 if part pmc; then
   for c in c2 c3 c4 c5; do
-    step fetch_$c 300 rocprofv3 --pmc FETCH_SIZE -d $O/fetch_$c -o run --output-format csv -- $B --config $c --steps 1 --warmup 1 || exit $?
-    step write_$c 300 rocprofv3 --pmc WRITE_SIZE -d $O/write_$c -o run --output-format csv -- $B --config $c --steps 1 --warmup 1 || exit $?
+    F=""; [ $c = c2 ] && F="--files 1000000"  # config 2 alone (no sub-lines)
+    step fetch_$c 300 rocprofv3 --pmc FETCH_SIZE -d $O/fetch_$c -o run --output-format csv -- $B --config $c $F --steps 1 --warmup 1 || exit $?
+    step write_$c 300 rocprofv3 --pmc WRITE_SIZE -d $O/write_$c -o run --output-format csv -- $B --config $c $F --steps 1 --warmup 1 || exit $?
   done
   # issue picture (scripts/pmc_clock.py: clock, SIMD issue occupancy)
   SQ="SQ_WAVES SQ_WAVE_CYCLES SQ_ACTIVE_INST_ANY SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_MFMA GRBM_GUI_ACTIVE"
-  step sq_c2 300 rocprofv3 --pmc $SQ -d $O/sq_c2 -o run --output-format csv -- $B --steps 2 --warmup 1 || exit $?
+  step sq_c2 300 rocprofv3 --pmc $SQ -d $O/sq_c2 -o run --output-format csv -- $B --config c2 --files 1000000 --steps 2 --warmup 1 || exit $?
   step sq_c3 600 rocprofv3 --pmc $SQ -d $O/sq_c3 -o run --output-format csv -- $B --config c3 --steps 1 --warmup 1 || exit $?
   step sq_c4 300 rocprofv3 --pmc $SQ -d $O/sq_c4 -o run --output-format csv -- $B --config c4 --steps 2 --warmup 1 || exit $?
 fi
