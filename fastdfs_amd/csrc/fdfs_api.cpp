@@ -8,6 +8,7 @@
 #include <cerrno>
 #include <cstdio>
 #include <cstring>
+#include <memory>
 #include <mutex>
 #include <new>
 #include <vector>
@@ -1600,7 +1601,16 @@ int fdfs_gpu_dedup_global(fdfs_gpu_ctx *ctx, void *comm, const uint8_t *sig, con
         return EINVAL;
     }
     ctx->x_row_bytes = ctx->x_ans_bytes = 0;
+    // the host-side plan and answer-count matrices (64 KB together: heap,
+    // not a daemon thread's stack), before any collective, so that a failed
+    // allocation is announced like any local error
+    std::unique_ptr<DgPlan> plp(new (std::nothrow) DgPlan);
+    std::unique_ptr<DgAns> anp(new (std::nothrow) DgAns);
     int err = dg_check(sig, gidx, n, rep_out, ref_out, nranks);
+    if (!err && (!plp || !anp)) {
+        std::snprintf(ctx->err, sizeof(ctx->err), "dedup_global: host allocation");
+        err = ENOMEM;
+    }
     if (!err)
         err = ensure_buf(ctx, &ctx->xa, &ctx->xa_bytes, dg_a_bytes(n, nranks), st);
     // room for the own rows the bucket pass writes in place (<= n of them)
@@ -1637,7 +1647,9 @@ int fdfs_gpu_dedup_global(fdfs_gpu_ctx *ctx, void *comm, const uint8_t *sig, con
     if ((e = hipMemcpyAsync(hall, all, 8 * w * nranks, hipMemcpyDeviceToHost, st)) != hipSuccess ||
         (e = hipStreamSynchronize(st)) != hipSuccess)
         return fail(ctx, e, "dedup_global announcements");
-    DgPlan pl;
+    if (!plp)
+        return ENOMEM;  // announced above: every rank returns
+    DgPlan &pl = *plp;
     dg_plan(hall, nranks, pl);
     if (pl.err)
         return dg_plan_error(ctx, pl, me);
@@ -1697,11 +1709,7 @@ int fdfs_gpu_dedup_global(fdfs_gpu_ctx *ctx, void *comm, const uint8_t *sig, con
         if ((e = hipMemcpyAsync(hans, dans, 4 * (size_t)nranks * nranks, hipMemcpyDeviceToHost, st)) != hipSuccess ||
             (e = hipStreamSynchronize(st)) != hipSuccess)
             return fail(ctx, e, "dedup_global answer counts");
-        DgAns *an = new (std::nothrow) DgAns;
-        if (!an) {
-            std::snprintf(ctx->err, sizeof(ctx->err), "dedup_global: host allocation");
-            return EIO;  // the other ranks are past the point of a common error
-        }
+        DgAns *an = anp.get();
         an->load(hans, nranks);
         sends.clear();
         recvs.clear();
@@ -1714,7 +1722,6 @@ int fdfs_gpu_dedup_global(fdfs_gpu_ctx *ctx, void *comm, const uint8_t *sig, con
             if (q != me && an->a[q][me])
                 recvs.push_back({q, reinterpret_cast<char *>(s.back) + 16 * an->boff(me, q), 16 * an->a[q][me]});
         nb = an->recv_total(me, nranks);
-        delete an;
         if ((rc = dg_nccl_group(ctx, c, sends, recvs, st)))
             return rc;
     }
