@@ -79,6 +79,128 @@ __device__ __forceinline__ uint32_t and_xor80(uint32_t a, uint32_t m)
     return __builtin_amdgcn_bitop3_b32(a, m, 0x80808080u, 0x6a);
 }
 
+// ELFHash_ex of one big file on a workgroup of its own (one-shot batches of
+// at most lat_files files with at most chain_cap big files; sig_hash_kernel's
+// first workgroups).  A lane alone on its SIMD issues about one instruction
+// per 4 cycles, so the chain lane's own byte extraction and loads are time on
+// the chain: here wave 1 puts the file's bytes one per dword into an LDS ring
+// (two slots of 2 KiB of file, 32 coalesced byte loads per lane per slot) and
+// wave 0 runs the three dependent VALU per byte alone (v_lshl_add_u32 with
+// the byte, shift, v_bitop3), reading each 64 bytes' dwords one group ahead.
+// CRC, simple_hash and Time33 of a big file come from the segmented kernels
+// (big_patch_kernel); this writes the signature's size and ELF fields and
+// codes[1].  Waves 2 and 3 only keep the barrier count.
+constexpr uint32_t kElfSlot = 2048;  // file bytes per LDS slot (8 KiB of byte-dwords)
+
+template <bool SAR>
+__device__ __forceinline__ void elf_byte(uint32_t b, uint32_t &e, uint32_t &y)
+{
+    const uint32_t t = (e << 4) + b;
+    y = SAR ? (uint32_t)((int32_t)t >> 24) : (t >> 24);
+    e = t ^ (y & 0xFFFFFFF0u);  // dirty top nibble (elf_exact_after)
+}
+
+template <bool SAR>
+__device__ __forceinline__ void elf_chain_wg(const uint8_t *p, uint64_t L, uint32_t f, uint32_t *ring,
+                                             uint8_t *sig_out, int32_t *codes_out)
+{
+    const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
+    const uint64_t nslots = uniform64((L + kElfSlot - 1) / kElfSlot);
+    if (wv == 1) {
+        auto fill = [&](uint32_t *slot, uint64_t s) {
+            const uint8_t *q = p + s * kElfSlot;
+            const uint64_t nb = L - s * kElfSlot;  // > 0
+#pragma unroll
+            for (int j0 = 0; j0 < (int)(kElfSlot / 64); j0 += 16) {
+                uint32_t v[16];
+#pragma unroll
+                for (int u = 0; u < 16; u++) {
+                    const uint32_t k = (j0 + u) * 64 + lane;
+                    v[u] = k < nb ? q[k] : 0u;
+                }
+#pragma unroll
+                for (int u = 0; u < 16; u++)
+                    slot[(j0 + u) * 64 + lane] = v[u];
+            }
+        };
+        if (nslots)
+            fill(ring, 0);
+        __syncthreads();
+        for (uint64_t s = 0; s < nslots; s++) {
+            if (s + 1 < nslots)
+                fill(ring + ((s + 1) & 1) * kElfSlot, s + 1);
+            __syncthreads();
+        }
+        return;
+    }
+    if (wv != 0) {
+        __syncthreads();
+        for (uint64_t s = 0; s < nslots; s++)
+            __syncthreads();
+        return;
+    }
+    __builtin_amdgcn_s_setprio(3);
+    // the same chain on every lane: an opaque per-lane zero keeps it in VGPRs
+    // (hipcc would run a wave-uniform chain on the scalar unit, with a
+    // v_readfirstlane per step)
+    uint32_t z;
+    asm volatile("v_mov_b32 %0, 0" : "=v"(z));
+    uint32_t e = z, y = 0x80000000u;  // INIT_HASH_CODES4's 0; y < 0: exact as it stands
+    __syncthreads();
+    for (uint64_t s = 0; s < nslots; s++) {
+        const uint4 *R = reinterpret_cast<const uint4 *>(ring + (s & 1) * kElfSlot);
+        const uint64_t rem = L - s * kElfSlot;
+        const uint32_t nb = (uint32_t)uniform64(rem < kElfSlot ? rem : kElfSlot);
+        const uint32_t ng = nb >> 6;  // whole 64-byte groups
+        // group g's steps from cur while a quarter of group g + 1's reads
+        // goes out before each quarter's steps (at most 8 LDS reads
+        // outstanding: lgkmcnt counts to 15); two buffers in turn, no copies
+        auto group = [&](const uint4 (&cur)[16], uint4 (&nxt)[16], const uint4 *N) {
+#pragma unroll
+            for (int h = 0; h < 4; h++) {
+#pragma unroll
+                for (int k = 4 * h; k < 4 * h + 4; k++)
+                    nxt[k] = N[k];
+                __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+                for (int k = 4 * h; k < 4 * h + 4; k++) {
+                    elf_byte<SAR>(cur[k].x, e, y);
+                    elf_byte<SAR>(cur[k].y, e, y);
+                    elf_byte<SAR>(cur[k].z, e, y);
+                    elf_byte<SAR>(cur[k].w, e, y);
+                }
+                __builtin_amdgcn_sched_barrier(0);
+            }
+        };
+        uint4 A[16], B[16];
+#pragma unroll
+        for (int k = 0; k < 16; k++)
+            A[k] = R[k];
+        uint32_t g = 0;
+        for (; g + 2 <= ng; g += 2) {
+            group(A, B, R + 16 * (g + 1));
+            group(B, A, R + 16 * (g + 2 < ng ? g + 2 : 0));
+        }
+        if (g < ng)  // an odd group count: the last group (the reads go to B unused)
+            group(A, B, R);
+        const uint32_t *Rw = reinterpret_cast<const uint32_t *>(R);
+        for (uint32_t k = ng << 6; k < nb; k++)  // the slot's last < 64 bytes (the file's end)
+            elf_byte<SAR>(Rw[k], e, y);
+        __syncthreads();
+    }
+    e = elf_exact_after(e, y);
+    if (lane == 0) {
+        if (sig_out) {  // be64 size at 0, be32 ELF at 12 (big_patch_kernel writes the CRC, simple, Time33)
+            uint32_t *sp = reinterpret_cast<uint32_t *>(sig_out + 24ull * f);
+            sp[0] = bswap32((uint32_t)(L >> 32));
+            sp[1] = bswap32((uint32_t)L);
+            sp[3] = bswap32(e);
+        }
+        if (codes_out)
+            codes_out[4ull * f + 1] = (int32_t)e;
+    }
+}
+
 // ST (fdfs_gpu_update_batch): the lane continues the chunk's
 // StorageFileContext-shaped state (crc32, file_hash_codes) instead of
 // INIT_HASH_CODES4 and writes it back unfinalised; every step above is a
@@ -94,9 +216,10 @@ __global__ __launch_bounds__(kHashBlock) __attribute__((amdgpu_waves_per_eu(1)))
     const uint64_t *__restrict__ sizes, const uint32_t *__restrict__ order, uint32_t n,
     const DevTables *__restrict__ tabs, const uint64_t *__restrict__ big_min_p,
     uint32_t *__restrict__ crc_out, uint8_t *__restrict__ sig_out, int32_t *__restrict__ codes_out,
-    fdfs_gpu_file_state *__restrict__ states, const uint32_t *__restrict__ sidx)
+    fdfs_gpu_file_state *__restrict__ states, const uint32_t *__restrict__ sidx,
+    const uint32_t *__restrict__ nbig_p, uint32_t chain_slots)
 {
-    __shared__ uint32_t sD[16 * 256];
+    __shared__ __attribute__((aligned(16))) uint32_t sD[16 * 256];  // also elf_chain_wg's ring
     __shared__ uint32_t sT[256];
     constexpr int SV = 8;             // vectors per step: one 128-byte line
     constexpr int NSETS = 2;          // register sets of loads in flight
@@ -121,8 +244,23 @@ __global__ __launch_bounds__(kHashBlock) __attribute__((amdgpu_waves_per_eu(1)))
     __syncthreads();
     const int brow = ((threadIdx.x & 63) >> 4) == ((threadIdx.x & 15) >> 2) ? (threadIdx.x & 3) : 4;
 
+    // The first chain_slots workgroups: big file i < *nbig (when *nbig <=
+    // chain_slots) on workgroup i (elf_chain_wg); the lanes skip those files.
+    uint32_t nchain = 0;
+    if (!ST && chain_slots) {
+        const uint32_t nb = __builtin_amdgcn_readfirstlane(*nbig_p);
+        nchain = nb <= chain_slots ? nb : 0;
+        if (blockIdx.x < chain_slots) {
+            if (blockIdx.x < nchain) {
+                const uint32_t fc = order[blockIdx.x];
+                if (fc < n)  // else a stale order entry (flagged by big_plan_kernel)
+                    elf_chain_wg<SAR>(base + offs[fc], sizes[fc], fc, sD, sig_out, codes_out);
+            }
+            return;
+        }
+    }
     const int lane = threadIdx.x & 63;
-    const uint32_t wave0 = blockIdx.x * blockDim.x + (threadIdx.x & ~63u);
+    const uint32_t wave0 = (blockIdx.x - chain_slots) * blockDim.x + (threadIdx.x & ~63u);
     if (wave0 >= n)  // whole wave past the batch (wave-uniform: MFMAs below need every lane)
         return;
     const uint32_t i = wave0 + lane;
@@ -134,6 +272,8 @@ __global__ __launch_bounds__(kHashBlock) __attribute__((amdgpu_waves_per_eu(1)))
         valid = false;
         f = 0;
     }
+    if (nchain && valid && sizes[f] >= *big_min_p)  // a chain workgroup's file
+        valid = false;
     const uint64_t L = valid ? sizes[f] : 0;
     const uint8_t *p = valid ? base + offs[f] : safe;
     uint32_t c = 0xFFFFFFFFu;  // CRC32_XINIT (storage/storage_service.c:7149)
@@ -726,12 +866,14 @@ hipError_t launch_sig_hash(bool sar, const uint8_t *base, const uint64_t *offs,
                            const uint64_t *sizes, uint32_t n, const uint32_t *order,
                            const DevTables *tabs, const uint64_t *big_min, uint32_t *crc_out, uint8_t *sig_out,
                            int32_t *codes_out, fdfs_gpu_file_state *states, const uint32_t *sidx,
-                           hipStream_t st)
+                           hipStream_t st, const uint32_t *nbig, uint32_t chain_cap)
 {
-    const unsigned grid = (n + kHashBlock - 1) / kHashBlock;
+    // the chain workgroups first: as many as there can be big files
+    const uint32_t slots = (states || !nbig || !big_min) ? 0u : (n < chain_cap ? n : chain_cap);
+    const unsigned grid = slots + (n + kHashBlock - 1) / kHashBlock;
 #define HASH_LAUNCH(S, T)                                                                                \
     sig_hash_kernel<S, T><<<grid, kHashBlock, 0, st>>>(base, offs, sizes, order, n, tabs, big_min, crc_out, \
-                                                       sig_out, codes_out, states, sidx)
+                                                       sig_out, codes_out, states, sidx, nbig, slots)
     if (states)
         sar ? HASH_LAUNCH(true, true) : HASH_LAUNCH(false, true);
     else

@@ -72,11 +72,15 @@ hipError_t launch_crc_seg(bool sar, const uint8_t *base, const uint64_t *offs, c
                           uint32_t n, uint64_t *nseg, uint64_t *seg_first, uint64_t *bsum,
                           const DevTables *tabs, uint32_t *crc_out, unsigned ncu, hipStream_t st,
                           hipEvent_t ev0, hipEvent_t ev1);
+// chain_cap > 0 (one-shot batches of at most lat_files files, big files
+// offloaded): when big_plan_kernel's *nbig is at most chain_cap, each big
+// file's MD5 runs on a workgroup of its own (md5_chain_wg, fdfs_md5.hip).
 hipError_t launch_md5_stage(bool sar, const uint8_t *base, const uint64_t *offs,
                             const uint64_t *sizes, uint32_t n, const uint32_t *order,
                             const DevTables *tabs, const uint64_t *big_min, uint32_t *queue, uint32_t *crc_out,
                             uint8_t *sig_out, int32_t *codes_out, fdfs_gpu_file_state *states,
-                            const uint32_t *sidx, unsigned ncu, hipStream_t st);
+                            const uint32_t *sidx, unsigned ncu, hipStream_t st,
+                            const uint32_t *nbig = nullptr, uint32_t chain_cap = 0);
 // CRC32 only, one lane per file of a size-binned order (large batches of
 // files below *big_min; fdfs_hash.hip crc_lane_kernel).
 hipError_t launch_crc_lane(bool sar, const uint8_t *base, const uint64_t *offs, const uint64_t *sizes, uint32_t n,
@@ -86,7 +90,7 @@ hipError_t launch_sig_hash(bool sar, const uint8_t *base, const uint64_t *offs,
                            const uint64_t *sizes, uint32_t n, const uint32_t *order,
                            const DevTables *tabs, const uint64_t *big_min, uint32_t *crc_out, uint8_t *sig_out,
                            int32_t *codes_out, fdfs_gpu_file_state *states, const uint32_t *sidx,
-                           hipStream_t st);
+                           hipStream_t st, const uint32_t *nbig = nullptr, uint32_t chain_cap = 0);
 
 // chunked-update helpers (fdfs_stream.hip)
 hipError_t launch_state_init(fdfs_gpu_file_state *states, uint32_t n, hipStream_t st);

@@ -355,12 +355,143 @@ __device__ __forceinline__ void pair_barrier()
     asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
 }
 
+// ------------------------------------------- MD5 path, one workgroup per file
+//
+// A batch's few big files (at most chain_cap of them: config 4's 1 GiB
+// files) are each one serial chain, on one lane of one wave alone on its
+// SIMD, and such a wave issues about one instruction per 4 cycles: every
+// instruction it issues is time on the chain.  md5_compress spends five per
+// step, one of them the a + m + K sum off the chain.  Here a helper wave makes
+// those sums: its lane i computes K[i] + m[g(i)] of each block (g the RFC 1321
+// message index of step i), a slot ahead of the MD5 wave (two slots of 32
+// blocks in the tables' 16 KiB of LDS), which then runs four dependent
+// instructions per step
+// (md5_round_km) and reads each round's 16 sums one round ahead of its use.
+// 16.8 against 21.2 cycles per byte on one wave (profiles/r06/
+// chain_lds_ubench.json).  Every lane of the MD5 wave runs the same chain
+// (the LDS reads broadcast); lane 0 stores.  The file's CRC comes from
+// crc_seg_kernel (big_patch_kernel), as for any big file.
+static __device__ const uint32_t kMd5Kc[64] = {
+    0xd76aa478u, 0xe8c7b756u, 0x242070dbu, 0xc1bdceeeu, 0xf57c0fafu, 0x4787c62au, 0xa8304613u, 0xfd469501u,
+    0x698098d8u, 0x8b44f7afu, 0xffff5bb1u, 0x895cd7beu, 0x6b901122u, 0xfd987193u, 0xa679438eu, 0x49b40821u,
+    0xf61e2562u, 0xc040b340u, 0x265e5a51u, 0xe9b6c7aau, 0xd62f105du, 0x02441453u, 0xd8a1e681u, 0xe7d3fbc8u,
+    0x21e1cde6u, 0xc33707d6u, 0xf4d50d87u, 0x455a14edu, 0xa9e3e905u, 0xfcefa3f8u, 0x676f02d9u, 0x8d2a4c8au,
+    0xfffa3942u, 0x8771f681u, 0x6d9d6122u, 0xfde5380cu, 0xa4beea44u, 0x4bdecfa9u, 0xf6bb4b60u, 0xbebfbc70u,
+    0x289b7ec6u, 0xeaa127fau, 0xd4ef3085u, 0x04881d05u, 0xd9d4d039u, 0xe6db99e5u, 0x1fa27cf8u, 0xc4ac5665u,
+    0xf4292244u, 0x432aff97u, 0xab9423a7u, 0xfc93a039u, 0x655b59c3u, 0x8f0ccc92u, 0xffeff47du, 0x85845dd1u,
+    0x6fa87e4fu, 0xfe2ce6e0u, 0xa3014314u, 0x4e0811a1u, 0xf7537e82u, 0xbd3af235u, 0x2ad7d2bbu, 0xeb86d391u};
+
+__device__ __forceinline__ int md5_msg_index(int i)  // g(i), RFC 1321 3.4
+{
+    return i < 16 ? i : i < 32 ? (5 * i + 1) & 15 : i < 48 ? (3 * i + 5) & 15 : (7 * i) & 15;
+}
+
+constexpr uint32_t kChainSlotBlocks = 32;  // blocks per LDS slot: 32 x 64 sums = 8 KiB
+
+// ring: two slots, 16 KiB of the workgroup's LDS.  Both waves call it.
+__device__ __forceinline__ void md5_chain_wg(const uint8_t *p, uint64_t L, uint32_t f, bool helper, uint4 *ring,
+                                          uint8_t *sig_out, int32_t *codes_out)
+{
+    const int lane = threadIdx.x & 63;
+    const uint64_t nblk = L >> 6;
+    const uint64_t nslots = uniform64((nblk + kChainSlotBlocks - 1) / kChainSlotBlocks);
+    if (helper) {
+        const uint32_t kk = kMd5Kc[lane];
+        const uint8_t *src = p + 4 * md5_msg_index(lane);
+        auto fill = [&](uint4 *slot, uint64_t s) {
+            const uint64_t b0 = s * kChainSlotBlocks;
+            const uint32_t nb = (uint32_t)uniform64(nblk - b0 < kChainSlotBlocks ? nblk - b0 : kChainSlotBlocks);
+            uint32_t *w = reinterpret_cast<uint32_t *>(slot);
+            for (uint32_t j0 = 0; j0 < nb; j0 += 16) {
+                uint32_t v[16];
+#pragma unroll
+                for (int u = 0; u < 16; u++) {
+                    const uint64_t blk = b0 + j0 + u < nblk ? b0 + j0 + u : b0;  // past the end: re-read block b0
+                    __builtin_memcpy(&v[u], src + 64 * blk, 4);  // any alignment (unaligned memory mode)
+                }
+#pragma unroll
+                for (int u = 0; u < 16; u++)
+                    w[(j0 + u) * 64 + lane] = v[u] + kk;
+            }
+        };
+        if (nslots)
+            fill(ring, 0);
+        __syncthreads();
+        for (uint64_t s = 0; s < nslots; s++) {
+            if (s + 1 < nslots)
+                fill(ring + ((s + 1) & 1) * (kChainSlotBlocks * 16), s + 1);
+            __syncthreads();
+        }
+        return;
+    }
+    __builtin_amdgcn_s_setprio(3);
+    // Every lane holds the same state, which hipcc would otherwise keep in
+    // SGPRs (the LDS reads are wave-uniform) and run on the scalar unit with a
+    // v_readfirstlane per step; an opaque per-lane zero keeps it in VGPRs.
+    uint32_t z;
+    asm volatile("v_mov_b32 %0, 0" : "=v"(z));
+    uint32_t st[4] = {0x67452301u ^ z, 0xefcdab89u ^ z, 0x98badcfeu ^ z, 0x10325476u ^ z};  // my_md5_init
+    __syncthreads();
+    for (uint64_t s = 0; s < nslots; s++) {
+        const uint4 *R = ring + (s & 1) * (kChainSlotBlocks * 16);
+        const uint32_t nb = (uint32_t)uniform64(nblk - s * kChainSlotBlocks < kChainSlotBlocks
+                                                    ? nblk - s * kChainSlotBlocks : kChainSlotBlocks);
+        uint4 ga[4], gb[4];
+#pragma unroll
+        for (int k = 0; k < 4; k++)
+            ga[k] = R[k];
+        for (uint32_t j = 0; j < nb; j++) {
+            const uint4 *B = R + 16 * j;
+            const uint4 *N = R + (j + 1 < nb ? 16 * (j + 1) : 0);  // the next block's first round
+            uint32_t a = st[0], b = st[1], c = st[2], d = st[3];
+            // each round's sums are read while the round before is computed
+#pragma unroll
+            for (int k = 0; k < 4; k++)
+                gb[k] = B[4 + k];
+            __builtin_amdgcn_sched_barrier(0);
+            md5_round_km<0>(a, b, c, d, ga);
+            __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+            for (int k = 0; k < 4; k++)
+                ga[k] = B[8 + k];
+            __builtin_amdgcn_sched_barrier(0);
+            md5_round_km<1>(a, b, c, d, gb);
+            __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+            for (int k = 0; k < 4; k++)
+                gb[k] = B[12 + k];
+            __builtin_amdgcn_sched_barrier(0);
+            md5_round_km<2>(a, b, c, d, ga);
+            __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+            for (int k = 0; k < 4; k++)
+                ga[k] = N[k];
+            __builtin_amdgcn_sched_barrier(0);
+            md5_round_km<3>(a, b, c, d, gb);
+            __builtin_amdgcn_sched_barrier(0);
+            st[0] += a;
+            st[1] += b;
+            st[2] += c;
+            st[3] += d;
+        }
+        __syncthreads();
+    }
+    md5_finish(st, p + (nblk << 6), L);
+    if (lane == 0) {
+        if (sig_out)  // memcpy(sig + 8, md5 digest, 16) (storage/storage_service.c:119)
+            store_sig(sig_out + 24ull * f, L, st[0], st[1], st[2], st[3]);
+        if (codes_out)
+            reinterpret_cast<int4 *>(codes_out)[f] = make_int4((int)st[0], (int)st[1], (int)st[2], (int)st[3]);
+    }
+}
+
 template <bool SAR>
 __global__ __launch_bounds__(128) void md5_pair_kernel(
     const uint8_t *__restrict__ base, const uint64_t *__restrict__ offs,
     const uint64_t *__restrict__ sizes, const uint32_t *__restrict__ order, uint32_t n,
     const DevTables *__restrict__ tabs, const uint64_t *__restrict__ big_min_p, uint32_t *__restrict__ queue,
-    uint32_t *__restrict__ crc_out, uint8_t *__restrict__ sig_out, int32_t *__restrict__ codes_out)
+    uint32_t *__restrict__ crc_out, uint8_t *__restrict__ sig_out, int32_t *__restrict__ codes_out,
+    const uint32_t *__restrict__ nbig_p, uint32_t chain_cap)
 {
     constexpr int CH = kMd5Chunk;
     constexpr int PIECES = CH / 16;
@@ -369,7 +500,7 @@ __global__ __launch_bounds__(128) void md5_pair_kernel(
     constexpr int STRIDE = CH + 16;
     constexpr int BPR = CH / 64;
     static_assert(NLD == 8, "the asm waits below name 8 registers");
-    __shared__ uint32_t sD[16 * 256];
+    __shared__ __attribute__((aligned(16))) uint32_t sD[16 * 256];  // also md5_chain_wg's ring
     __shared__ uint32_t sT[256];
     __shared__ __attribute__((aligned(16))) uint8_t sbuf[2][64 * STRIDE];
     __shared__ uint32_t s_chunk;
@@ -384,6 +515,22 @@ __global__ __launch_bounds__(128) void md5_pair_kernel(
     const uint8_t *safe = reinterpret_cast<const uint8_t *>(tabs);
     const uint32_t K16 = tabs->t.K16;
     const uint64_t big_min = big_min_p ? *big_min_p : ~0ull;
+    // Big files (the first *nbig of the order) of a batch with at most
+    // chain_cap of them: workgroup i < nchain runs big file i's MD5 alone
+    // (md5_chain_wg; the tables' LDS is its ring), and the
+    // pairs skip those files.
+    uint32_t nchain = 0;
+    if (chain_cap && nbig_p) {
+        const uint32_t nb = __builtin_amdgcn_readfirstlane(*nbig_p);
+        nchain = nb <= chain_cap ? nb : 0;
+    }
+    if (blockIdx.x < nchain) {
+        const uint32_t f = order[blockIdx.x];
+        if (f >= n)  // a stale order entry (flagged by big_plan_kernel)
+            return;
+        md5_chain_wg(base + offs[f], sizes[f], f, loader, reinterpret_cast<uint4 *>(sD), sig_out, codes_out);
+        return;
+    }
     for (;;) {
         if (threadIdx.x == 64)
             s_chunk = atomicAdd(queue, 1u);
@@ -399,6 +546,8 @@ __global__ __launch_bounds__(128) void md5_pair_kernel(
             valid = false;
             f = 0;
         }
+        if (nchain && valid && sizes[f] >= big_min)  // a chain workgroup's file
+            valid = false;
         const uint64_t L = valid ? sizes[f] : 0;
         const uint8_t *p = valid ? base + offs[f] : safe;
         const uint64_t nblk = L >> 6;
@@ -557,7 +706,8 @@ hipError_t launch_md5_stage(bool sar, const uint8_t *base, const uint64_t *offs,
                             const uint64_t *sizes, uint32_t n, const uint32_t *order,
                             const DevTables *tabs, const uint64_t *big_min, uint32_t *queue, uint32_t *crc_out,
                             uint8_t *sig_out, int32_t *codes_out, fdfs_gpu_file_state *states,
-                            const uint32_t *sidx, unsigned ncu, hipStream_t st)
+                            const uint32_t *sidx, unsigned ncu, hipStream_t st,
+                            const uint32_t *nbig, uint32_t chain_cap)
 {
     if (ncu == 0)
         return hipErrorInvalidValue;
@@ -565,13 +715,17 @@ hipError_t launch_md5_stage(bool sar, const uint8_t *base, const uint64_t *offs,
     const uint32_t nw = (n + 63) / 64;
     if (queue && !states) {  // one-shot batches: the wave pairs (queue zeroed by the caller)
         const unsigned g = 4u * ncu;
-        const unsigned grid2 = g < nw ? g : nw;
+        // the pairs' grid, after the chain workgroups (as many as there can
+        // be big files; those past *nbig join the pairs)
+        if (!nbig || !big_min)
+            chain_cap = 0;
+        const unsigned grid2 = (g < nw ? g : nw) + (n < chain_cap ? n : chain_cap);
         if (sar)
             md5_pair_kernel<true><<<grid2, 128, 0, st>>>(base, offs, sizes, order, n, tabs, big_min, queue, crc_out,
-                                                         sig_out, codes_out);
+                                                         sig_out, codes_out, nbig, chain_cap);
         else
             md5_pair_kernel<false><<<grid2, 128, 0, st>>>(base, offs, sizes, order, n, tabs, big_min, queue, crc_out,
-                                                          sig_out, codes_out);
+                                                          sig_out, codes_out, nbig, chain_cap);
         return hipGetLastError();
     }
     unsigned grid = (n + kBlk - 1) / kBlk;

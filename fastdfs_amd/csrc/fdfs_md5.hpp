@@ -114,6 +114,43 @@ __device__ __forceinline__ void md5_compress(uint32_t st[4], const uint32_t m[16
     st[3] += d;
 }
 
+// One round (16 steps) of a block whose K[i] + m[g(i)] sums were made in
+// advance (md5_chain_wg's helper wave): q[u] holds steps 16 R + 4 u .. + 3.
+// With the sum given, the step is four dependent VALU (F, v_add3_u32,
+// rotate, add) and nothing off the chain: on one wave alone on its SIMD, 16.8
+// against 21.2 cycles per byte for md5_compress (profiles/r06/chain_lds_ubench.json).
+#define MD5_KSTEP(FN, a, b, c, d, km, s) a = (b) + rotl((a) + (km) + FN(b, c, d), s)
+template <int R>
+__device__ __forceinline__ void md5_round_km(uint32_t &a, uint32_t &b, uint32_t &c, uint32_t &d, const uint4 q[4])
+{
+    constexpr int S[4][4] = {{7, 12, 17, 22}, {5, 9, 14, 20}, {4, 11, 16, 23}, {6, 10, 15, 21}};
+#pragma unroll
+    for (int u = 0; u < 4; u++) {
+        if constexpr (R == 0) {
+            MD5_KSTEP(MD5_F, a, b, c, d, q[u].x, S[R][0]);
+            MD5_KSTEP(MD5_F, d, a, b, c, q[u].y, S[R][1]);
+            MD5_KSTEP(MD5_F, c, d, a, b, q[u].z, S[R][2]);
+            MD5_KSTEP(MD5_F, b, c, d, a, q[u].w, S[R][3]);
+        } else if constexpr (R == 1) {
+            MD5_KSTEP(MD5_G, a, b, c, d, q[u].x, S[R][0]);
+            MD5_KSTEP(MD5_G, d, a, b, c, q[u].y, S[R][1]);
+            MD5_KSTEP(MD5_G, c, d, a, b, q[u].z, S[R][2]);
+            MD5_KSTEP(MD5_G, b, c, d, a, q[u].w, S[R][3]);
+        } else if constexpr (R == 2) {
+            MD5_KSTEP(MD5_H, a, b, c, d, q[u].x, S[R][0]);
+            MD5_KSTEP(MD5_H, d, a, b, c, q[u].y, S[R][1]);
+            MD5_KSTEP(MD5_H, c, d, a, b, q[u].z, S[R][2]);
+            MD5_KSTEP(MD5_H, b, c, d, a, q[u].w, S[R][3]);
+        } else {
+            MD5_KSTEP(MD5_I, a, b, c, d, q[u].x, S[R][0]);
+            MD5_KSTEP(MD5_I, d, a, b, c, q[u].y, S[R][1]);
+            MD5_KSTEP(MD5_I, c, d, a, b, q[u].z, S[R][2]);
+            MD5_KSTEP(MD5_I, b, c, d, a, q[u].w, S[R][3]);
+        }
+    }
+}
+#undef MD5_KSTEP
+
 // The final block(s) after the L & 63 pending bytes (RFC 1321 3.1-3.2):
 // m holds those bytes (any value past them); 0x80, zero pad and the 64-bit
 // bit count are put in and one or two blocks compressed.

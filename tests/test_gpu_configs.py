@@ -91,6 +91,33 @@ def test_config3_full_batch(oracle, ctxs):
     torch.cuda.empty_cache()
 
 
+def test_config1_upload_mix(oracle, ctxs):
+    """Config 1 at its bench size, the batch bench.py's upload_mix line hashes
+    on rank 0: test/test_upload.c:32-39's DEBUG mix of the gen_files sizes
+    (65,560 files, 3.89 GB; sizes permuted with seed 1, bytes seed 2).  HASH:
+    the ten 100 MB and fifty 10 MB files (>= kBigCrcMin) run their ELF chains
+    on workgroups of their own, their CRC / simple / Time33 on the segmented
+    kernels, the rest on the lanes; MD5: the wave pairs.  Every file's CRC and
+    24-byte signature against the oracle (storage/storage_dio.c:465-515)."""
+    from oracle_windows import whole_batch
+    torch.cuda.empty_cache()
+    mix = [(5 << 10, 50000), (50 << 10, 10000), (200 << 10, 5000), (1 << 20, 500), (10 << 20, 50),
+           (100 << 20, 10)]
+    sizes = np.concatenate([np.full(c, sz, np.int64) for sz, c in mix])
+    sizes = sizes[np.random.default_rng(1).permutation(sizes.size)]
+    data, offs_t, sizes_t = C.device_batch(sizes, seed=2, device="cuda:0")
+    offs = offs_t.cpu().numpy()
+    for method in (1, 2):
+        crc, sig, _ = ctxs[0].sig_batch(data, offs_t, sizes_t, method=method, check_bounds=False)
+        torch.cuda.synchronize()
+        crc_np, sig_np = crc.cpu().numpy().view(np.uint32), sig.cpu().numpy()
+        ocrc, osig = whole_batch(oracle, data, offs, sizes, method)
+        bad = np.flatnonzero((crc_np != ocrc) | (sig_np != osig).any(axis=1))
+        assert bad.size == 0, (method, bad.size, bad[:8], sizes[bad[:8]])
+    del data, crc, sig
+    torch.cuda.empty_cache()
+
+
 C5_TOTAL = 100_000_000
 
 

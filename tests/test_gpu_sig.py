@@ -209,6 +209,25 @@ def test_adaptive_offload_threshold(oracle, ctxs, variant, top):
     _check(oracle, ctxs[variant], variant, buf, offs, sz, methods=(1, 2))
 
 
+@pytest.mark.parametrize("variant", [0, 1])
+def test_chain_workgroups(oracle, ctxs, variant):
+    """The serial chain of a small batch's few big files on workgroups of
+    their own: MD5 (md5_chain_wg: a helper wave makes each step's K + m sum
+    in LDS, two slots of 32 blocks) and ELFHash_ex (elf_chain_wg: the bytes
+    one per dword in LDS, two slots of 2 KiB), the CRC / simple / Time33 of
+    those files from the segmented kernels: block counts odd, a slot boundary
+    +- 1, byte-aligned starts, tails of 0-63 bytes, beside small files on the
+    lanes.  Reference: storage/storage_dio.c:465-512 (CALC_HASH_CODES4,
+    my_md5_update / my_md5_final)."""
+    rng = np.random.default_rng(71 + variant)
+    big = [(4 << 20) + 4095, (3 << 20) + 65, (2 << 20) - 1, 12_345_678, (2 << 20) + 2048 - 64,
+           (2 << 20) + 2048 + 64, 6 << 20]
+    sizes = np.concatenate([big, rng.integers(0, 5000, 60), [0, 63, 64, 65]]).astype(np.int64)
+    rng.shuffle(sizes)
+    buf, offs, sz = _packed(sizes, 1, rng)
+    _check(oracle, ctxs[variant], variant, buf, offs, sz, methods=(1, 2))
+
+
 def test_crc_paths_agree_at_scale(oracle, ctxs):
     """Config 2 at full size, the batch bench.py hashes on rank 0 (1M files of
     U[4, 64] KiB, sizes seed 1, bytes seed 2, 16-byte aligned: ~34.8 GB in
