@@ -25,7 +25,7 @@ constexpr uint64_t kFile = 256ull << 20;  // bytes per lane
 constexpr int kLanes = 8;
 
 template <int NS>
-__global__ void k_chain(const uint8_t *src, uint64_t bytes, uint32_t *out, Stamp *st)
+__global__ __launch_bounds__(64) void k_chain(const uint8_t *src, uint64_t bytes, uint32_t *out, Stamp *st)
 {
     constexpr int SV = 8;
     const int lane = threadIdx.x & 63;
@@ -113,7 +113,11 @@ int main()
                 hipLaunchKernelGGL(k_chain<2>, dim3(1), dim3(64), 0, 0, src, bytes, out, st);
             else
                 hipLaunchKernelGGL(k_chain<4>, dim3(1), dim3(64), 0, 0, src, bytes, out, st);
-            hipDeviceSynchronize();
+            const hipError_t err = hipDeviceSynchronize();
+            if (err != hipSuccess) {  // stop at the first failure: nothing more runs on the GPU
+                printf("\n]}\nerror %s in %s\n", hipGetErrorString(err), name);
+                return 2;
+            }
         }
         hipMemcpy(&hst, st, sizeof(Stamp), hipMemcpyDeviceToHost);
         const double cyc = (double)(hst.c1 - hst.c0), ns = (double)(hst.t1 - hst.t0) * 10.0;
