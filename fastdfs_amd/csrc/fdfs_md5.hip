@@ -570,7 +570,10 @@ __global__ __launch_bounds__(128) void md5_pair_kernel(
                 lp[k] = reinterpret_cast<const uint8_t *>(__shfl((uintptr_t)p, src)) + piece * 16;
                 lim[k] = __shfl(nblk, src) * 4;
             }
-            u32x4 RA[NLD], RB[NLD];
+            // Three register sets: round r + 2's loads are issued while round
+            // r is staged and hashed (two rounds of lookahead: under the
+            // batch's 3.6 TB/s a load takes longer than one round).
+            u32x4 RA[NLD], RB[NLD], RC[NLD];
             auto issue = [&](u32x4 (&R)[NLD], uint64_t r) {
                 const uint64_t rp = r * PIECES + piece;
 #pragma unroll
@@ -579,12 +582,12 @@ __global__ __launch_bounds__(128) void md5_pair_kernel(
                     asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(R[k]) : "v"(a) : "memory");
                 }
             };
-            // R is the older of the two sets in flight.  The wait is taken on
-            // every path through the loop body (only the staging is
+            // R is the oldest of the three sets in flight.  The wait is taken
+            // on every path through the loop body (only the staging is
             // conditional), so no path reaches the next issue into R's
             // registers with R's loads still in flight (tests/test_isa.py).
             auto wait_older = [&](u32x4 (&R)[NLD]) {
-                asm volatile("s_waitcnt vmcnt(8)" : "+v"(R[0]), "+v"(R[1]), "+v"(R[2]), "+v"(R[3]) :: "memory");
+                asm volatile("s_waitcnt vmcnt(16)" : "+v"(R[0]), "+v"(R[1]), "+v"(R[2]), "+v"(R[3]) :: "memory");
                 asm volatile("" : "+v"(R[4]), "+v"(R[5]), "+v"(R[6]), "+v"(R[7]));
             };
             auto stage = [&](u32x4 (&R)[NLD], uint8_t *tile) {
@@ -619,27 +622,36 @@ __global__ __launch_bounds__(128) void md5_pair_kernel(
                     }
                 zin = 0;  // taken by round 0
             };
-            issue(RA, 0);
-            for (uint64_t r = 0; r < rounds; r += 2) {
-                if ((r & 255) == 0)
-                    prio_by_remaining(rounds - r);
-                issue(RB, r + 1);
-                wait_older(RA);
-                stage(RA, sbuf[0]);
+            // round r's rows go to sbuf[r & 1] (the MD5 wave reads them there)
+            auto round = [&](u32x4 (&R)[NLD], uint64_t r) {
+                uint8_t *tile = sbuf[r & 1];
+                stage(R, tile);
                 pair_barrier();
-                crc_round(r, sbuf[0]);
-                issue(RA, r + 2);
+                crc_round(r, tile);
+            };
+            issue(RA, 0);
+            issue(RB, 1);
+            for (uint64_t r = 0; r < rounds; r += 3) {
+                if ((r & 255) < 3)  // every 256 rounds
+                    prio_by_remaining(rounds - r);
+                issue(RC, r + 2);
+                wait_older(RA);
+                round(RA, r);
+                issue(RA, r + 3);
                 wait_older(RB);
-                if (r + 1 < rounds) {
-                    stage(RB, sbuf[1]);
-                    pair_barrier();
-                    crc_round(r + 1, sbuf[1]);
-                }
+                if (r + 1 < rounds)
+                    round(RB, r + 1);
+                issue(RB, r + 4);
+                wait_older(RC);
+                if (r + 2 < rounds)
+                    round(RC, r + 2);
             }
-            // the last (past-the-end) set
+            // the last (past-the-end) sets
             asm volatile("s_waitcnt vmcnt(0)"
                          : "+v"(RA[0]), "+v"(RA[1]), "+v"(RA[2]), "+v"(RA[3]), "+v"(RA[4]), "+v"(RA[5]),
                            "+v"(RA[6]), "+v"(RA[7]) :: "memory");
+            asm volatile("" : "+v"(RB[0]), "+v"(RB[1]), "+v"(RB[2]), "+v"(RB[3]), "+v"(RB[4]), "+v"(RB[5]),
+                         "+v"(RB[6]), "+v"(RB[7]) :: "memory");
             if (valid && small) {
                 if (nblk > 0) {
                     // the last 32 dwords in position order: an odd block
