@@ -102,7 +102,7 @@ __device__ __forceinline__ void elf_byte(uint32_t b, uint32_t &e, uint32_t &y)
 
 template <bool SAR>
 __device__ __forceinline__ void elf_chain_wg(const uint8_t *p, uint64_t L, uint32_t f, uint32_t *ring,
-                                             uint8_t *sig_out, int32_t *codes_out)
+                                             uint8_t *sig_out, int32_t *codes_out, fdfs_gpu_file_state *fs)
 {
     const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
     const uint64_t nslots = uniform64((L + kElfSlot - 1) / kElfSlot);
@@ -145,7 +145,9 @@ __device__ __forceinline__ void elf_chain_wg(const uint8_t *p, uint64_t L, uint3
     // v_readfirstlane per step)
     uint32_t z;
     asm volatile("v_mov_b32 %0, 0" : "=v"(z));
-    uint32_t e = z, y = 0x80000000u;  // INIT_HASH_CODES4's 0; y < 0: exact as it stands
+    // INIT_HASH_CODES4's 0, or the chunk's state (fdfs_gpu_update_batch);
+    // y < 0: exact as it stands
+    uint32_t e = z ^ (fs ? (uint32_t)fs->hash_codes[1] : 0u), y = 0x80000000u;
     __syncthreads();
     for (uint64_t s = 0; s < nslots; s++) {
         const uint4 *R = reinterpret_cast<const uint4 *>(ring + (s & 1) * kElfSlot);
@@ -189,6 +191,17 @@ __device__ __forceinline__ void elf_chain_wg(const uint8_t *p, uint64_t L, uint3
         __syncthreads();
     }
     e = elf_exact_after(e, y);
+    if (fs) {  // the state-carrying update: ELF and the byte count (the CRC and
+               // polynomials come from big_patch_state_kernel)
+        if (lane == 0) {
+            fs->hash_codes[1] = (int32_t)e;
+            uint32_t cnt[2] = {fs->md5_count[0], fs->md5_count[1]};
+            count_add(cnt, L);
+            fs->md5_count[0] = cnt[0];
+            fs->md5_count[1] = cnt[1];
+        }
+        return;
+    }
     if (lane == 0) {
         if (sig_out) {  // be64 size at 0, be32 ELF at 12 (big_patch_kernel writes the CRC, simple, Time33)
             uint32_t *sp = reinterpret_cast<uint32_t *>(sig_out + 24ull * f);
@@ -247,14 +260,15 @@ __global__ __launch_bounds__(kHashBlock) __attribute__((amdgpu_waves_per_eu(1)))
     // The first chain_slots workgroups: big file i < *nbig (when *nbig <=
     // chain_slots) on workgroup i (elf_chain_wg); the lanes skip those files.
     uint32_t nchain = 0;
-    if (!ST && chain_slots) {
+    if (chain_slots) {
         const uint32_t nb = __builtin_amdgcn_readfirstlane(*nbig_p);
         nchain = nb <= chain_slots ? nb : 0;
         if (blockIdx.x < chain_slots) {
             if (blockIdx.x < nchain) {
                 const uint32_t fc = order[blockIdx.x];
                 if (fc < n)  // else a stale order entry (flagged by big_plan_kernel)
-                    elf_chain_wg<SAR>(base + offs[fc], sizes[fc], fc, sD, sig_out, codes_out);
+                    elf_chain_wg<SAR>(base + offs[fc], sizes[fc], fc, sD, sig_out, codes_out,
+                                      ST ? states + (sidx ? sidx[fc] : fc) : nullptr);
             }
             return;
         }
@@ -869,7 +883,7 @@ hipError_t launch_sig_hash(bool sar, const uint8_t *base, const uint64_t *offs,
                            hipStream_t st, const uint32_t *nbig, uint32_t chain_cap)
 {
     // the chain workgroups first: as many as there can be big files
-    const uint32_t slots = (states || !nbig || !big_min) ? 0u : (n < chain_cap ? n : chain_cap);
+    const uint32_t slots = (!nbig || !big_min) ? 0u : (n < chain_cap ? n : chain_cap);
     const unsigned grid = slots + (n + kHashBlock - 1) / kHashBlock;
 #define HASH_LAUNCH(S, T)                                                                                \
     sig_hash_kernel<S, T><<<grid, kHashBlock, 0, st>>>(base, offs, sizes, order, n, tabs, big_min, crc_out, \
