@@ -42,6 +42,196 @@ __device__ __forceinline__ void md5_finish(uint32_t st[4], const uint8_t *tp, ui
     md5_pad_compress(st, m, r, (uint32_t)bits, (uint32_t)(bits >> 32));
 }
 
+// ------------------------------------------- MD5 path, one workgroup per file
+//
+// A batch's few big files (at most chain_cap of them: config 4's 1 GiB
+// files) are each one serial chain, on one lane of one wave alone on its
+// SIMD, and such a wave issues about one instruction per 4 cycles: every
+// instruction it issues is time on the chain.  md5_compress spends five per
+// step, one of them the a + m + K sum off the chain.  Here a helper wave makes
+// those sums: its lane i computes K[i] + m[g(i)] of each block (g the RFC 1321
+// message index of step i), a slot ahead of the MD5 wave (two slots of 32
+// blocks in the tables' 16 KiB of LDS), which then runs four dependent
+// instructions per step
+// (md5_round_km) and reads each round's 16 sums one round ahead of its use.
+// 16.8 against 21.2 cycles per byte on one wave (profiles/r06/
+// chain_lds_ubench.json).  Every lane of the MD5 wave runs the same chain
+// (the LDS reads broadcast); lane 0 stores.  The file's CRC comes from
+// crc_seg_kernel (big_patch_kernel), as for any big file.
+static __device__ const uint32_t kMd5Kc[64] = {
+    0xd76aa478u, 0xe8c7b756u, 0x242070dbu, 0xc1bdceeeu, 0xf57c0fafu, 0x4787c62au, 0xa8304613u, 0xfd469501u,
+    0x698098d8u, 0x8b44f7afu, 0xffff5bb1u, 0x895cd7beu, 0x6b901122u, 0xfd987193u, 0xa679438eu, 0x49b40821u,
+    0xf61e2562u, 0xc040b340u, 0x265e5a51u, 0xe9b6c7aau, 0xd62f105du, 0x02441453u, 0xd8a1e681u, 0xe7d3fbc8u,
+    0x21e1cde6u, 0xc33707d6u, 0xf4d50d87u, 0x455a14edu, 0xa9e3e905u, 0xfcefa3f8u, 0x676f02d9u, 0x8d2a4c8au,
+    0xfffa3942u, 0x8771f681u, 0x6d9d6122u, 0xfde5380cu, 0xa4beea44u, 0x4bdecfa9u, 0xf6bb4b60u, 0xbebfbc70u,
+    0x289b7ec6u, 0xeaa127fau, 0xd4ef3085u, 0x04881d05u, 0xd9d4d039u, 0xe6db99e5u, 0x1fa27cf8u, 0xc4ac5665u,
+    0xf4292244u, 0x432aff97u, 0xab9423a7u, 0xfc93a039u, 0x655b59c3u, 0x8f0ccc92u, 0xffeff47du, 0x85845dd1u,
+    0x6fa87e4fu, 0xfe2ce6e0u, 0xa3014314u, 0x4e0811a1u, 0xf7537e82u, 0xbd3af235u, 0x2ad7d2bbu, 0xeb86d391u};
+
+__device__ __forceinline__ int md5_msg_index(int i)  // g(i), RFC 1321 3.4
+{
+    return i < 16 ? i : i < 32 ? (5 * i + 1) & 15 : i < 48 ? (3 * i + 5) & 15 : (7 * i) & 15;
+}
+
+constexpr uint32_t kChainSlotBlocks = 32;  // blocks per LDS slot: 32 x 64 sums = 8 KiB
+
+// ring: two slots, 16 KiB of the workgroup's LDS.  Every wave of the
+// workgroup calls it: wave 0 runs the chain, wave 1 makes the sums, any
+// others only keep the barrier count.  fs != nullptr: the state-carrying
+// update (fdfs_gpu_update_batch): the chunk continues fs's MD5 -- the bytes
+// my_md5_update left pending are completed first from the chunk's head, the
+// chunk's last bytes become the new pending buffer, and the byte count
+// advances (the CRC comes from big_patch_state_kernel).
+__device__ __forceinline__ void md5_chain_wg(const uint8_t *p, uint64_t L, uint32_t f, int wv, uint4 *ring,
+                                          uint8_t *sig_out, int32_t *codes_out, fdfs_gpu_file_state *fs)
+{
+    const int lane = threadIdx.x & 63;
+    const uint32_t have = fs ? (fs->md5_count[0] >> 3) & 63u : 0u;  // bytes pending in fs's buffer
+    const uint64_t pre = have ? (64 - have < L ? 64 - have : L) : 0;  // chunk bytes that complete them
+    const uint8_t *s0 = p + pre;  // the stream of whole blocks
+    const uint64_t nblk = (L - pre) >> 6;
+    const uint64_t nslots = uniform64((nblk + kChainSlotBlocks - 1) / kChainSlotBlocks);
+    if (wv == 1) {
+        const uint32_t kk = kMd5Kc[lane];
+        const uint8_t *src = s0 + 4 * md5_msg_index(lane);
+        auto fill = [&](uint4 *slot, uint64_t s) {
+            const uint64_t b0 = s * kChainSlotBlocks;
+            const uint32_t nb = (uint32_t)uniform64(nblk - b0 < kChainSlotBlocks ? nblk - b0 : kChainSlotBlocks);
+            uint32_t *w = reinterpret_cast<uint32_t *>(slot);
+            for (uint32_t j0 = 0; j0 < nb; j0 += 16) {
+                uint32_t v[16];
+#pragma unroll
+                for (int u = 0; u < 16; u++) {
+                    const uint64_t blk = b0 + j0 + u < nblk ? b0 + j0 + u : b0;  // past the end: re-read block b0
+                    __builtin_memcpy(&v[u], src + 64 * blk, 4);  // any alignment (unaligned memory mode)
+                }
+#pragma unroll
+                for (int u = 0; u < 16; u++)
+                    w[(j0 + u) * 64 + lane] = v[u] + kk;
+            }
+        };
+        if (nslots)
+            fill(ring, 0);
+        __syncthreads();
+        for (uint64_t s = 0; s < nslots; s++) {
+            if (s + 1 < nslots)
+                fill(ring + ((s + 1) & 1) * (kChainSlotBlocks * 16), s + 1);
+            __syncthreads();
+        }
+        return;
+    }
+    if (wv != 0) {
+        __syncthreads();
+        for (uint64_t s = 0; s < nslots; s++)
+            __syncthreads();
+        return;
+    }
+    __builtin_amdgcn_s_setprio(3);
+    uint32_t st[4] = {0x67452301u, 0xefcdab89u, 0x98badcfeu, 0x10325476u};  // my_md5_init
+    if (fs) {
+#pragma unroll
+        for (int k = 0; k < 4; k++)
+            st[k] = fs->md5_state[k];
+        if (have && have + pre == 64) {  // my_md5_update's partial block: buffer || chunk head
+            uint32_t m[16];
+#pragma unroll
+            for (int wd = 0; wd < 16; wd++) {
+                uint32_t word = 0;
+#pragma unroll
+                for (int q = 0; q < 4; q++) {
+                    const uint32_t k = 4 * wd + q;
+                    word |= (uint32_t)(k < have ? fs->md5_buffer[k] : p[k - have]) << (8 * q);
+                }
+                m[wd] = word;
+            }
+            md5_compress(st, m);
+        }
+    }
+    // Every lane holds the same state, which hipcc would otherwise keep in
+    // SGPRs (the LDS reads are wave-uniform) and run on the scalar unit with a
+    // v_readfirstlane per step; an opaque per-lane zero keeps it in VGPRs.
+    uint32_t z;
+    asm volatile("v_mov_b32 %0, 0" : "=v"(z));
+#pragma unroll
+    for (int k = 0; k < 4; k++)
+        st[k] ^= z;
+    __syncthreads();
+    for (uint64_t s = 0; s < nslots; s++) {
+        const uint4 *R = ring + (s & 1) * (kChainSlotBlocks * 16);
+        const uint32_t nb = (uint32_t)uniform64(nblk - s * kChainSlotBlocks < kChainSlotBlocks
+                                                    ? nblk - s * kChainSlotBlocks : kChainSlotBlocks);
+        uint4 ga[4], gb[4];
+#pragma unroll
+        for (int k = 0; k < 4; k++)
+            ga[k] = R[k];
+        for (uint32_t j = 0; j < nb; j++) {
+            const uint4 *B = R + 16 * j;
+            const uint4 *N = R + (j + 1 < nb ? 16 * (j + 1) : 0);  // the next block's first round
+            uint32_t a = st[0], b = st[1], c = st[2], d = st[3];
+            // each round's sums are read while the round before is computed
+#pragma unroll
+            for (int k = 0; k < 4; k++)
+                gb[k] = B[4 + k];
+            __builtin_amdgcn_sched_barrier(0);
+            md5_round_km<0>(a, b, c, d, ga);
+            __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+            for (int k = 0; k < 4; k++)
+                ga[k] = B[8 + k];
+            __builtin_amdgcn_sched_barrier(0);
+            md5_round_km<1>(a, b, c, d, gb);
+            __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+            for (int k = 0; k < 4; k++)
+                gb[k] = B[12 + k];
+            __builtin_amdgcn_sched_barrier(0);
+            md5_round_km<2>(a, b, c, d, ga);
+            __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+            for (int k = 0; k < 4; k++)
+                ga[k] = N[k];
+            __builtin_amdgcn_sched_barrier(0);
+            md5_round_km<3>(a, b, c, d, gb);
+            __builtin_amdgcn_sched_barrier(0);
+            st[0] += a;
+            st[1] += b;
+            st[2] += c;
+            st[3] += d;
+        }
+        __syncthreads();
+    }
+    const uint8_t *tp = s0 + (nblk << 6);
+    if (fs) {
+        if (lane == 0) {
+            // the new pending bytes: the chunk appended to a still-partial
+            // buffer, or the chunk's last (L - pre) & 63 bytes
+            const uint32_t r = (uint32_t)((L - pre) & 63u);
+            if (have && have + L < 64) {
+                for (uint32_t k = 0; k < (uint32_t)L; k++)
+                    fs->md5_buffer[have + k] = p[k];
+            } else {
+                for (uint32_t k = 0; k < r; k++)
+                    fs->md5_buffer[k] = tp[k];
+            }
+#pragma unroll
+            for (int k = 0; k < 4; k++)
+                fs->md5_state[k] = st[k];
+            uint32_t cnt[2] = {fs->md5_count[0], fs->md5_count[1]};
+            count_add(cnt, L);
+            fs->md5_count[0] = cnt[0];
+            fs->md5_count[1] = cnt[1];
+        }
+        return;
+    }
+    md5_finish(st, tp, L);
+    if (lane == 0) {
+        if (sig_out)  // memcpy(sig + 8, md5 digest, 16) (storage/storage_service.c:119)
+            store_sig(sig_out + 24ull * f, L, st[0], st[1], st[2], st[3]);
+        if (codes_out)
+            reinterpret_cast<int4 *>(codes_out)[f] = make_int4((int)st[0], (int)st[1], (int)st[2], (int)st[3]);
+    }
+}
+
 // ------------------------------------------------ MD5 path, staged loads
 //
 // MD5 is serial per file, so it stays one LANE per file, but the bytes do not
@@ -92,7 +282,8 @@ __global__ __launch_bounds__(64 * kMd5Waves) void md5_stage_kernel(
     const DevTables *__restrict__ tabs, const uint64_t *__restrict__ big_min_p, uint32_t w1,
     uint32_t *__restrict__ queue,
     uint32_t *__restrict__ crc_out, uint8_t *__restrict__ sig_out, int32_t *__restrict__ codes_out,
-    fdfs_gpu_file_state *__restrict__ states, const uint32_t *__restrict__ sidx)
+    fdfs_gpu_file_state *__restrict__ states, const uint32_t *__restrict__ sidx,
+    const uint32_t *__restrict__ nbig_p, uint32_t chain_slots)
 {
     constexpr int CH = kMd5Chunk;
     constexpr int PIECES = CH / 16;   // 16-byte pieces of one file's chunk
@@ -101,7 +292,7 @@ __global__ __launch_bounds__(64 * kMd5Waves) void md5_stage_kernel(
     constexpr int STRIDE = CH + 16;   // padded LDS row per file
     constexpr int BPR = CH / 64;      // MD5 blocks per round
     static_assert(NLD == 8, "the asm waits below name 8 registers");
-    __shared__ uint32_t sD[16 * 256];
+    __shared__ __attribute__((aligned(16))) uint32_t sD[16 * 256];  // also md5_chain_wg's ring
     __shared__ uint32_t sT[256];
     __shared__ __attribute__((aligned(16))) uint8_t sbuf[kMd5Waves][64 * STRIDE];
     lds_fill(sD, &tabs->t.D[0][0], 16 * 256);
@@ -129,6 +320,23 @@ __global__ __launch_bounds__(64 * kMd5Waves) void md5_stage_kernel(
     const uint8_t *safe = reinterpret_cast<const uint8_t *>(tabs);  // >= 16 readable bytes
     const uint32_t K16 = tabs->t.K16;
     const uint64_t big_min = big_min_p ? *big_min_p : ~0ull;
+    // With a queue: the first chain_slots workgroups run big file i < *nbig
+    // (when *nbig <= chain_slots) alone (md5_chain_wg), the waves skip those.
+    uint32_t nchain = 0;
+    if (queue && chain_slots) {
+        const uint32_t nb = __builtin_amdgcn_readfirstlane(*nbig_p);
+        nchain = nb <= chain_slots ? nb : 0;
+        if (blockIdx.x < chain_slots) {
+            if (blockIdx.x < nchain) {
+                const uint32_t fc = order[blockIdx.x];
+                if (fc < n)  // else a stale order entry (flagged by big_plan_kernel)
+                    md5_chain_wg(base + offs[fc], sizes[fc], fc, __builtin_amdgcn_readfirstlane(threadIdx.x >> 6),
+                                 reinterpret_cast<uint4 *>(sD), sig_out, codes_out,
+                                 ST ? states + (sidx ? sidx[fc] : fc) : nullptr);
+            }
+            return;
+        }
+    }
     uint32_t chunk;
     if (queue) {
         uint32_t c0 = 0;
@@ -150,6 +358,8 @@ __global__ __launch_bounds__(64 * kMd5Waves) void md5_stage_kernel(
         valid = false;
         f = 0;
     }
+    if (nchain && valid && sizes[f] >= big_min)  // a chain workgroup's file
+        valid = false;
     const uint64_t L = valid ? sizes[f] : 0;
     const uint8_t *p = valid ? base + offs[f] : safe;
     const bool small = L < big_min;  // else the CRC comes from crc_seg_kernel
@@ -355,136 +565,6 @@ __device__ __forceinline__ void pair_barrier()
     asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
 }
 
-// ------------------------------------------- MD5 path, one workgroup per file
-//
-// A batch's few big files (at most chain_cap of them: config 4's 1 GiB
-// files) are each one serial chain, on one lane of one wave alone on its
-// SIMD, and such a wave issues about one instruction per 4 cycles: every
-// instruction it issues is time on the chain.  md5_compress spends five per
-// step, one of them the a + m + K sum off the chain.  Here a helper wave makes
-// those sums: its lane i computes K[i] + m[g(i)] of each block (g the RFC 1321
-// message index of step i), a slot ahead of the MD5 wave (two slots of 32
-// blocks in the tables' 16 KiB of LDS), which then runs four dependent
-// instructions per step
-// (md5_round_km) and reads each round's 16 sums one round ahead of its use.
-// 16.8 against 21.2 cycles per byte on one wave (profiles/r06/
-// chain_lds_ubench.json).  Every lane of the MD5 wave runs the same chain
-// (the LDS reads broadcast); lane 0 stores.  The file's CRC comes from
-// crc_seg_kernel (big_patch_kernel), as for any big file.
-static __device__ const uint32_t kMd5Kc[64] = {
-    0xd76aa478u, 0xe8c7b756u, 0x242070dbu, 0xc1bdceeeu, 0xf57c0fafu, 0x4787c62au, 0xa8304613u, 0xfd469501u,
-    0x698098d8u, 0x8b44f7afu, 0xffff5bb1u, 0x895cd7beu, 0x6b901122u, 0xfd987193u, 0xa679438eu, 0x49b40821u,
-    0xf61e2562u, 0xc040b340u, 0x265e5a51u, 0xe9b6c7aau, 0xd62f105du, 0x02441453u, 0xd8a1e681u, 0xe7d3fbc8u,
-    0x21e1cde6u, 0xc33707d6u, 0xf4d50d87u, 0x455a14edu, 0xa9e3e905u, 0xfcefa3f8u, 0x676f02d9u, 0x8d2a4c8au,
-    0xfffa3942u, 0x8771f681u, 0x6d9d6122u, 0xfde5380cu, 0xa4beea44u, 0x4bdecfa9u, 0xf6bb4b60u, 0xbebfbc70u,
-    0x289b7ec6u, 0xeaa127fau, 0xd4ef3085u, 0x04881d05u, 0xd9d4d039u, 0xe6db99e5u, 0x1fa27cf8u, 0xc4ac5665u,
-    0xf4292244u, 0x432aff97u, 0xab9423a7u, 0xfc93a039u, 0x655b59c3u, 0x8f0ccc92u, 0xffeff47du, 0x85845dd1u,
-    0x6fa87e4fu, 0xfe2ce6e0u, 0xa3014314u, 0x4e0811a1u, 0xf7537e82u, 0xbd3af235u, 0x2ad7d2bbu, 0xeb86d391u};
-
-__device__ __forceinline__ int md5_msg_index(int i)  // g(i), RFC 1321 3.4
-{
-    return i < 16 ? i : i < 32 ? (5 * i + 1) & 15 : i < 48 ? (3 * i + 5) & 15 : (7 * i) & 15;
-}
-
-constexpr uint32_t kChainSlotBlocks = 32;  // blocks per LDS slot: 32 x 64 sums = 8 KiB
-
-// ring: two slots, 16 KiB of the workgroup's LDS.  Both waves call it.
-__device__ __forceinline__ void md5_chain_wg(const uint8_t *p, uint64_t L, uint32_t f, bool helper, uint4 *ring,
-                                          uint8_t *sig_out, int32_t *codes_out)
-{
-    const int lane = threadIdx.x & 63;
-    const uint64_t nblk = L >> 6;
-    const uint64_t nslots = uniform64((nblk + kChainSlotBlocks - 1) / kChainSlotBlocks);
-    if (helper) {
-        const uint32_t kk = kMd5Kc[lane];
-        const uint8_t *src = p + 4 * md5_msg_index(lane);
-        auto fill = [&](uint4 *slot, uint64_t s) {
-            const uint64_t b0 = s * kChainSlotBlocks;
-            const uint32_t nb = (uint32_t)uniform64(nblk - b0 < kChainSlotBlocks ? nblk - b0 : kChainSlotBlocks);
-            uint32_t *w = reinterpret_cast<uint32_t *>(slot);
-            for (uint32_t j0 = 0; j0 < nb; j0 += 16) {
-                uint32_t v[16];
-#pragma unroll
-                for (int u = 0; u < 16; u++) {
-                    const uint64_t blk = b0 + j0 + u < nblk ? b0 + j0 + u : b0;  // past the end: re-read block b0
-                    __builtin_memcpy(&v[u], src + 64 * blk, 4);  // any alignment (unaligned memory mode)
-                }
-#pragma unroll
-                for (int u = 0; u < 16; u++)
-                    w[(j0 + u) * 64 + lane] = v[u] + kk;
-            }
-        };
-        if (nslots)
-            fill(ring, 0);
-        __syncthreads();
-        for (uint64_t s = 0; s < nslots; s++) {
-            if (s + 1 < nslots)
-                fill(ring + ((s + 1) & 1) * (kChainSlotBlocks * 16), s + 1);
-            __syncthreads();
-        }
-        return;
-    }
-    __builtin_amdgcn_s_setprio(3);
-    // Every lane holds the same state, which hipcc would otherwise keep in
-    // SGPRs (the LDS reads are wave-uniform) and run on the scalar unit with a
-    // v_readfirstlane per step; an opaque per-lane zero keeps it in VGPRs.
-    uint32_t z;
-    asm volatile("v_mov_b32 %0, 0" : "=v"(z));
-    uint32_t st[4] = {0x67452301u ^ z, 0xefcdab89u ^ z, 0x98badcfeu ^ z, 0x10325476u ^ z};  // my_md5_init
-    __syncthreads();
-    for (uint64_t s = 0; s < nslots; s++) {
-        const uint4 *R = ring + (s & 1) * (kChainSlotBlocks * 16);
-        const uint32_t nb = (uint32_t)uniform64(nblk - s * kChainSlotBlocks < kChainSlotBlocks
-                                                    ? nblk - s * kChainSlotBlocks : kChainSlotBlocks);
-        uint4 ga[4], gb[4];
-#pragma unroll
-        for (int k = 0; k < 4; k++)
-            ga[k] = R[k];
-        for (uint32_t j = 0; j < nb; j++) {
-            const uint4 *B = R + 16 * j;
-            const uint4 *N = R + (j + 1 < nb ? 16 * (j + 1) : 0);  // the next block's first round
-            uint32_t a = st[0], b = st[1], c = st[2], d = st[3];
-            // each round's sums are read while the round before is computed
-#pragma unroll
-            for (int k = 0; k < 4; k++)
-                gb[k] = B[4 + k];
-            __builtin_amdgcn_sched_barrier(0);
-            md5_round_km<0>(a, b, c, d, ga);
-            __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-            for (int k = 0; k < 4; k++)
-                ga[k] = B[8 + k];
-            __builtin_amdgcn_sched_barrier(0);
-            md5_round_km<1>(a, b, c, d, gb);
-            __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-            for (int k = 0; k < 4; k++)
-                gb[k] = B[12 + k];
-            __builtin_amdgcn_sched_barrier(0);
-            md5_round_km<2>(a, b, c, d, ga);
-            __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-            for (int k = 0; k < 4; k++)
-                ga[k] = N[k];
-            __builtin_amdgcn_sched_barrier(0);
-            md5_round_km<3>(a, b, c, d, gb);
-            __builtin_amdgcn_sched_barrier(0);
-            st[0] += a;
-            st[1] += b;
-            st[2] += c;
-            st[3] += d;
-        }
-        __syncthreads();
-    }
-    md5_finish(st, p + (nblk << 6), L);
-    if (lane == 0) {
-        if (sig_out)  // memcpy(sig + 8, md5 digest, 16) (storage/storage_service.c:119)
-            store_sig(sig_out + 24ull * f, L, st[0], st[1], st[2], st[3]);
-        if (codes_out)
-            reinterpret_cast<int4 *>(codes_out)[f] = make_int4((int)st[0], (int)st[1], (int)st[2], (int)st[3]);
-    }
-}
-
 template <bool SAR>
 __global__ __launch_bounds__(128) void md5_pair_kernel(
     const uint8_t *__restrict__ base, const uint64_t *__restrict__ offs,
@@ -528,7 +608,8 @@ __global__ __launch_bounds__(128) void md5_pair_kernel(
         const uint32_t f = order[blockIdx.x];
         if (f >= n)  // a stale order entry (flagged by big_plan_kernel)
             return;
-        md5_chain_wg(base + offs[f], sizes[f], f, loader, reinterpret_cast<uint4 *>(sD), sig_out, codes_out);
+        md5_chain_wg(base + offs[f], sizes[f], f, loader ? 1 : 0, reinterpret_cast<uint4 *>(sD), sig_out, codes_out,
+                     nullptr);
         return;
     }
     for (;;) {
@@ -741,12 +822,17 @@ hipError_t launch_md5_stage(bool sar, const uint8_t *base, const uint64_t *offs,
         return hipGetLastError();
     }
     unsigned grid = (n + kBlk - 1) / kBlk;
-    if (queue)  // queue zeroed by the caller (launch_sig_lane's workspace memset)
+    uint32_t slots = 0;
+    if (queue) {  // queue zeroed by the caller (launch_sig_lane's workspace memset)
         grid = ncu < (nw + kMd5Waves - 1) / kMd5Waves ? ncu : (nw + kMd5Waves - 1) / kMd5Waves;
+        if (nbig && big_min)  // the chain workgroups first: as many as there can be big files
+            slots = n < chain_cap ? n : chain_cap;
+        grid += slots;
+    }
     const uint32_t w1 = ncu * kMd5Waves;
 #define MD5_LAUNCH(S, T)                                                                                  \
     md5_stage_kernel<S, T><<<grid, kBlk, 0, st>>>(base, offs, sizes, order, n, tabs, big_min, w1, queue, \
-                                                  crc_out, sig_out, codes_out, states, sidx)
+                                                  crc_out, sig_out, codes_out, states, sidx, nbig, slots)
     if (states)
         sar ? MD5_LAUNCH(true, true) : MD5_LAUNCH(false, true);
     else

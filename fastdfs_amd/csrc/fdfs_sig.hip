@@ -884,12 +884,12 @@ hipError_t launch_sig_lane(bool sar, int method, const uint8_t *base, const uint
     const uint64_t *bmin = offload ? big->big_min : nullptr;
     if (ev0 && method != 0)
         (void)hipEventRecord(ev0, st);
-    // HASH batches, one-shot or chunked (big files >= T: big_plan_kernel's
-    // adaptive T up to lat_files files, kBigCrcMin above), and one-shot MD5
-    // batches small enough to offload (n <= lat_files): when there are at
-    // most one big file per CU, each runs its serial chain (ELF / MD5) on a
+    // HASH batches (big files >= T: big_plan_kernel's adaptive T up to
+    // lat_files files, kBigCrcMin above) and MD5 batches small enough to
+    // offload (n <= lat_files), one-shot or chunked: when there are at most
+    // one big file per CU, each runs its serial chain (ELF / MD5) on a
     // workgroup of its own
-    const bool chains = offload && (method == 1 || (method == 2 && !states && n <= big->lat_files));
+    const bool chains = offload && (method == 1 || (method == 2 && n <= big->lat_files));
     e = (method == 2)   ? launch_md5_stage(sar, base, offs, sizes, n, order, tabs, bmin, hist + 2 * kSizeBins,
                                            crc_out, sig_out, codes_out, states, sidx, big ? big->ncu : 0, st,
                                            chains ? big->nbig : nullptr, chains ? big->ncu : 0u)

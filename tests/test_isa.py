@@ -39,7 +39,7 @@ def test_shipped_kernels_carry_no_probe_code(isa):
     gidx mode): no probe-mode parameter is left in a shipped name.  Round 4
     made md5_pair_kernel's longest-remaining-first issue priority production
     (prio_by_remaining); round 6's chain workgroups (md5_chain_wg
-    in md5_pair_kernel, elf_chain_wg in sig_hash_kernel) raise
+    in md5_pair_kernel and md5_stage_kernel, elf_chain_wg in sig_hash_kernel) raise
     their chain wave's: those are the only shipped kernels that change
     their priority."""
     names = isa["names"]
@@ -51,7 +51,8 @@ def test_shipped_kernels_carry_no_probe_code(isa):
                for k in names if "crc_seg_kernel" in k)
     assert isa["setprio"], "the pair kernel's priority policy is missing"
     assert any("md5_pair_kernel" in k for k in isa["setprio"]), isa["setprio"]
-    assert all("md5_pair_kernel" in k or "sig_hash_kernel" in k for k in isa["setprio"]), isa["setprio"]
+    assert all(any(m in k for m in ("md5_pair_kernel", "md5_stage_kernel", "sig_hash_kernel"))
+               for k in isa["setprio"]), isa["setprio"]
     # measured-and-not-kept variants of rounds 1-4 are gone from the product
     for probe in ("sig_split_kernel", "tail_plan_kernel", "dp_tile_kernelILb", "dp_split_kernelILi1024ELb"):
         assert not any(probe in k for k in names), probe
