@@ -72,9 +72,11 @@ hipError_t launch_crc_seg(bool sar, const uint8_t *base, const uint64_t *offs, c
                           uint32_t n, uint64_t *nseg, uint64_t *seg_first, uint64_t *bsum,
                           const DevTables *tabs, uint32_t *crc_out, unsigned ncu, hipStream_t st,
                           hipEvent_t ev0, hipEvent_t ev1);
-// chain_cap > 0 (one-shot batches of at most lat_files files, big files
-// offloaded): when big_plan_kernel's *nbig is at most chain_cap, each big
-// file's MD5 runs on a workgroup of its own (md5_chain_wg, fdfs_md5.hip).
+// chain_cap > 0 (batches with big files offloaded): when big_plan_kernel's
+// *nbig is at most chain_cap / 4 (one per CU), each big file's MD5 runs on a
+// workgroup of its own (md5_chain_wg, fdfs_md5.hip), up to chain_cap (one
+// per SIMD) on a wave of its own (md5_chain_wave).  launch_sig_hash: up to
+// chain_cap (one per CU) ELF chains on workgroups of their own.
 hipError_t launch_md5_stage(bool sar, const uint8_t *base, const uint64_t *offs,
                             const uint64_t *sizes, uint32_t n, const uint32_t *order,
                             const DevTables *tabs, const uint64_t *big_min, uint32_t *queue, uint32_t *crc_out,

@@ -232,6 +232,172 @@ __device__ __forceinline__ void md5_chain_wg(const uint8_t *p, uint64_t L, uint3
     }
 }
 
+// The same chain on one wave with no helper (md5_chain_wave): lane i makes
+// step i's sums of each 8-block slot two slots ahead into the wave's own LDS
+// ring (~1 % of the chain's instructions), so four chains fit a CU, one per
+// SIMD.  Used when a batch has more big files than CUs and at most one per
+// SIMD; with at most one per CU the helper form above is faster (18 % on
+// config 4 --method md5, profiles/r06/chain_wave_ab.txt).
+constexpr uint32_t kWaveSlotBlocks = 8;  // blocks per LDS slot: 8 x 64 sums = 2 KiB
+
+// ring: two slots, 4 KiB of LDS, this wave's own.  fs != nullptr: the
+// state-carrying update (fdfs_gpu_update_batch): the chunk continues fs's
+// MD5 -- the bytes my_md5_update left pending are completed first from the
+// chunk's head, the chunk's last bytes become the new pending buffer, and the
+// byte count advances (the CRC comes from big_patch_state_kernel).
+__device__ __forceinline__ void md5_chain_wave(const uint8_t *p, uint64_t L, uint32_t f, uint4 *ring,
+                                            uint8_t *sig_out, int32_t *codes_out, fdfs_gpu_file_state *fs)
+{
+    const int lane = threadIdx.x & 63;
+    const uint32_t have = fs ? (fs->md5_count[0] >> 3) & 63u : 0u;  // bytes pending in fs's buffer
+    const uint64_t pre = have ? (64 - have < L ? 64 - have : L) : 0;  // chunk bytes that complete them
+    const uint8_t *s0 = p + pre;  // the stream of whole blocks
+    const uint64_t nblk = (L - pre) >> 6;
+    const uint64_t nslots = uniform64((nblk + kWaveSlotBlocks - 1) / kWaveSlotBlocks);
+    const uint32_t kk = kMd5Kc[lane];
+    const uint8_t *src = s0 + 4 * md5_msg_index(lane);
+    // slot s: lane i holds m[g(i)] of its blocks (past the end the last
+    // block's, never hashed; the loads are unconditional, see elf_chain_wave)
+    auto load = [&](uint32_t (&v)[kWaveSlotBlocks], uint64_t s) {
+        const uint64_t b0 = s * kWaveSlotBlocks;
+#pragma unroll
+        for (int j = 0; j < (int)kWaveSlotBlocks; j++) {
+            const uint64_t blk = b0 + j < nblk ? b0 + j : nblk - 1;  // nblk > 0 whenever called
+            __builtin_memcpy(&v[j], src + 64 * blk, 4);  // any alignment (unaligned memory mode)
+        }
+    };
+    auto put = [&](const uint32_t (&v)[kWaveSlotBlocks], uint64_t s) {
+        uint32_t *w = reinterpret_cast<uint32_t *>(ring + (s & 1) * (kWaveSlotBlocks * 16));
+#pragma unroll
+        for (int j = 0; j < (int)kWaveSlotBlocks; j++)
+            w[64 * j + lane] = v[j] + kk;
+    };
+    __builtin_amdgcn_s_setprio(3);
+    uint32_t st[4] = {0x67452301u, 0xefcdab89u, 0x98badcfeu, 0x10325476u};  // my_md5_init
+    if (fs) {
+#pragma unroll
+        for (int k = 0; k < 4; k++)
+            st[k] = fs->md5_state[k];
+        if (have && have + pre == 64) {  // my_md5_update's partial block: buffer || chunk head
+            uint32_t m[16];
+#pragma unroll
+            for (int wd = 0; wd < 16; wd++) {
+                uint32_t word = 0;
+#pragma unroll
+                for (int q = 0; q < 4; q++) {
+                    const uint32_t k = 4 * wd + q;
+                    word |= (uint32_t)(k < have ? fs->md5_buffer[k] : p[k - have]) << (8 * q);
+                }
+                m[wd] = word;
+            }
+            md5_compress(st, m);
+        }
+    }
+    // Every lane holds the same state, which hipcc would otherwise keep in
+    // SGPRs (the LDS reads are wave-uniform) and run on the scalar unit with a
+    // v_readfirstlane per step; an opaque per-lane zero keeps it in VGPRs.
+    uint32_t z;
+    asm volatile("v_mov_b32 %0, 0" : "=v"(z));
+#pragma unroll
+    for (int k = 0; k < 4; k++)
+        st[k] ^= z;
+    auto chain = [&](uint64_t s) {
+        const uint4 *R = ring + (s & 1) * (kWaveSlotBlocks * 16);
+        const uint32_t nb = (uint32_t)uniform64(nblk - s * kWaveSlotBlocks < kWaveSlotBlocks
+                                                    ? nblk - s * kWaveSlotBlocks : kWaveSlotBlocks);
+        uint4 ga[4], gb[4];
+#pragma unroll
+        for (int k = 0; k < 4; k++)
+            ga[k] = R[k];
+        for (uint32_t j = 0; j < nb; j++) {
+            const uint4 *B = R + 16 * j;
+            const uint4 *N = R + (j + 1 < nb ? 16 * (j + 1) : 0);  // the next block's first round
+            uint32_t a = st[0], b = st[1], c = st[2], d = st[3];
+            // each round's sums are read while the round before is computed
+#pragma unroll
+            for (int k = 0; k < 4; k++)
+                gb[k] = B[4 + k];
+            __builtin_amdgcn_sched_barrier(0);
+            md5_round_km<0>(a, b, c, d, ga);
+            __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+            for (int k = 0; k < 4; k++)
+                ga[k] = B[8 + k];
+            __builtin_amdgcn_sched_barrier(0);
+            md5_round_km<1>(a, b, c, d, gb);
+            __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+            for (int k = 0; k < 4; k++)
+                gb[k] = B[12 + k];
+            __builtin_amdgcn_sched_barrier(0);
+            md5_round_km<2>(a, b, c, d, ga);
+            __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+            for (int k = 0; k < 4; k++)
+                ga[k] = N[k];
+            __builtin_amdgcn_sched_barrier(0);
+            md5_round_km<3>(a, b, c, d, gb);
+            __builtin_amdgcn_sched_barrier(0);
+            st[0] += a;
+            st[1] += b;
+            st[2] += c;
+            st[3] += d;
+        }
+    };
+    // slot s + 1 goes into the ring and slot s + 2's loads go out before slot
+    // s's chain (the ring's other slot was read by the chain before; one
+    // wave's LDS operations run in order)
+    uint32_t va[kWaveSlotBlocks], vb[kWaveSlotBlocks];
+    if (nslots) {
+        load(va, 0);
+        put(va, 0);
+        load(va, 1);
+    }
+    uint64_t s = 0;
+    for (; s + 2 <= nslots; s += 2) {
+        load(vb, s + 2);
+        put(va, s + 1);
+        chain(s);
+        load(va, s + 3);
+        put(vb, s + 2);
+        chain(s + 1);
+    }
+    if (s < nslots) {
+        put(va, s + 1);  // past the end: never read
+        chain(s);
+    }
+    const uint8_t *tp = s0 + (nblk << 6);
+    if (fs) {
+        if (lane == 0) {
+            // the new pending bytes: the chunk appended to a still-partial
+            // buffer, or the chunk's last (L - pre) & 63 bytes
+            const uint32_t r = (uint32_t)((L - pre) & 63u);
+            if (have && have + L < 64) {
+                for (uint32_t k = 0; k < (uint32_t)L; k++)
+                    fs->md5_buffer[have + k] = p[k];
+            } else {
+                for (uint32_t k = 0; k < r; k++)
+                    fs->md5_buffer[k] = tp[k];
+            }
+#pragma unroll
+            for (int k = 0; k < 4; k++)
+                fs->md5_state[k] = st[k];
+            uint32_t cnt[2] = {fs->md5_count[0], fs->md5_count[1]};
+            count_add(cnt, L);
+            fs->md5_count[0] = cnt[0];
+            fs->md5_count[1] = cnt[1];
+        }
+        return;
+    }
+    md5_finish(st, tp, L);
+    if (lane == 0) {
+        if (sig_out)  // memcpy(sig + 8, md5 digest, 16) (storage/storage_service.c:119)
+            store_sig(sig_out + 24ull * f, L, st[0], st[1], st[2], st[3]);
+        if (codes_out)
+            reinterpret_cast<int4 *>(codes_out)[f] = make_int4((int)st[0], (int)st[1], (int)st[2], (int)st[3]);
+    }
+}
+
 // ------------------------------------------------ MD5 path, staged loads
 //
 // MD5 is serial per file, so it stays one LANE per file, but the bytes do not
@@ -283,7 +449,7 @@ __global__ __launch_bounds__(64 * kMd5Waves) void md5_stage_kernel(
     uint32_t *__restrict__ queue,
     uint32_t *__restrict__ crc_out, uint8_t *__restrict__ sig_out, int32_t *__restrict__ codes_out,
     fdfs_gpu_file_state *__restrict__ states, const uint32_t *__restrict__ sidx,
-    const uint32_t *__restrict__ nbig_p, uint32_t chain_slots)
+    const uint32_t *__restrict__ nbig_p, uint32_t chain_wg, uint32_t chain_wave)
 {
     constexpr int CH = kMd5Chunk;
     constexpr int PIECES = CH / 16;   // 16-byte pieces of one file's chunk
@@ -320,19 +486,35 @@ __global__ __launch_bounds__(64 * kMd5Waves) void md5_stage_kernel(
     const uint8_t *safe = reinterpret_cast<const uint8_t *>(tabs);  // >= 16 readable bytes
     const uint32_t K16 = tabs->t.K16;
     const uint64_t big_min = big_min_p ? *big_min_p : ~0ull;
-    // With a queue: the first chain_slots workgroups run big file i < *nbig
-    // (when *nbig <= chain_slots) alone (md5_chain_wg), the waves skip those.
+    // With a queue, the first chain workgroups: with *nbig <= chain_wg big
+    // files (at most one per CU) big file i runs on workgroup i
+    // (md5_chain_wg, a helper wave beside it), with up to chain_wave (one per
+    // SIMD) on wave i (md5_chain_wave); the waves of the queue skip them.
     uint32_t nchain = 0;
-    if (queue && chain_slots) {
+    if (queue && chain_wave) {
+        const uint32_t wpb = blockDim.x >> 6;
+        uint32_t cwgs = (chain_wave + wpb - 1) / wpb;
+        cwgs = cwgs > chain_wg ? cwgs : chain_wg;
         const uint32_t nb = __builtin_amdgcn_readfirstlane(*nbig_p);
-        nchain = nb <= chain_slots ? nb : 0;
-        if (blockIdx.x < chain_slots) {
-            if (blockIdx.x < nchain) {
-                const uint32_t fc = order[blockIdx.x];
-                if (fc < n)  // else a stale order entry (flagged by big_plan_kernel)
-                    md5_chain_wg(base + offs[fc], sizes[fc], fc, __builtin_amdgcn_readfirstlane(threadIdx.x >> 6),
-                                 reinterpret_cast<uint4 *>(sD), sig_out, codes_out,
-                                 ST ? states + (sidx ? sidx[fc] : fc) : nullptr);
+        nchain = nb <= chain_wave ? nb : 0;
+        if (blockIdx.x < cwgs) {
+            const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+            if (nchain <= chain_wg) {
+                if (blockIdx.x < nchain) {
+                    const uint32_t fc = order[blockIdx.x];
+                    if (fc < n)  // else a stale order entry (flagged by big_plan_kernel)
+                        md5_chain_wg(base + offs[fc], sizes[fc], fc, wv, reinterpret_cast<uint4 *>(sD), sig_out,
+                                     codes_out, ST ? states + (sidx ? sidx[fc] : fc) : nullptr);
+                }
+            } else {
+                const uint32_t id = blockIdx.x * wpb + wv;
+                if (id < nchain) {
+                    const uint32_t fc = order[id];
+                    if (fc < n)
+                        md5_chain_wave(base + offs[fc], sizes[fc], fc,
+                                       reinterpret_cast<uint4 *>(sD) + wv * (2 * kWaveSlotBlocks * 16), sig_out,
+                                       codes_out, ST ? states + (sidx ? sidx[fc] : fc) : nullptr);
+                }
             }
             return;
         }
@@ -571,7 +753,7 @@ __global__ __launch_bounds__(128) void md5_pair_kernel(
     const uint64_t *__restrict__ sizes, const uint32_t *__restrict__ order, uint32_t n,
     const DevTables *__restrict__ tabs, const uint64_t *__restrict__ big_min_p, uint32_t *__restrict__ queue,
     uint32_t *__restrict__ crc_out, uint8_t *__restrict__ sig_out, int32_t *__restrict__ codes_out,
-    const uint32_t *__restrict__ nbig_p, uint32_t chain_cap)
+    const uint32_t *__restrict__ nbig_p, uint32_t chain_wg, uint32_t chain_wave)
 {
     constexpr int CH = kMd5Chunk;
     constexpr int PIECES = CH / 16;
@@ -595,22 +777,38 @@ __global__ __launch_bounds__(128) void md5_pair_kernel(
     const uint8_t *safe = reinterpret_cast<const uint8_t *>(tabs);
     const uint32_t K16 = tabs->t.K16;
     const uint64_t big_min = big_min_p ? *big_min_p : ~0ull;
-    // Big files (the first *nbig of the order) of a batch with at most
-    // chain_cap of them: workgroup i < nchain runs big file i's MD5 alone
-    // (md5_chain_wg; the tables' LDS is its ring), and the
-    // pairs skip those files.
+    // Big files (the first *nbig of the order): with *nbig <= chain_wg (at
+    // most one per CU) big file i runs on workgroup i (md5_chain_wg, the
+    // loader wave its helper), with up to chain_wave (one per SIMD) on wave i
+    // (md5_chain_wave); the tables' LDS is the rings, and the pairs skip
+    // those files.
     uint32_t nchain = 0;
-    if (chain_cap && nbig_p) {
+    if (chain_wave && nbig_p) {
+        uint32_t cwgs = (chain_wave + 1) / 2;
+        cwgs = cwgs > chain_wg ? cwgs : chain_wg;
         const uint32_t nb = __builtin_amdgcn_readfirstlane(*nbig_p);
-        nchain = nb <= chain_cap ? nb : 0;
-    }
-    if (blockIdx.x < nchain) {
-        const uint32_t f = order[blockIdx.x];
-        if (f >= n)  // a stale order entry (flagged by big_plan_kernel)
+        nchain = nb <= chain_wave ? nb : 0;
+        if (blockIdx.x < cwgs) {
+            const uint32_t wv = loader ? 1u : 0u;
+            if (nchain <= chain_wg) {
+                if (blockIdx.x < nchain) {
+                    const uint32_t fc = order[blockIdx.x];
+                    if (fc < n)  // else a stale order entry (flagged by big_plan_kernel)
+                        md5_chain_wg(base + offs[fc], sizes[fc], fc, (int)wv, reinterpret_cast<uint4 *>(sD),
+                                     sig_out, codes_out, nullptr);
+                }
+            } else {
+                const uint32_t id = blockIdx.x * 2 + wv;
+                if (id < nchain) {
+                    const uint32_t fc = order[id];
+                    if (fc < n)
+                        md5_chain_wave(base + offs[fc], sizes[fc], fc,
+                                       reinterpret_cast<uint4 *>(sD) + wv * (2 * kWaveSlotBlocks * 16), sig_out,
+                                       codes_out, nullptr);
+                }
+            }
             return;
-        md5_chain_wg(base + offs[f], sizes[f], f, loader ? 1 : 0, reinterpret_cast<uint4 *>(sD), sig_out, codes_out,
-                     nullptr);
-        return;
+        }
     }
     for (;;) {
         if (threadIdx.x == 64)
@@ -808,31 +1006,37 @@ hipError_t launch_md5_stage(bool sar, const uint8_t *base, const uint64_t *offs,
     const uint32_t nw = (n + 63) / 64;
     if (queue && !states) {  // one-shot batches: the wave pairs (queue zeroed by the caller)
         const unsigned g = 4u * ncu;
-        // the pairs' grid, after the chain workgroups (as many as there can
-        // be big files; those past *nbig join the pairs)
+        // the chain workgroups (one per big file up to one per CU, or a
+        // wave per big file up to one per SIMD), then the pairs' grid
         if (!nbig || !big_min)
             chain_cap = 0;
-        const unsigned grid2 = (g < nw ? g : nw) + (n < chain_cap ? n : chain_cap);
+        const uint32_t wv_cap = n < chain_cap ? n : chain_cap;
+        const uint32_t wg_cap = wv_cap < chain_cap / 4 ? wv_cap : chain_cap / 4;
+        const uint32_t cw = (wv_cap + 1) / 2;
+        const unsigned grid2 = (cw > wg_cap ? cw : wg_cap) + (g < nw ? g : nw);
         if (sar)
             md5_pair_kernel<true><<<grid2, 128, 0, st>>>(base, offs, sizes, order, n, tabs, big_min, queue, crc_out,
-                                                         sig_out, codes_out, nbig, chain_cap);
+                                                         sig_out, codes_out, nbig, wg_cap, wv_cap);
         else
             md5_pair_kernel<false><<<grid2, 128, 0, st>>>(base, offs, sizes, order, n, tabs, big_min, queue, crc_out,
-                                                          sig_out, codes_out, nbig, chain_cap);
+                                                          sig_out, codes_out, nbig, wg_cap, wv_cap);
         return hipGetLastError();
     }
     unsigned grid = (n + kBlk - 1) / kBlk;
-    uint32_t slots = 0;
+    uint32_t wv_cap = 0, wg_cap = 0;
     if (queue) {  // queue zeroed by the caller (launch_sig_lane's workspace memset)
         grid = ncu < (nw + kMd5Waves - 1) / kMd5Waves ? ncu : (nw + kMd5Waves - 1) / kMd5Waves;
-        if (nbig && big_min)  // the chain workgroups first: as many as there can be big files
-            slots = n < chain_cap ? n : chain_cap;
-        grid += slots;
+        if (nbig && big_min) {  // the chain workgroups first
+            wv_cap = n < chain_cap ? n : chain_cap;
+            wg_cap = wv_cap < chain_cap / 4 ? wv_cap : chain_cap / 4;
+        }
+        const uint32_t cw = (wv_cap + kMd5Waves - 1) / kMd5Waves;
+        grid += cw > wg_cap ? cw : wg_cap;
     }
     const uint32_t w1 = ncu * kMd5Waves;
 #define MD5_LAUNCH(S, T)                                                                                  \
     md5_stage_kernel<S, T><<<grid, kBlk, 0, st>>>(base, offs, sizes, order, n, tabs, big_min, w1, queue, \
-                                                  crc_out, sig_out, codes_out, states, sidx, nbig, slots)
+                                                  crc_out, sig_out, codes_out, states, sidx, nbig, wg_cap, wv_cap)
     if (states)
         sar ? MD5_LAUNCH(true, true) : MD5_LAUNCH(false, true);
     else

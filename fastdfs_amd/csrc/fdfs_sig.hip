@@ -887,12 +887,15 @@ hipError_t launch_sig_lane(bool sar, int method, const uint8_t *base, const uint
     // HASH batches (big files >= T: big_plan_kernel's adaptive T up to
     // lat_files files, kBigCrcMin above) and MD5 batches small enough to
     // offload (n <= lat_files), one-shot or chunked: when there are at most
-    // one big file per CU, each runs its serial chain (ELF / MD5) on a
-    // workgroup of its own
+    // one big file per CU each runs its serial chain (ELF / MD5) on a
+    // workgroup of its own; MD5 up to one per SIMD on a wave of its own (the
+    // ELF form of that, probes/extra/chain_wave.patch, gains 6 % at 1,024
+    // uploads per call and is kept out of sig_hash_kernel, the headline
+    // kernel: profiles/r06/chain_wave_ab.txt)
     const bool chains = offload && (method == 1 || (method == 2 && n <= big->lat_files));
     e = (method == 2)   ? launch_md5_stage(sar, base, offs, sizes, n, order, tabs, bmin, hist + 2 * kSizeBins,
                                            crc_out, sig_out, codes_out, states, sidx, big ? big->ncu : 0, st,
-                                           chains ? big->nbig : nullptr, chains ? big->ncu : 0u)
+                                           chains ? big->nbig : nullptr, chains ? 4 * big->ncu : 0u)
         : (method == 1) ? launch_sig_hash(sar, base, offs, sizes, n, order, tabs, bmin, crc_out, sig_out,
                                           codes_out, states, sidx, st, chains ? big->nbig : nullptr,
                                           chains ? big->ncu : 0u)

@@ -228,6 +228,21 @@ def test_chain_workgroups(oracle, ctxs, variant):
     _check(oracle, ctxs[variant], variant, buf, offs, sz, methods=(1, 2))
 
 
+@pytest.mark.parametrize("variant", [0, 1])
+def test_chain_waves(oracle, ctxs, variant):
+    """More big files than CUs, at most one per SIMD: each big file's MD5
+    chain on a wave of its own that feeds its own LDS ring (md5_chain_wave,
+    8-block slots loaded two slots ahead; HASH keeps these files' ELF chains
+    on the lanes), byte-aligned starts, odd sizes, beside small files.
+    Reference: storage/storage_dio.c:465-512."""
+    rng = np.random.default_rng(81 + variant)
+    sizes = np.concatenate([rng.integers(1 << 20, 2 << 20, 500), rng.integers(0, 5000, 300),
+                            [(1 << 20) + 511, (1 << 20) + 512, (1 << 20) + 513]]).astype(np.int64)
+    rng.shuffle(sizes)
+    buf, offs, sz = _packed(sizes, 1, rng)
+    _check(oracle, ctxs[variant], variant, buf, offs, sz, methods=(1, 2))
+
+
 def test_crc_paths_agree_at_scale(oracle, ctxs):
     """Config 2 at full size, the batch bench.py hashes on rank 0 (1M files of
     U[4, 64] KiB, sizes seed 1, bytes seed 2, 16-byte aligned: ~34.8 GB in
