@@ -10,6 +10,7 @@
 #include "../../fastdfs_amd/csrc/fdfs_md5.hip"
 
 #include <cstdio>
+#include <cstdlib>
 
 using namespace fdfs;
 
@@ -33,11 +34,11 @@ __global__ __launch_bounds__(64 * W) void k_wave(const uint8_t *src, uint8_t *si
                    nullptr);
 }
 
-int main()
+int main(int argc, char **argv)
 {
     int ncu = 0;
     hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, 0);
-    const int nfiles = ncu;
+    const int nfiles = argc > 1 ? atoi(argv[1]) : ncu;  // chains (a multiple of 4)
     uint8_t *src, *sig;
     hipMalloc(&src, kFileBytes * nfiles);
     hipMalloc(&sig, 24 * nfiles);
@@ -45,7 +46,8 @@ int main()
     hipEvent_t e0, e1;
     hipEventCreate(&e0);
     hipEventCreate(&e1);
-    printf("{\"cus\": %d, \"file_bytes\": %llu, \"runs\": [\n", ncu, (unsigned long long)kFileBytes);
+    printf("{\"cus\": %d, \"chains\": %d, \"file_bytes\": %llu, \"runs\": [\n", ncu, nfiles,
+           (unsigned long long)kFileBytes);
     const char *names[] = {"wg_helper", "wave_x1", "wave_x2", "wave_x4", "wg_helper"};
     for (int v = 0; v < 5; v++) {
         float best = 1e30f;
